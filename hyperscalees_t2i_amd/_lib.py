@@ -1,0 +1,79 @@
+"""ctypes binding of libeggroll.so — the C-ABI declared in include/eggroll.h.
+
+The product path has NO CPU / PyTorch fallback: if the HIP library is missing or a call
+fails, an exception is raised.  Build it with `python -m hyperscalees_t2i_amd.build_ext`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "_build" / "libeggroll.so"
+HEADER = _PKG.parent / "include" / "eggroll.h"
+
+i32, i64, u32, u64, f32 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
+vp = C.c_void_p
+
+# name -> (restype, argtypes); mirrors include/eggroll.h exactly (checked by tests)
+SIGNATURES = {
+    "eggroll_version": (C.c_char_p, []),
+    "eggroll_last_error": (C.c_char_p, []),
+    "eggroll_noise_factors": (C.c_int, [u64, i64, i64, i64, i64, vp, vp]),
+    "eggroll_philox_words": (C.c_int, [u64, i64, i64, vp, vp]),
+    "eggroll_perturb": (C.c_int, [vp, vp, i64, i64, vp, i32, i64, i64, i32, i32, i32, i64, i64, f32, vp, i64, vp]),
+    "eggroll_fitness": (C.c_int, [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "eggroll_update_workspace_bytes": (i64, [i64]),
+    "eggroll_update": (C.c_int, [vp, vp, i64, i64, vp, vp, i32, i32, vp, i32, i64, i64, i32, f32, f32, f32, vp, vp,
+                                 vp]),
+    "eggroll_lora_linear_pop": (C.c_int, [vp, i64, vp, i64, vp, vp, i64, i64, i64, i32, f32, i64, i64, i64, i64, vp,
+                                          i64, vp, vp]),
+    "eggroll_lora_project": (C.c_int, [vp, i64, vp, i64, i64, i32, i64, i64, i64, vp, vp]),
+    "eggroll_lora_expand": (C.c_int, [vp, vp, i64, i64, i32, f32, i64, i64, i64, vp, i64, vp]),
+}
+
+_lib = None
+
+
+class EggrollError(RuntimeError):
+    pass
+
+
+def header_symbols() -> list:
+    """Function names declared in include/eggroll.h."""
+    txt = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(eggroll_[a-z0-9_]+)\s*\(", txt)))
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = Path(os.environ.get("EGGROLL_LIB", LIB_PATH))
+    if not path.exists():
+        raise EggrollError(
+            f"libeggroll.so not found at {path}: build it with `python -m hyperscalees_t2i_amd.build_ext` "
+            "(there is no CPU fallback)")
+    lib = C.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().eggroll_last_error().decode(errors="replace")
+        raise EggrollError(f"{what} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def version() -> str:
+    return load().eggroll_version().decode()

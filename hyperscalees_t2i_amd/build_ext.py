@@ -1,0 +1,62 @@
+"""Build libeggroll.so (HIP, gfx950) in-tree with plain hipcc — no torch in the C-ABI.
+
+`python -m hyperscalees_t2i_amd.build_ext` (also run by `__graft_entry__.build()`).
+The library lands in hyperscalees_t2i_amd/_build/ so it travels with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "_build"
+LIB = BUILD / "libeggroll.so"
+SOURCES = ["eggroll_es.hip", "eggroll_lora.hip"]
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build libeggroll)")
+
+
+def _stale() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    deps = [CSRC / s for s in SOURCES] + [CSRC / "common.h", ROOT / "include" / "eggroll.h"]
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    if not force and not _stale():
+        return LIB
+    BUILD.mkdir(parents=True, exist_ok=True)
+    objs = []
+    for s in SOURCES:
+        obj = BUILD / (Path(s).stem + ".o")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
+               "-Wall", "-Wno-unused-function", f"-I{ROOT / 'include'}", str(CSRC / s), "-o", str(obj)]
+        if verbose:
+            print("[build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(str(obj))
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)]
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)
+    print(LIB)

@@ -1,0 +1,73 @@
+// Shared helpers for libeggroll (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/eggroll.h"
+
+namespace eggroll {
+
+void set_error(const char* fmt, ...);
+
+#define EGG_CHECK_ARG(cond, ...)                 \
+    do {                                         \
+        if (!(cond)) {                           \
+            ::eggroll::set_error(__VA_ARGS__);   \
+            return EGGROLL_ERR_ARG;              \
+        }                                        \
+    } while (0)
+
+#define EGG_CHECK_LAUNCH(what)                                                        \
+    do {                                                                              \
+        hipError_t e_ = hipGetLastError();                                            \
+        if (e_ != hipSuccess) {                                                       \
+            ::eggroll::set_error("%s: launch failed: %s", what, hipGetErrorString(e_)); \
+            return EGGROLL_ERR_LAUNCH;                                                \
+        }                                                                             \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- wave (64-lane) reductions -------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---- Philox4x32-10 (Salmon et al., SC'11; Random123 constants) ----------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+__host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
+        const uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+        u32x4 n;
+        n.x = hi1 ^ c.y ^ k0;
+        n.y = lo1;
+        n.z = hi0 ^ c.w ^ k1;
+        n.w = lo0;
+        c = n;
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+constexpr uint32_t kNoiseTag = 0xE6606011u;
+
+}  // namespace eggroll

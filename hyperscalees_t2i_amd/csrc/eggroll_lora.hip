@@ -1,0 +1,355 @@
+// libeggroll — (2) population-batched perturbed LoRA linear for gfx950 (MI355X).
+//
+// Replaces, for all members of one rank at once, the reference's per-member
+//   unflatten_to_params(theta + sigma*eps[k])  (unifed_es.py:160-161, utills.py:155-162)
+//   PEFT lora.Linear: y = x W^T + bias + (alpha/r) * (x A_k^T) B_k^T   (es_backend.py:193-200)
+// Rows of X are stacked member-major, so the frozen base weight W streams through LDS once
+// per M-tile for every member instead of once per member-forward.
+//
+//   k_lora_project : T[row, q] = X[row,:] . A_k[q,:]   (fp32; HBM-bound X read)
+//   k_lora_gemm    : Y = X W^T (bf16 MFMA 16x16x32, 128x128x64 tiles, global_load_lds staging,
+//                    XOR-swizzled LDS, 2-stage pipeline) with the epilogue
+//                    + bias[n] + scale * sum_q T[row,q] * B_k[n,q]
+//   k_lora_expand  : Y += scale * T B_k^T  (for hosts that run the base GEMM elsewhere)
+#include "common.h"
+
+namespace eggroll {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) {
+    return __uint_as_float(((uint32_t)h) << 16);
+}
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {  // RNE, NaN-preserving cast
+    __bf16 b = (__bf16)f;
+    return *reinterpret_cast<unsigned short*>(&b);
+}
+
+// ------------------------------------------------------------------------------------
+// T = X A_k^T : one wave per row, 16-byte X loads, fp32 accumulate, wave reduction.
+// ------------------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256) void k_lora_project(const unsigned short* __restrict__ X, int64_t ldx,
+                                                      const float* __restrict__ theta_pop, int64_t ld_theta,
+                                                      int64_t offA, int64_t rows_per_member, int64_t M, int64_t K,
+                                                      float* __restrict__ T) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int64_t kl = row / rows_per_member;
+    const float* A = theta_pop + kl * ld_theta + offA;
+    const unsigned short* x = X + row * ldx;
+    float acc[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) acc[q] = 0.0f;
+    for (int64_t c = lane * 8; c < K; c += 64 * 8) {
+        const u16x8 xv = *reinterpret_cast<const u16x8*>(x + c);
+        float xf[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) xf[t] = bf16_to_f32(xv[t]);
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float4 a0 = *reinterpret_cast<const float4*>(A + q * K + c);
+            const float4 a1 = *reinterpret_cast<const float4*>(A + q * K + c + 4);
+            acc[q] += xf[0] * a0.x + xf[1] * a0.y + xf[2] * a0.z + xf[3] * a0.w + xf[4] * a1.x + xf[5] * a1.y +
+                      xf[6] * a1.z + xf[7] * a1.w;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const float v = wave_sum(acc[q]);
+        if (lane == 0) T[row * R + q] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Base GEMM + fused LoRA epilogue.
+// ------------------------------------------------------------------------------------
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;             // 16 KiB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;         // A + B
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;          // 2 stages = 64 KiB
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+// Stage one 128x64 bf16 tile (rows of a K-contiguous matrix) into LDS.  LDS image: row r at
+// byte 128*r; 16-B slot s' of row r holds global chunk s' ^ (r & 7)  (conflict-free b128
+// fragment reads).  Each wave issues 4 global_load_lds_dwordx4 (1 KiB = 8 rows each).
+__device__ __forceinline__ void stage_tile(const unsigned short* __restrict__ G, int64_t ld, int64_t row0,
+                                           int64_t row_max, int64_t k0, char* lds_tile, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int R0 = (wave * 4 + i) * 8;
+        const int r = R0 + (lane >> 3);
+        const int slot = lane & 7;
+        const int chunk = slot ^ (r & 7);
+        int64_t gr = row0 + r;
+        gr = gr < row_max ? gr : row_max;  // clamp: rows past the end are never stored
+        const unsigned short* src = G + gr * ld + k0 + chunk * 8;
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds_tile + R0 * 128), 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int chunk) {
+    return *reinterpret_cast<const bf16x8*>(lds_tile + row * 128 + ((chunk ^ (row & 7)) << 4));
+}
+
+template <int R>
+__global__ __launch_bounds__(256, 2) void k_lora_gemm(const unsigned short* __restrict__ X, int64_t ldx,
+                                                      const unsigned short* __restrict__ W, int64_t ldw,
+                                                      const unsigned short* __restrict__ bias,
+                                                      const float* __restrict__ T,
+                                                      const float* __restrict__ theta_pop, int64_t ld_theta,
+                                                      int64_t offB, float scale, int rows_per_member,
+                                                      int M, int N, int64_t K, int tiles_n,
+                                                      unsigned short* __restrict__ Y, int64_t ldy) {
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-aware bijective remap: consecutive tile ids (sharing X rows) land on one XCD.
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+    const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (int)(K / BK);
+    stage_tile(X, ldx, m0, M - 1, 0, smem, wave, lane);
+    stage_tile(W, ldw, n0, N - 1, 0, smem + TILE_BYTES, wave, lane);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* cur = smem + (kt & 1) * STAGE_BYTES;
+        if (kt + 1 < nk) {
+            char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+            stage_tile(X, ldx, m0, M - 1, (int64_t)(kt + 1) * BK, nxt, wave, lane);
+            stage_tile(W, ldw, n0, N - 1, (int64_t)(kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + (lane >> 4);
+            bf16x8 a[4], b[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) a[f] = read_frag(cur, wm * 64 + f * 16 + (lane & 15), ch);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) b[f] = read_frag(cur + TILE_BYTES, wn * 64 + f * 16 + (lane & 15), ch);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: + bias[n] + scale * T[row,:] . B_k[n,:]  ->  bf16 via LDS, 16-B stores ----
+    const int col_l = lane & 15, rq = (lane >> 4) * 4;
+    float bv[4];
+    int colv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + col_l;
+        colv[j] = col < N ? col : N - 1;
+        bv[j] = bias ? bf16_to_f32(bias[colv[j]]) : 0.0f;
+    }
+    if constexpr (R > 0) {
+        const int first = m0 / rows_per_member;
+        const int last_row = (m0 + BM - 1 < M ? m0 + BM - 1 : M - 1);
+        const bool one_member = (last_row / rows_per_member) == first;
+        float bk[4][R];
+        if (one_member) {
+            const float* Bk = theta_pop + (int64_t)first * ld_theta + offB;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int qq = 0; qq < R; ++qq) bk[j][qq] = Bk[colv[j] * R + qq];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                int row = m0 + wm * 64 + i * 16 + rq + e;
+                row = row < M ? row : M - 1;
+                float t[R];
+#pragma unroll
+                for (int qq = 0; qq < R; ++qq) t[qq] = T[(int64_t)row * R + qq];
+                if (!one_member) {
+                    const float* Bk = theta_pop + (int64_t)(row / rows_per_member) * ld_theta + offB;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int qq = 0; qq < R; ++qq) bk[j][qq] = Bk[colv[j] * R + qq];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float d = 0.0f;
+#pragma unroll
+                    for (int qq = 0; qq < R; ++qq) d += t[qq] * bk[j][qq];
+                    acc[i][j][e] += bv[j] + scale * d;
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i][j][e] += bv[j];
+    }
+    // stage this wave's 64x64 bf16 sub-tile in LDS (128-B rows, 16-B slots XOR-swizzled by row)
+    char* ctile = smem + wave * (64 * 128);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int rr = i * 16 + rq + e;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int cc = j * 16 + col_l;  // element column within the wave tile
+                const int slot = (cc >> 3) ^ (rr & 7);
+                *reinterpret_cast<unsigned short*>(ctile + rr * 128 + slot * 16 + (cc & 7) * 2) = f32_to_bf16(acc[i][j][e]);
+            }
+        }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int rr = it * 8 + (lane >> 3), sl = lane & 7;
+        const int row = m0 + wm * 64 + rr;
+        const int col = n0 + wn * 64 + sl * 8;
+        if (row >= M || col >= N) continue;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * 128 + ((sl ^ (rr & 7)) << 4));
+        unsigned short* dst = Y + (int64_t)row * ldy + col;
+        if (col + 8 <= N && (((uintptr_t)dst) & 15) == 0) {
+            *reinterpret_cast<u16x8*>(dst) = v;
+        } else {
+            for (int u = 0; u < 8 && col + u < N; ++u) dst[u] = v[u];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Y += scale * T B_k^T   (8 bf16 per thread)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_lora_expand(const float* __restrict__ T, const float* __restrict__ theta_pop,
+                                                     int64_t ld_theta, int64_t offB, int r, float scale,
+                                                     int64_t rows_per_member, int64_t M, int64_t N,
+                                                     unsigned short* __restrict__ Y, int64_t ldy) {
+    const int64_t nch = (N + 7) / 8;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= M * nch) return;
+    const int64_t row = idx / nch, c0 = (idx - row * nch) * 8;
+    const int64_t kl = row / rows_per_member;
+    const float* Bk = theta_pop + kl * ld_theta + offB;
+    const float* t = T + row * r;
+    unsigned short* y = Y + row * ldy + c0;
+    for (int u = 0; u < 8 && c0 + u < N; ++u) {
+        float d = 0.0f;
+        for (int qq = 0; qq < r; ++qq) d += t[qq] * Bk[(c0 + u) * r + qq];
+        y[u] = f32_to_bf16(bf16_to_f32(y[u]) + scale * d);
+    }
+}
+
+template <int R>
+static void launch_project(const void* X, int64_t ldx, const float* tp, int64_t ldt, int64_t offA, int64_t rpm,
+                           int64_t M, int64_t K, float* T, hipStream_t st) {
+    hipLaunchKernelGGL(k_lora_project<R>, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st,
+                       (const unsigned short*)X, ldx, tp, ldt, offA, rpm, M, K, T);
+}
+
+static int project(const void* X, int64_t ldx, const float* tp, int64_t ldt, int64_t offA, int32_t r, int64_t rpm,
+                   int64_t M, int64_t K, float* T, hipStream_t st) {
+    switch (r) {
+        case 1: launch_project<1>(X, ldx, tp, ldt, offA, rpm, M, K, T, st); break;
+        case 2: launch_project<2>(X, ldx, tp, ldt, offA, rpm, M, K, T, st); break;
+        case 3: launch_project<3>(X, ldx, tp, ldt, offA, rpm, M, K, T, st); break;
+        case 4: launch_project<4>(X, ldx, tp, ldt, offA, rpm, M, K, T, st); break;
+        case 8: launch_project<8>(X, ldx, tp, ldt, offA, rpm, M, K, T, st); break;
+        case 16: launch_project<16>(X, ldx, tp, ldt, offA, rpm, M, K, T, st); break;
+        default: set_error("lora: r=%d unsupported (1,2,3,4,8,16)", r); return EGGROLL_ERR_UNSUPPORTED;
+    }
+    EGG_CHECK_LAUNCH("lora_project");
+    return EGGROLL_OK;
+}
+
+}  // namespace eggroll
+
+using namespace eggroll;
+
+extern "C" {
+
+int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta, int64_t offA, int32_t r,
+                         int64_t rows_per_member, int64_t M, int64_t K, float* T, void* stream) {
+    EGG_CHECK_ARG(M >= 0 && K > 0 && K % 8 == 0 && ldx % 8 == 0 && ldx >= K, "lora_project: need K%%8==0, ldx%%8==0");
+    EGG_CHECK_ARG(ld_theta % 4 == 0 && offA % 4 == 0, "lora_project: theta offsets must be 16-byte aligned");
+    EGG_CHECK_ARG(rows_per_member > 0, "lora_project: rows_per_member must be > 0");
+    if (M == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(X && theta_pop && T, "lora_project: NULL pointer");
+    return project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T, as_stream(stream));
+}
+
+int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                        int64_t rows_per_member, int64_t M, int64_t N, void* Y, int64_t ldy, void* stream) {
+    EGG_CHECK_ARG(M >= 0 && N > 0 && r >= 1 && r <= 16 && rows_per_member > 0 && ldy >= N, "lora_expand: bad sizes");
+    if (M == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(T && theta_pop && Y, "lora_expand: NULL pointer");
+    const int64_t work = M * ((N + 7) / 8);
+    hipLaunchKernelGGL(k_lora_expand, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, as_stream(stream), T,
+                       theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, (unsigned short*)Y, ldy);
+    EGG_CHECK_LAUNCH("lora_expand");
+    return EGGROLL_OK;
+}
+
+int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                            const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                            float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                            int64_t ldy, float* T_ws, void* stream) {
+    EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0, "lora_linear_pop: bad sizes M=%lld N=%lld K=%lld", (long long)M,
+                  (long long)N, (long long)K);
+    EGG_CHECK_ARG(K % 64 == 0, "lora_linear_pop: K=%lld must be a multiple of 64", (long long)K);
+    EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop: bad strides");
+    EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_linear_pop: r=%d out of range", r);
+    EGG_CHECK_ARG(rows_per_member > 0, "lora_linear_pop: rows_per_member must be > 0");
+    const int64_t tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_linear_pop: grid too large");
+    if (M == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(X && W && Y, "lora_linear_pop: NULL pointer");
+    hipStream_t st = as_stream(stream);
+    if (r > 0) {
+        EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop: theta_pop / T_ws NULL with r > 0");
+        int rc = eggroll_lora_project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T_ws, stream);
+        if (rc) return rc;
+    }
+    EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_linear_pop: M/N too large");
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+#define EGG_GEMM(RV)                                                                                              \
+    hipLaunchKernelGGL(k_lora_gemm<RV>, grid, dim3(256), 0, st, (const unsigned short*)X, ldx,                 \
+                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T_ws, theta_pop, ld_theta,   \
+                       offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy)
+    switch (r) {
+        case 0: EGG_GEMM(0); break;
+        case 1: EGG_GEMM(1); break;
+        case 2: EGG_GEMM(2); break;
+        case 3: EGG_GEMM(3); break;
+        case 4: EGG_GEMM(4); break;
+        case 8: EGG_GEMM(8); break;
+        case 16: EGG_GEMM(16); break;
+        default: set_error("lora_linear_pop: r=%d unsupported (0,1,2,3,4,8,16)", r); return EGGROLL_ERR_UNSUPPORTED;
+    }
+#undef EGG_GEMM
+    EGG_CHECK_LAUNCH("lora_gemm");
+    return EGGROLL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,254 @@
+"""Torch-tensor front end of the libeggroll C-ABI (device memory + streams come from PyTorch).
+
+Every function here launches HIP kernels through include/eggroll.h on the tensor's device and
+the current torch stream; none of them computes anything on the host.  Tensors must live on
+a ROCm device (`cuda:*` in torch) — a CPU tensor raises.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+CHUNK = 1024  # EGGROLL_CHUNK in include/eggroll.h
+
+
+def _dev(t: torch.Tensor, what: str, dtype=None) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise _lib.EggrollError(f"{what}: expected a ROCm device tensor, got "
+                                f"{getattr(t, 'device', type(t))} (no CPU fallback)")
+    if dtype is not None and t.dtype != dtype:
+        raise _lib.EggrollError(f"{what}: expected dtype {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise _lib.EggrollError(f"{what}: tensor must be contiguous")
+    return t
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device: torch.device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+# ---------------------------------------------------------------------------------------
+# theta layout (reference utills.py:141-162: concat of trainable params, row-major)
+# ---------------------------------------------------------------------------------------
+
+
+@dataclass
+class ThetaLayout:
+    """Per-parameter records of the flat theta vector and of one base sample's factors."""
+
+    shapes: List[Tuple[int, ...]]
+    rank: int
+    mats: np.ndarray = field(init=False)      # [n_mats, 6] int64 (eggroll_mat_t)
+    D: int = field(init=False)
+    factor_len: int = field(init=False)
+    factor_ld: int = field(init=False)        # row stride of factor buffers (multiple of 4)
+    total_chunks: int = field(init=False)
+    theta_offsets: List[int] = field(init=False)
+
+    def __post_init__(self):
+        self.shapes = [tuple(int(x) for x in s) for s in self.shapes]
+        if self.rank < 1:
+            raise ValueError("egg rank must be >= 1")
+        recs, offs = [], []
+        toff = foff = coff = 0
+        for s in self.shapes:
+            if len(s) == 2:
+                m, n = s
+                numel, fl = m * n, self.rank * (m + n)
+            else:
+                m, n = int(np.prod(s)), 0
+                numel, fl = m, m
+            recs.append((m, n, toff, foff, coff, 0))
+            offs.append(toff)
+            toff += numel
+            foff += fl
+            coff += -(-numel // CHUNK)
+        self.mats = np.array(recs, dtype=np.int64).reshape(-1, 6)
+        self.D, self.factor_len, self.total_chunks = toff, foff, coff
+        self.factor_ld = -(-foff // 4) * 4
+        self.theta_offsets = offs
+        self._dev_cache: Dict[str, torch.Tensor] = {}
+
+    @property
+    def n_mats(self) -> int:
+        return len(self.shapes)
+
+    def mats_on(self, device) -> torch.Tensor:
+        key = str(torch.device(device))
+        t = self._dev_cache.get(key)
+        if t is None:
+            t = torch.from_numpy(self.mats.copy()).to(device)
+            self._dev_cache[key] = t
+        return t
+
+
+def n_base_samples(pop: int, antithetic: bool) -> int:
+    """reference utills.py:88-89"""
+    return (pop // 2 + pop % 2) if antithetic else pop
+
+
+# ---------------------------------------------------------------------------------------
+# (1) noise factors
+# ---------------------------------------------------------------------------------------
+
+
+def noise_factors(seed: int, n_base: int, layout: ThetaLayout, device, base_lo: int = 0,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    device = torch.device(device)
+    rows = n_base - base_lo
+    if out is None:
+        out = torch.empty((rows, layout.factor_ld), dtype=torch.float32, device=device)
+    _dev(out, "noise_factors(out)", torch.float32)
+    _lib.call("eggroll_noise_factors", int(seed) & 0xFFFFFFFFFFFFFFFF, base_lo, n_base, layout.factor_len,
+              layout.factor_ld, out.data_ptr(), _stream(device))
+    return out
+
+
+def philox_words(seed: int, j: int, n_quads: int, device) -> torch.Tensor:
+    out = torch.empty(4 * n_quads, dtype=torch.int32, device=device)
+    _lib.call("eggroll_philox_words", int(seed), int(j), int(n_quads), out.data_ptr(), _stream(out.device))
+    return out
+
+
+def perturb(theta: Optional[torch.Tensor], factors: torch.Tensor, layout: ThetaLayout, pop: int, antithetic: bool,
+            member_lo: int, member_hi: int, sigma: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """theta_k = theta + sigma * eps_k for k in [member_lo, member_hi) (theta=None: eps rows)."""
+    _dev(factors, "perturb(factors)", torch.float32)
+    device = factors.device
+    if theta is not None:
+        _dev(theta, "perturb(theta)", torch.float32)
+    n = member_hi - member_lo
+    if out is None:
+        out = torch.empty((n, layout.D), dtype=torch.float32, device=device)
+    _dev(out, "perturb(out)", torch.float32)
+    _lib.call("eggroll_perturb", _p(theta), factors.data_ptr(), factors.stride(0), factors.shape[0],
+              layout.mats_on(device).data_ptr(), layout.n_mats, layout.total_chunks, layout.D, layout.rank, pop,
+              int(bool(antithetic)), member_lo, member_hi, float(sigma), out.data_ptr(), out.stride(0),
+              _stream(device))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# (3) fitness
+# ---------------------------------------------------------------------------------------
+
+
+def fitness(S: torch.Tensor, promptnorm: bool) -> Dict[str, torch.Tensor]:
+    """scores/mu/stats/fitness/finite/order of S [n, m] (see include/eggroll.h)."""
+    _dev(S, "fitness(S)", torch.float32)
+    if S.ndim != 2:
+        raise ValueError(f"S must be [n, m], got {tuple(S.shape)}")
+    n, m = S.shape
+    dev = S.device
+    out = {
+        "scores": torch.empty(n, dtype=torch.float32, device=dev),
+        "mu": torch.empty(m, dtype=torch.float32, device=dev),
+        "stats": torch.empty(4, dtype=torch.float32, device=dev),
+        "fitness": torch.empty(n, dtype=torch.float32, device=dev),
+        "finite": torch.empty(n, dtype=torch.int32, device=dev),
+        "order": torch.empty(n, dtype=torch.int32, device=dev),
+    }
+    _lib.call("eggroll_fitness", S.data_ptr(), n, m, int(bool(promptnorm)), out["scores"].data_ptr(),
+              out["mu"].data_ptr(), out["stats"].data_ptr(), out["fitness"].data_ptr(), out["finite"].data_ptr(),
+              out["order"].data_ptr(), _stream(dev))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# (4) update
+# ---------------------------------------------------------------------------------------
+
+
+class UpdateWorkspace:
+    def __init__(self, layout: ThetaLayout, device):
+        nbytes = int(_lib.load().eggroll_update_workspace_bytes(layout.total_chunks))
+        self.buf = torch.empty(-(-nbytes // 16) * 16, dtype=torch.uint8, device=device)
+
+
+def update(theta: torch.Tensor, factors: torch.Tensor, fit: Dict[str, torch.Tensor], layout: ThetaLayout, pop: int,
+           antithetic: bool, lr: float, max_step_norm: float, theta_max_norm: float,
+           out: Optional[torch.Tensor] = None, workspace: Optional[UpdateWorkspace] = None) -> torch.Tensor:
+    """theta' = caps(theta + lr * mean_k f_k eps_k) with lr = lr_scale * sigma (utills.py:131)."""
+    _dev(theta, "update(theta)", torch.float32)
+    _dev(factors, "update(factors)", torch.float32)
+    dev = theta.device
+    if out is None:
+        out = torch.empty_like(theta)
+    if workspace is None:
+        workspace = UpdateWorkspace(layout, dev)
+    _lib.call("eggroll_update", theta.data_ptr(), factors.data_ptr(), factors.stride(0), factors.shape[0],
+              fit["fitness"].data_ptr(), fit["stats"].data_ptr(), pop, int(bool(antithetic)),
+              layout.mats_on(dev).data_ptr(), layout.n_mats, layout.total_chunks, layout.D, layout.rank, float(lr),
+              float(max_step_norm or 0.0), float(theta_max_norm or 0.0), workspace.buf.data_ptr(), out.data_ptr(),
+              _stream(dev))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# (2) population LoRA linear
+# ---------------------------------------------------------------------------------------
+
+
+def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], theta_pop: Optional[torch.Tensor],
+                    offA: int, offB: int, r: int, scale: float, rows_per_member: int,
+                    out: Optional[torch.Tensor] = None, T_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Y = x W^T + bias + scale * (x A_k^T) B_k^T with member k = row // rows_per_member.
+
+    x: [M, K] bf16; W: [N, K] bf16; bias: [N] bf16 or None; theta_pop: [n_members, ld] fp32.
+    r = 0 runs the plain base GEMM (no LoRA term)."""
+    _dev(x, "lora_linear_pop(x)", torch.bfloat16)
+    _dev(W, "lora_linear_pop(W)", torch.bfloat16)
+    M, K = x.shape
+    N = W.shape[0]
+    if W.shape[1] != K:
+        raise ValueError(f"W {tuple(W.shape)} does not match x {tuple(x.shape)}")
+    if bias is not None:
+        _dev(bias, "lora_linear_pop(bias)", torch.bfloat16)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    if r > 0:
+        _dev(theta_pop, "lora_linear_pop(theta_pop)", torch.float32)
+        n_members = -(-M // rows_per_member)
+        if theta_pop.shape[0] < n_members:
+            raise ValueError(f"theta_pop has {theta_pop.shape[0]} members, rows need {n_members}")
+        if T_ws is None or T_ws.numel() < M * r:
+            T_ws = torch.empty(M * r, dtype=torch.float32, device=x.device)
+        ld_t = theta_pop.stride(0)
+    else:
+        ld_t = 0
+    _lib.call("eggroll_lora_linear_pop", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
+              _p(theta_pop) if r > 0 else None, ld_t, offA, offB, r, float(scale), rows_per_member, M, N, K,
+              out.data_ptr(), out.stride(0), _p(T_ws) if r > 0 else None, _stream(x.device))
+    return out
+
+
+def lora_project(x: torch.Tensor, theta_pop: torch.Tensor, offA: int, r: int, rows_per_member: int,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(x, "lora_project(x)", torch.bfloat16)
+    _dev(theta_pop, "lora_project(theta_pop)", torch.float32)
+    M, K = x.shape
+    if out is None:
+        out = torch.empty((M, r), dtype=torch.float32, device=x.device)
+    _lib.call("eggroll_lora_project", x.data_ptr(), x.stride(0), theta_pop.data_ptr(), theta_pop.stride(0), offA, r,
+              rows_per_member, M, K, out.data_ptr(), _stream(x.device))
+    return out
+
+
+def lora_expand(T: torch.Tensor, theta_pop: torch.Tensor, offB: int, r: int, scale: float, rows_per_member: int,
+                y: torch.Tensor) -> torch.Tensor:
+    _dev(T, "lora_expand(T)", torch.float32)
+    _dev(y, "lora_expand(y)", torch.bfloat16)
+    M, N = y.shape
+    _lib.call("eggroll_lora_expand", T.data_ptr(), theta_pop.data_ptr(), theta_pop.stride(0), offB, r, float(scale),
+              rows_per_member, M, N, y.data_ptr(), y.stride(0), _stream(y.device))
+    return y

@@ -1,0 +1,142 @@
+/*
+ * eggroll.h — C-ABI of the MI355X-native EGGROLL ES engine (libeggroll.so).
+ *
+ * This is the drop-in boundary for the reference's ES hot path
+ * (amit154154/HyperscaleES_T2I, `unifed_es.py:89-314` es_step_unified on top of
+ * `utills.py:14-136` EggRollNoiser, `utills.py:310-349` fitness shaping / caps, and the
+ * PEFT LoRA linear injected at `es_backend.py:193-200`).  The reference is pure Python;
+ * these entry points are what its `ctypes` binding would call.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a caller-allocated DEVICE pointer unless the name ends in `_host`;
+ *   - work is stream-ordered on `stream` (a hipStream_t, NULL = default stream);
+ *   - no internal allocation, no host synchronisation (graph-capturable);
+ *   - return 0 on success, negative on error; eggroll_last_error() gives a message
+ *     (thread-local);
+ *   - deterministic: identical inputs give bit-identical outputs, independent of which
+ *     rank/device evaluates which member (noise is a pure function of (seed, base member,
+ *     factor element)).
+ *
+ * Noise model (reference `utills.py:43-106`): every parameter MATRIX P (m x n) gets
+ *   E = a b^T / sqrt(r),  a in R^{m x r}, b in R^{n x r}, entries iid N(0,1);
+ * 1-D parameters get dense iid N(0,1) noise (reference fallback `utills.py:63-66`).
+ * Antithetic layout (`utills.py:88-105`): with h = pop/2, member k uses base sample
+ *   j = k (k < h, sign +), j = k-h (h <= k < 2h, sign -), j = h (k = 2h, odd pop, sign +).
+ * Non-antithetic: member k uses base sample k with sign +.
+ */
+#ifndef EGGROLL_H_
+#define EGGROLL_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EGGROLL_OK 0
+#define EGGROLL_ERR_ARG (-1)
+#define EGGROLL_ERR_LAUNCH (-2)
+#define EGGROLL_ERR_UNSUPPORTED (-3)
+
+/* One trainable parameter inside the flat theta vector (reference `utills.py:141-162`:
+ * theta = concat of module.parameters() with requires_grad, row-major views).
+ * Passed to kernels as a DEVICE array of n_mats records (int64 fields).              */
+typedef struct eggroll_mat {
+    int64_t rows;       /* m: first dim (or numel for a 1-D param)                    */
+    int64_t cols;       /* n: second dim; 0 marks a 1-D param (dense Gaussian noise)  */
+    int64_t theta_off;  /* element offset of this param in theta                       */
+    int64_t factor_off; /* element offset of its factors in one base sample's factor   *
+                         * vector: a [rows][r] then b [cols][r]; 1-D: numel values     */
+    int64_t chunk_off;  /* prefix count of EGGROLL_CHUNK-element work chunks           */
+    int64_t reserved;
+} eggroll_mat_t;
+
+#define EGGROLL_CHUNK 1024
+
+/* Library identification. */
+const char* eggroll_version(void);
+const char* eggroll_last_error(void);
+
+/* (1) Noise factors — replaces `torch.randn` calls of `EggRollNoiser._sample_low_rank_block`
+ * (utills.py:59-65).  Counter-based Philox4x32-10 keyed by `seed` (the epoch, as in
+ * unifed_es.py:120-122), counter = (element/4, base member j, 0xE6606011).  Writes
+ * out[(j - base_lo) * ld + g] = N(0,1) for j in [base_lo, base_hi), g in [0, factor_len).
+ * ld >= factor_len, ld % 4 == 0.                                                        */
+int eggroll_noise_factors(uint64_t seed, int64_t base_lo, int64_t base_hi, int64_t factor_len,
+                          int64_t ld, float* out, void* stream);
+
+/* Debug/parity: raw Philox4x32-10 words for (seed, j, quads [0, n_quads)). out: 4*n_quads u32. */
+int eggroll_philox_words(uint64_t seed, int64_t j, int64_t n_quads, uint32_t* out, void* stream);
+
+/* Perturb — replaces `theta_k = theta + sigma * eps[k]` (unifed_es.py:160) and, with
+ * theta == NULL and sigma == 1, materialises eps rows (EggRollNoiser.sample_eps,
+ * utills.py:70-106).  For members k in [member_lo, member_hi):
+ *   out[(k - member_lo) * ld_out + d] = theta[d] + sigma * s_k * E_{j(k)}[d]
+ * with E computed as (sum_q a[i,q] b[c,q]) / sqrt(r) in fp32 (reference op order).
+ * factors: base samples [0, n_base) with row stride ld_f (as written by noise_factors,
+ * base_lo = 0).  mats: device array of n_mats records; total_chunks = sum over mats of
+ * ceil(numel / EGGROLL_CHUNK) (host-known); D = total theta length.                     */
+int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int64_t n_base,
+                    const eggroll_mat_t* mats, int32_t n_mats, int64_t total_chunks, int64_t D,
+                    int32_t rank,
+                    int32_t pop, int32_t antithetic, int64_t member_lo, int64_t member_hi,
+                    float sigma, float* out, int64_t ld_out, void* stream);
+
+/* (3) Fitness — replaces paper_prompt_normalized_scores (utills.py:310-330) or
+ * S.mean(dim=1) (unifed_es.py:234), the finite mask (unifed_es.py:236-240,266),
+ * standardize_fitness (utills.py:168-178) and the rank sort (unifed_es.py:244).
+ * S: [n, m] fp32 row-major.  Outputs (device):
+ *   scores[n], mu[m] (promptnorm column means; S column means otherwise),
+ *   stats[4] = {sigma_bar (NaN if promptnorm off), n_finite, mean_f, std_f},
+ *   fitness[n] (z-scored over finite members; 0 for non-finite members),
+ *   finite[n] (0/1), order[n] = stable ascending argsort of scores (NaN last).
+ * Single workgroup; n <= 4096, m <= 1024.                                                 */
+int eggroll_fitness(const float* S, int32_t n, int32_t m, int32_t use_promptnorm,
+                    float* scores, float* mu, float* stats, float* fitness, int32_t* finite,
+                    int32_t* order, void* stream);
+
+/* (4) Update — replaces EggRollNoiser.do_update (utills.py:115-136) followed by
+ * cap_step_norm and cap_theta_norm (utills.py:333-349, unifed_es.py:280-281):
+ *   theta_out = theta + (lr_scale*sigma) * (1/N_f) * sum_k f_k eps_k
+ * evaluated in factor form as a rank-(n_base*r) reduction per matrix (antithetic pairs
+ * collapsed: c_j = f_j - f_{j+h}).  N_f is read from stats[1] (device, written by
+ * eggroll_fitness); N_f == 0 leaves theta unchanged (unifed_es.py:237-240).
+ * max_step_norm / theta_max_norm <= 0 disable the caps.
+ * workspace: >= eggroll_update_workspace_bytes(n_mats_chunks) bytes.
+ * theta_out may not alias theta.                                                          */
+int64_t eggroll_update_workspace_bytes(int64_t total_chunks);
+int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64_t n_base,
+                   const float* fitness, const float* stats, int32_t pop, int32_t antithetic,
+                   const eggroll_mat_t* mats, int32_t n_mats, int64_t total_chunks, int64_t D,
+                   int32_t rank, float lr, float max_step_norm, float theta_max_norm,
+                   void* workspace, float* theta_out, void* stream);
+
+/* (2) Population-batched perturbed LoRA linear — replaces per-member
+ * `unflatten_to_params` + PEFT lora.Linear.forward (peft: y = base(x) + B(A x) * alpha/r),
+ * members evaluated sequentially in the reference (unifed_es.py:159-163).
+ * Rows of X are stacked member-major: row -> member k = member_lo + row / rows_per_member.
+ *   Y[row, n] = sum_k X[row,k] W[n,k] + bias[n] + scale * sum_q T[row,q] * Bk[n,q]
+ *   T[row, q] = sum_k X[row,k] * Ak[q,k]            (fp32, full-K reduction)
+ * Ak = theta_pop[k_local*ld_theta + offA] as [r][K]; Bk = theta_pop[... + offB] as [N][r]
+ * (PEFT lora_A.weight / lora_B.weight row-major inside theta_k).
+ * X, W, Y bf16 row-major (ldx, ldw, ldy in elements); bias bf16 or NULL; theta_pop fp32.
+ * T_ws: fp32 workspace [M, r].  Requires K % 64 == 0, r <= 16, ldx/ldw % 8 == 0.      */
+int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw,
+                            const void* bias, const float* theta_pop, int64_t ld_theta,
+                            int64_t offA, int64_t offB, int32_t r, float scale,
+                            int64_t rows_per_member, int64_t M, int64_t N, int64_t K,
+                            void* Y, int64_t ldy, float* T_ws, void* stream);
+
+/* Pieces of (2), exported for A/B measurement and for hosts that run the base GEMM
+ * elsewhere:  T = X Ak^T per member (fp32), and Y += scale * T Bk^T (bf16 in place).   */
+int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
+                         int64_t offA, int32_t r, int64_t rows_per_member, int64_t M, int64_t K,
+                         float* T, void* stream);
+int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
+                        int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
+                        void* Y, int64_t ldy, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EGGROLL_H_ */

@@ -1,0 +1,253 @@
+"""Generate golden vectors from the REFERENCE implementation (run in the build container only).
+
+    python tests/golden/make_golden.py          # needs /root/reference (read-only mount)
+
+Imports the reference's own `utills.py` (amit154154/HyperscaleES_T2I) and records, for small
+seeded inputs, the outputs of the functions on the ES hot path.  The random factors that
+`EggRollNoiser._sample_low_rank_block` draws with `torch.randn` (utills.py:59-65) are captured
+by wrapping torch.randn, so the fixtures double as NOISE-INJECTION vectors: feeding the
+captured factors to our kernels must reproduce the reference eps exactly.
+Fixtures are data only (inputs + expected outputs), written to tests/golden/*.npz.
+The GPU box never runs this script and never reads /root/reference.
+"""
+from __future__ import annotations
+
+import math
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+
+
+def load_reference():
+    if not (REF / "utills.py").exists():
+        raise SystemExit("reference not mounted at /root/reference")
+    sys.path.insert(0, str(REF))
+    import utills  # noqa: E402  (reference module)
+    return utills
+
+
+class RandnRecorder:
+    """Wraps torch.randn; records every tensor drawn (in call order)."""
+
+    def __init__(self):
+        self.calls = []
+        self._orig = torch.randn
+
+    def __enter__(self):
+        orig = self._orig
+
+        def rec(*a, **k):
+            t = orig(*a, **k)
+            self.calls.append(t.detach().clone())
+            return t
+
+        torch.randn = rec
+        return self
+
+    def __exit__(self, *exc):
+        torch.randn = self._orig
+
+
+SHAPE_SETS = {
+    # LoRA-like: lora_A [r_l, in], lora_B [out, r_l] pairs + a 1-D param (dense fallback)
+    "lora_small": [(2, 12), (10, 2), (2, 7), (5, 2)],
+    "mixed": [(3, 4), (6,), (2, 9), (9, 2), (1, 1)],
+}
+
+
+def gen_eps(u):
+    recs = {}
+    idx = 0
+    for sname, shapes in SHAPE_SETS.items():
+        for pop in (1, 2, 3, 4, 5, 8):
+            for rank in (1, 2, 4):
+                for anti in (False, True):
+                    for seed in (0, 3):
+                        torch.manual_seed(seed)
+                        noiser = u.EggRollNoiser([torch.Size(s) for s in shapes], sigma=0.01, lr_scale=0.1,
+                                                 rank=rank, use_antithetic=anti)
+                        with RandnRecorder() as rr:
+                            eps = noiser.sample_eps(pop, "cpu")
+                        base_pop = (pop // 2 + pop % 2) if anti else pop
+                        # flatten captured factors into our per-base-sample layout
+                        parts = []
+                        ci = 0
+                        for s in shapes:
+                            if len(s) == 2:
+                                a, b = rr.calls[ci], rr.calls[ci + 1]
+                                ci += 2
+                                parts.append(a.reshape(base_pop, -1))
+                                parts.append(b.reshape(base_pop, -1))
+                            else:
+                                parts.append(rr.calls[ci].reshape(base_pop, -1))
+                                ci += 1
+                        assert ci == len(rr.calls)
+                        factors = torch.cat(parts, dim=1)
+                        theta = torch.randn(noiser.num_params, generator=torch.Generator().manual_seed(100 + idx))
+                        k = pop - 1
+                        theta_k = theta + noiser.sigma * eps[k]
+                        key = f"{sname}_p{pop}_r{rank}_a{int(anti)}_s{seed}"
+                        recs[key + "/factors"] = factors.numpy()
+                        recs[key + "/eps"] = eps.numpy()
+                        recs[key + "/theta"] = theta.numpy()
+                        recs[key + "/theta_last"] = theta_k.numpy()
+                        idx += 1
+    recs["meta/shape_sets"] = np.array(repr(SHAPE_SETS))
+    np.savez_compressed(OUT / "g1_eps.npz", **recs)
+    return len(recs)
+
+
+def gen_fitness(u):
+    recs = {}
+    g = torch.Generator().manual_seed(7)
+    cases = {}
+    for n in (1, 2, 3, 4, 8, 64, 128):
+        for m in (1, 4):
+            cases[f"rand_n{n}_m{m}"] = torch.randn(n, m, generator=g) * 3 + 20
+    cases["tied_rows"] = torch.tensor([[1.0, 2.0], [1.0, 2.0], [0.5, 3.0], [1.0, 2.0]])
+    cases["const"] = torch.full((6, 4), 21.5)
+    t = torch.randn(8, 4, generator=g)
+    t[3, 1] = float("nan")
+    cases["nan_one"] = t
+    t = torch.randn(8, 4, generator=g)
+    t[:, 0] = float("inf")
+    cases["inf_col"] = t
+    t = torch.randn(5, 3, generator=g)
+    cases["ints"] = torch.round(t * 4)
+    for name, S in cases.items():
+        scores, mu, sb = u.paper_prompt_normalized_scores(S)
+        recs[f"{name}/S"] = S.numpy()
+        recs[f"{name}/pn_scores"] = scores.numpy()
+        recs[f"{name}/pn_mu"] = mu.numpy()
+        recs[f"{name}/pn_sigma_bar"] = np.array(sb.item(), np.float32)
+        recs[f"{name}/mean_scores"] = S.mean(dim=1).numpy()
+        for tag, sc in (("pn", scores), ("mean", S.mean(dim=1))):
+            fin = torch.isfinite(sc)
+            recs[f"{name}/{tag}_finite"] = fin.numpy()
+            if fin.any():
+                recs[f"{name}/{tag}_fitness"] = u.standardize_fitness(sc[fin]).numpy()
+            if fin.all():
+                recs[f"{name}/{tag}_order"] = torch.sort(sc, stable=True)[1].numpy()
+    # z-score edge cases (utills.py:168-178)
+    for name, r in {"z_one": torch.tensor([3.0]), "z_two": torch.tensor([1.0, 2.0]),
+                    "z_const": torch.full((5,), 2.0), "z_rand": torch.randn(33, generator=g)}.items():
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            recs[f"{name}/r"] = r.numpy()
+            recs[f"{name}/f"] = u.standardize_fitness(r).numpy()
+    np.savez_compressed(OUT / "g2_fitness.npz", **recs)
+    return len(recs)
+
+
+def gen_update(u):
+    recs = {}
+    g = torch.Generator().manual_seed(11)
+    shapes = SHAPE_SETS["lora_small"]
+    D = sum(int(np.prod(s)) for s in shapes)
+    for pop in (2, 5, 8):
+        for caps in ((0.0, 0.0), (0.0, 40.0), (1e-3, 40.0), (0.0, 1.0), (5e-4, 1.0)):
+            torch.manual_seed(pop)
+            noiser = u.EggRollNoiser([torch.Size(s) for s in shapes], sigma=0.01, lr_scale=0.1, rank=1,
+                                     use_antithetic=True)
+            eps = noiser.sample_eps(pop, "cpu")
+            theta = torch.randn(D, generator=g) * 0.3
+            raw = torch.randn(pop, generator=g)
+            f = noiser.convert_fitnesses(raw)
+            after = noiser.do_update(theta, eps, f)
+            after_s = u.cap_step_norm(theta, after, caps[0])
+            after_t = u.cap_theta_norm(after_s, caps[1])
+            key = f"p{pop}_ms{caps[0]}_mt{caps[1]}"
+            recs[key + "/theta"] = theta.numpy()
+            recs[key + "/eps"] = eps.numpy()
+            recs[key + "/raw"] = raw.numpy()
+            recs[key + "/f"] = f.numpy()
+            recs[key + "/after_update"] = after.numpy()
+            recs[key + "/after_caps"] = after_t.numpy()
+    np.savez_compressed(OUT / "g4_update.npz", **recs)
+    return len(recs)
+
+
+def gen_indices(u):
+    recs = {}
+    for P in (4, 8, 1631):
+        for k in (1, 2, 4, 7):
+            rows = []
+            for seed in range(100):
+                rows.append(u.sample_indices_unique(seed, P, k))
+            recs[f"P{P}_k{k}"] = np.array(rows, np.int64)
+    recs["repeat_4x3"] = np.array(u.repeat_batches([3, 1, 2, 0], 3), np.int64)
+    np.savez_compressed(OUT / "g5_indices.npz", **recs)
+    return len(recs)
+
+
+def gen_es_tail(u):
+    """unifed_es.py:227-281 composed from the reference's own functions (unifed_es.py itself does
+    not import here: wandb / lovely_tensors / peft are absent)."""
+    recs = {}
+    g = torch.Generator().manual_seed(23)
+    shapes = SHAPE_SETS["lora_small"]
+    for case, (pop, m, pn, nan_row) in enumerate([(8, 4, True, None), (8, 4, False, None), (7, 2, True, None),
+                                                  (8, 4, True, 3), (8, 4, False, 5), (64, 4, True, None)]):
+        torch.manual_seed(case)
+        noiser = u.EggRollNoiser([torch.Size(s) for s in shapes], sigma=0.01, lr_scale=0.1, rank=1,
+                                 use_antithetic=True)
+        eps = noiser.sample_eps(pop, "cpu")
+        theta = torch.randn(noiser.num_params, generator=g)
+        S = torch.randn(pop, m, generator=g) + 21
+        if nan_row is not None:
+            S[nan_row, 0] = float("nan")
+        if pn:
+            scores, mu, sb = u.paper_prompt_normalized_scores(S)
+        else:
+            scores = S.mean(dim=1)
+        fin = torch.isfinite(scores)
+        key = f"case{case}"
+        recs[key + "/S"] = S.numpy()
+        recs[key + "/eps"] = eps.numpy()
+        recs[key + "/theta"] = theta.numpy()
+        recs[key + "/cfg"] = np.array([pop, m, int(pn)], np.int64)
+        if not fin.any():  # unifed_es.py:237-240 early return: theta unchanged
+            after = theta.clone()
+        else:
+            if fin.all():
+                recs[key + "/order"] = torch.sort(scores)[1].numpy()
+            f = noiser.convert_fitnesses(scores[fin])
+            after = noiser.do_update(theta, eps[fin], f)
+            after = u.cap_step_norm(theta, after, 0.0)
+            after = u.cap_theta_norm(after, 40.0)
+        recs[key + "/after"] = after.numpy()
+        recs[key + "/scores"] = scores.numpy()
+    np.savez_compressed(OUT / "g6_es_tail.npz", **recs)
+    return len(recs)
+
+
+def gen_lora(u):
+    """PEFT LoRA-linear formula (peft not importable here -> formula-level fixture only)."""
+    recs = {}
+    g = torch.Generator().manual_seed(5)
+    for name, (M, K, N, r) in {"small": (24, 64, 40, 2), "r4": (16, 128, 72, 4)}.items():
+        x = torch.randn(M, K, generator=g, dtype=torch.float64)
+        W = torch.randn(N, K, generator=g, dtype=torch.float64) * 0.05
+        b = torch.randn(N, generator=g, dtype=torch.float64)
+        A = torch.randn(r, K, generator=g, dtype=torch.float64) * 0.1
+        B = torch.randn(N, r, generator=g, dtype=torch.float64) * 0.1
+        s = 8.0 / r
+        y = torch.nn.functional.linear(x, W, b) + torch.nn.functional.linear(torch.nn.functional.linear(x, A), B) * s
+        for k, v in dict(x=x, W=W, b=b, A=A, B=B, y=y).items():
+            recs[f"{name}/{k}"] = v.numpy()
+        recs[f"{name}/scale"] = np.array(s)
+    np.savez_compressed(OUT / "g7_lora.npz", **recs)
+    return len(recs)
+
+
+if __name__ == "__main__":
+    u = load_reference()
+    torch.set_num_threads(1)
+    for fn in (gen_eps, gen_fitness, gen_update, gen_indices, gen_es_tail, gen_lora):
+        print(fn.__name__, fn(u))

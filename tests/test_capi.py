@@ -1,0 +1,62 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly what
+include/eggroll.h declares, and rejects bad arguments with a message (no kernel launched)."""
+import ctypes as C
+import subprocess
+
+import numpy as np
+import pytest
+
+from hyperscalees_t2i_amd import _lib
+from hyperscalees_t2i_amd.kernels import ThetaLayout
+from oracle import eggroll_oracle as O
+
+
+def test_library_loads_and_versions():
+    lib = _lib.load()
+    assert _lib.version().startswith("eggroll-mi355x")
+    assert lib.eggroll_last_error() is not None
+
+
+def test_exports_match_header():
+    declared = _lib.header_symbols()
+    assert set(declared) == set(_lib.SIGNATURES), "ctypes signatures drift from include/eggroll.h"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln and ln.split()[-1].startswith("eggroll_")}
+    assert exported == set(declared)
+
+
+def test_header_compiles_as_c():
+    src = '#include "eggroll.h"\nint main(void){eggroll_mat_t m; (void)m; return (int)sizeof(eggroll_mat_t) - 48;}\n'
+    r = subprocess.run(["gcc", "-x", "c", "-std=c99", "-Wall", "-Werror", f"-I{_lib.HEADER.parent}", "-", "-o",
+                        "/tmp/eggroll_hdr_test"], input=src, text=True, capture_output=True)
+    assert r.returncode == 0, r.stderr
+    assert subprocess.run(["/tmp/eggroll_hdr_test"]).returncode == 0
+
+
+def test_argument_errors_are_reported():
+    lib = _lib.load()
+    rc = lib.eggroll_fitness(None, 0, 4, 1, None, None, None, None, None, None, None)
+    assert rc == -1 and b"fitness" in lib.eggroll_last_error()
+    rc = lib.eggroll_noise_factors(0, 0, 2, 10, 9, None, None)  # ld not multiple of 4
+    assert rc == -1 and b"ld" in lib.eggroll_last_error()
+    rc = lib.eggroll_lora_linear_pop(None, 64, None, 64, None, None, 0, 0, 0, 2, 1.0, 10, 10, 10, 60, None, 10,
+                                     None, None)  # K % 64 != 0
+    assert rc == -1 and b"multiple of 64" in lib.eggroll_last_error()
+    with pytest.raises(_lib.EggrollError):
+        _lib.check(-1, "probe")
+
+
+def test_zero_sized_calls_are_noops():
+    lib = _lib.load()
+    assert lib.eggroll_noise_factors(0, 3, 3, 16, 16, None, None) == 0
+    assert lib.eggroll_lora_project(None, 64, None, 64, 0, 2, 4, 0, 64, None, None) == 0
+
+
+def test_layout_matches_oracle():
+    shapes = [(2, 2240), (2240, 2), (6,), (2, 256), (13440, 2)]
+    for r in (1, 2, 4):
+        a = ThetaLayout(shapes, r)
+        b = O.layout(shapes, r)
+        assert np.array_equal(a.mats, b["mats"]) and a.D == b["D"] and a.factor_len == b["factor_len"]
+        assert a.total_chunks == b["total_chunks"] and a.factor_ld % 4 == 0

@@ -1,0 +1,251 @@
+"""HIP kernel parity vs the CPU oracle (and, through injected factors, vs the reference).
+
+Bars: integer/index work bit-exact (Philox words, member->base layout, ranks); fitness kernel
+bit-exact vs the oracle's fixed-order restatement; eps/perturb bit-exact for rank 1 (single
+product) and <= 2 ulp-ish (rtol 2e-6) otherwise; update within fp32 tolerance (rtol 1e-5);
+bf16 LoRA linear within a bf16 tolerance stated per test."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from hyperscalees_t2i_amd import kernels as K
+from hyperscalees_t2i_amd.es import EggRollNoiser, paper_prompt_normalized_scores, standardize_fitness
+from oracle import eggroll_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SHAPE_SETS = {
+    "lora_small": [(2, 12), (10, 2), (2, 7), (5, 2)],
+    "mixed": [(3, 4), (6,), (2, 9), (9, 2), (1, 1)],
+}
+
+
+def _groups(npz):
+    keys = {}
+    for k in npz.files:
+        if "/" in k:
+            g, f = k.split("/", 1)
+            keys.setdefault(g, {})[f] = npz[k]
+    return keys
+
+
+# ---------------------------------------------------------------------------------- noise
+def test_philox_words_bit_exact(dev):
+    for seed, j in ((0, 0), (7, 3), (2 ** 40 + 5, 17)):
+        got = K.philox_words(seed, j, 4099, dev).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, O.philox_words(seed, j, 4099))
+
+
+@pytest.mark.parametrize("flen", [1, 7, 4096, 100_003])
+def test_noise_factors_match_oracle(dev, flen):
+    lay = K.ThetaLayout([(flen,)], 1)
+    f = K.noise_factors(11, 5, lay, dev, base_lo=2).cpu().numpy()[:, :flen]
+    ref = O.noise_factors(11, 2, 5, flen)
+    np.testing.assert_allclose(f, ref, rtol=0, atol=2e-5)
+
+
+def test_noise_shard_invariance(dev):
+    """Base sample j's factors do not depend on which base range generated them."""
+    lay = K.ThetaLayout([(2, 2240), (2240, 2)], 1)
+    full = K.noise_factors(9, 8, lay, dev)
+    part = K.noise_factors(9, 8, lay, dev, base_lo=5)
+    assert torch.equal(full[5:], part)
+    z = full[:, :lay.factor_len].flatten()
+    assert abs(z.mean().item()) < 0.01 and abs(z.std().item() - 1) < 0.01
+
+
+# ---------------------------------------------------------------------------------- eps / perturb
+def test_injected_reference_factors_reproduce_reference_eps(dev, golden):
+    g = _groups(golden("g1_eps.npz"))
+    for key, d in g.items():
+        if key == "meta":
+            continue
+        sname, rest = key.rsplit("_p", 1)
+        pop, rank, anti, _ = rest.split("_")
+        pop, rank, anti = int(pop), int(rank[1:]), bool(int(anti[1:]))
+        shapes = SHAPE_SETS[sname]
+        lay = K.ThetaLayout(shapes, rank)
+        fac = torch.zeros((d["factors"].shape[0], lay.factor_ld), dtype=torch.float32)
+        fac[:, :lay.factor_len] = torch.from_numpy(d["factors"])
+        fac = fac.to(dev)
+        eps = K.perturb(None, fac, lay, pop, anti, 0, pop, 1.0).cpu().numpy()
+        if rank == 1:
+            assert np.array_equal(eps, d["eps"]), key
+        else:
+            np.testing.assert_allclose(eps, d["eps"], rtol=2e-6, atol=1e-7, err_msg=key)
+            np.testing.assert_array_equal(eps, O.dev_eps_rows(d["factors"], shapes, pop, rank, anti, 0, pop))
+        th = torch.from_numpy(d["theta"]).to(dev)
+        tl = K.perturb(th, fac, lay, pop, anti, pop - 1, pop, 0.01).cpu().numpy()[0]
+        if rank == 1:
+            assert np.array_equal(tl, d["theta_last"]), key
+        else:
+            np.testing.assert_allclose(tl, d["theta_last"], rtol=2e-6, atol=1e-7, err_msg=key)
+
+
+def test_perturb_member_ranges_consistent(dev):
+    shapes = [(2, 2240), (2240, 2), (2, 256), (13440, 2), (17,)]
+    n = EggRollNoiser(shapes, sigma=0.01, lr_scale=0.1, rank=1, use_antithetic=True)
+    pop = 9
+    fac = n.sample_factors(pop, dev, seed=4)
+    theta = torch.randn(n.num_params, device=dev)
+    full = n.perturb(theta, fac, pop, 0, pop)
+    for lo, hi in ((0, 3), (3, 7), (7, 9)):
+        assert torch.equal(n.perturb(theta, fac, pop, lo, hi), full[lo:hi])
+    eps = n.eps_from_factors(fac, pop)
+    h = pop // 2
+    assert torch.equal(eps[:h], -eps[h:2 * h])
+    ref = O.dev_eps_rows(fac[:, :n.layout.factor_len].cpu().numpy(), shapes, pop, 1, True, 0, pop)
+    assert np.array_equal(eps.cpu().numpy(), ref)
+
+
+# ---------------------------------------------------------------------------------- fitness
+def test_fitness_bit_exact_vs_oracle_and_reference_ranks(dev, golden):
+    g = _groups(golden("g2_fitness.npz"))
+    for name, d in g.items():
+        if name.startswith("z_"):
+            continue
+        S = torch.from_numpy(d["S"]).to(dev)
+        for tag, pn in (("pn", True), ("mean", False)):
+            out = {k: v.cpu().numpy() for k, v in K.fitness(S, pn).items()}
+            ref = O.dev_fitness(d["S"], pn)
+            for k in ("scores", "mu", "fitness", "finite"):
+                np.testing.assert_array_equal(out[k], ref[k], err_msg=f"{name}/{tag}/{k}")
+            np.testing.assert_array_equal(out["stats"], ref["stats"], err_msg=f"{name}/{tag}/stats")
+            assert np.array_equal(out["order"], ref["order"]), f"{name}/{tag} order"
+            if f"{tag}_order" in d:  # reference torch.sort ranks
+                assert np.array_equal(out["order"], d[f"{tag}_order"]), f"{name}/{tag} ref ranks"
+
+
+def test_fitness_api_mirrors(dev, golden):
+    g = _groups(golden("g2_fitness.npz"))
+    d = g["rand_n64_m4"]
+    sc, mu, sb = paper_prompt_normalized_scores(torch.from_numpy(d["S"]).to(dev))
+    np.testing.assert_allclose(sc.cpu().numpy(), d["pn_scores"], rtol=2e-6, atol=2e-6)
+    np.testing.assert_allclose(float(sb), float(d["pn_sigma_bar"]), rtol=1e-6)
+    for name in ("z_two", "z_const", "z_rand", "z_one"):
+        f = standardize_fitness(torch.from_numpy(g[name]["r"]).to(dev)).cpu().numpy()
+        np.testing.assert_allclose(f, g[name]["f"], rtol=2e-5, atol=2e-6, equal_nan=True, err_msg=name)
+
+
+# ---------------------------------------------------------------------------------- update
+@pytest.mark.parametrize("pop,anti,rank", [(8, True, 1), (7, True, 2), (6, False, 1), (64, True, 1), (5, False, 4)])
+@pytest.mark.parametrize("caps", [(0.0, 0.0), (0.0, 40.0), (1e-4, 0.0), (0.0, 0.5), (2e-4, 0.5)])
+def test_update_matches_reference_formula(dev, pop, anti, rank, caps):
+    shapes = [(2, 300), (260, 2), (2, 64), (7,), (96, 2)]
+    n = EggRollNoiser(shapes, sigma=0.01, lr_scale=0.1, rank=rank, use_antithetic=anti)
+    fac = n.sample_factors(pop, dev, seed=pop)
+    g = torch.Generator().manual_seed(pop)
+    theta = (torch.randn(n.num_params, generator=g) * 0.02).to(dev)
+    S = (torch.randn(pop, 4, generator=g) + 20).to(dev)
+    fit = K.fitness(S, True)
+    out = n.update_from_factors(theta, fac, fit, pop, max_step_norm=caps[0], theta_max_norm=caps[1])
+    eps = n.eps_from_factors(fac, pop).cpu().numpy()
+    ref, info = O.ref_es_tail(S.cpu().numpy(), eps, theta.cpu().numpy(), promptnorm=True, lr_scale=0.1, sigma=0.01,
+                              max_step_norm=caps[0], theta_max_norm=caps[1])
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
+
+
+def test_update_nonfinite_members(dev):
+    shapes = [(2, 40), (40, 2)]
+    pop = 8
+    n = EggRollNoiser(shapes, sigma=0.01, lr_scale=0.1, rank=1, use_antithetic=True)
+    fac = n.sample_factors(pop, dev, seed=1)
+    theta = torch.randn(n.num_params, device=dev)
+    S = torch.randn(pop, 4, device=dev) + 3
+    S[2, 1] = float("nan")
+    # promptnorm: one NaN poisons all -> theta unchanged (unifed_es.py:237-240)
+    fit = K.fitness(S, True)
+    assert fit["stats"][1].item() == 0
+    assert torch.equal(n.update_from_factors(theta, fac, fit, pop, 0.0, 40.0), theta)
+    # mean scoring: member 2 dropped, N_f = 7
+    fit = K.fitness(S, False)
+    out = n.update_from_factors(theta, fac, fit, pop, 0.0, 0.0)
+    eps = n.eps_from_factors(fac, pop).cpu().numpy()
+    ref, info = O.ref_es_tail(S.cpu().numpy(), eps, theta.cpu().numpy(), promptnorm=False, lr_scale=0.1, sigma=0.01,
+                              max_step_norm=0.0, theta_max_norm=0.0)
+    assert info["finite"].sum() == 7
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
+
+
+# ---------------------------------------------------------------------------------- LoRA linear
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _lora_case(dev, M, N, Kd, r, rpm, bias=True, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = _bf(torch.randn(M, Kd, generator=g)).to(dev)
+    W = _bf(torch.randn(N, Kd, generator=g) * 0.05).to(dev)
+    b = _bf(torch.randn(N, generator=g)).to(dev) if bias else None
+    nm = -(-M // rpm)
+    D = r * Kd + N * r + 5
+    ld = -(-D // 4) * 4
+    tp = (torch.randn(nm, ld, generator=g) * 0.1).to(dev)
+    offA, offB = 4, 4 + r * Kd
+    return x, W, b, tp, offA, offB
+
+
+def _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm):
+    return O.ref_lora_linear_pop(x.float().cpu().numpy(), W.float().cpu().numpy(),
+                                 None if b is None else b.float().cpu().numpy(), tp.cpu().numpy(), offA, offB, r,
+                                 scale, rpm)
+
+
+@pytest.mark.parametrize("M,N,Kd,r,rpm", [
+    (300, 200, 128, 2, 100),      # ragged M, N; members not tile-aligned
+    (257, 128, 64, 1, 257),       # single member, one row over a tile
+    (1000, 2240, 256, 2, 300),    # Sana cross-attn-like members of 300 rows
+    (512, 96, 192, 4, 128),       # r = 4 (VAR-like lora rank)
+    (64, 32, 2240, 2, 16),        # proj_out-like N = 32, time-embed rows per member = 16
+])
+def test_lora_linear_pop_vs_fp64(dev, M, N, Kd, r, rpm):
+    x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm)
+    scale = 8.0 / r
+    y = K.lora_linear_pop(x, W, b, tp, offA, offB, r, scale, rpm)
+    torch.cuda.synchronize()
+    ref = _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm)
+    got = y.float().cpu().numpy()
+    # bf16 output rounding (2^-9 relative) + fp32 accumulation over K
+    tol = 2 ** -8 * np.abs(ref) + 2e-4 * math.sqrt(Kd) * np.abs(ref).std()
+    assert (np.abs(got - ref) <= tol + 1e-3).all(), float(np.abs(got - ref).max())
+
+
+def test_lora_linear_no_lora_matches_torch_matmul(dev):
+    x, W, b, tp, *_ = _lora_case(dev, 640, 384, 512, 2, 640)
+    y = K.lora_linear_pop(x, W, b, None, 0, 0, 0, 0.0, 640)
+    ref = torch.nn.functional.linear(x.float(), W.float(), b.float())
+    assert torch.allclose(y.float(), ref, rtol=1e-2, atol=2e-2)
+
+
+def test_lora_project_expand_compose(dev):
+    M, N, Kd, r, rpm = 600, 320, 256, 2, 200
+    x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm, bias=False)
+    base = K.lora_linear_pop(x, W, None, None, 0, 0, 0, 0.0, rpm)
+    T = K.lora_project(x, tp, offA, r, rpm)
+    fused = K.lora_linear_pop(x, W, None, tp, offA, offB, r, 4.0, rpm)
+    two = K.lora_expand(T, tp, offB, r, 4.0, rpm, base.clone())
+    assert (fused.float() - two.float()).abs().max().item() <= 0.02 * fused.float().abs().max().item()
+    Tref = np.stack([x[i].float().cpu().numpy() @ tp[i // rpm, offA:offA + r * Kd].view(r, Kd).cpu().numpy().T
+                     for i in range(M)])
+    np.testing.assert_allclose(T.cpu().numpy(), Tref, rtol=1e-4, atol=1e-3)
+
+
+def test_lora_linear_sana_shape_sampled_rows(dev):
+    """Full Sana attention shape (K = N = 2240) at 2 members x 16384 rows; rows sampled vs fp64."""
+    M, N, Kd, r, rpm = 2 * 16384, 2240, 2240, 2, 16384
+    x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm)
+    y = K.lora_linear_pop(x, W, b, tp, offA, offB, r, 4.0, rpm)
+    rows = torch.tensor([0, 1, 127, 128, 5000, 16383, 16384, 16385, 30000, M - 1])
+    ref = _lora_ref(x[rows.to(dev)], W, b, tp, offA, offB, r, 4.0, rpm)
+    # recompute reference rows with the right member per row
+    for i, row in enumerate(rows.tolist()):
+        k = row // rpm
+        A = tp[k, offA:offA + r * Kd].view(r, Kd).double().cpu().numpy()
+        B = tp[k, offB:offB + N * r].view(N, r).double().cpu().numpy()
+        ref[i] = O.ref_lora_linear(x[row:row + 1].float().cpu().numpy(), W.float().cpu().numpy(),
+                                   b.float().cpu().numpy(), A, B, 4.0)[0]
+    got = y[rows.to(dev)].float().cpu().numpy()
+    err = np.abs(got - ref)
+    assert (err <= 2 ** -8 * np.abs(ref) + 2e-2).all(), float(err.max())
