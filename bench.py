@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Benchmark: ES member-evals/sec (whole node) for the Sana-Sprint 1.6B one-step EGGROLL epoch.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one full ES epoch (noise -> perturb -> population forward of the 1.6B transformer at
+1024 px -> DC-AE decode -> CLIP-B/32 + PickScore rewards -> S all-gather -> promptnorm fitness ->
+update) with pop_per_gpu = 8 members per GPU (weak scaling: N=1 is BASELINE configs[1], pop 8;
+N=8 is configs[2], pop 64).  value = pop_total * K / max-over-ranks wall time of the K timed epochs.
+Synthetic data: random-init frozen weights of the Sana/DC-AE/CLIP architectures (no checkpoints
+offline), synthetic prompt embeddings, random-init LoRA.
+
+Extra fields: `roofline` of the dominant hand-written kernel (the population LoRA GEMM, MFMA-bound,
+timed live with HIP events on its launch stream during the timed epochs), `cpu_baseline` (the
+reference path restated in numpy, timed on this host's cores; rank 0, N=1 only), per-phase times.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+
+METRIC = "ES member-evals/sec (whole node) Sana-Sprint 1.6B pop=64; % HBM/MFMA roofline"
+BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+HBM_PEAK_GBPS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--pop-per-gpu", type=int, default=8)
+    p.add_argument("--latent", type=int, default=32, help="32 -> 1024 px")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--small", action="store_true", help="tiny architecture (smoke only; not a valid metric)")
+    p.add_argument("--aux-out", type=str, default="", help="write per-phase / per-kernel details here")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], device="cuda", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def build(args, world, rank, device):
+    from hyperscalees_t2i_amd.backend import SanaBackend, SanaConfig
+    from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params
+    from hyperscalees_t2i_amd.es_step import DistInfo, ESConfig, ESEngine
+    from hyperscalees_t2i_amd.rewards import RewardModels
+    from hyperscalees_t2i_amd.sana import SanaArch
+
+    cfg = SanaConfig(width_latent=args.latent, height_latent=args.latent)
+    if args.small:
+        cfg.arch = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=2,
+                            cross_attention_head_dim=64, caption_channels=256)
+        cfg.vae_widths, cfg.vae_layers = (16, 32, 32, 64, 64, 64), (1, 1, 1, 1, 1, 1)
+    backend = SanaBackend(device=str(device), cfg=cfg)
+    backend.init_and_attach_lora()
+    if args.small:  # synthetic prompt embeds must match the tiny caption width
+        backend.base_prompt_embeds = backend.base_prompt_embeds[..., :256].contiguous()
+        backend._dev_prompts = (backend.base_prompt_embeds.to(device), backend.base_attention_mask.to(device))
+    params, shapes = backend.collect_lora_params()
+    theta = flatten_params(params).to(device=device, dtype=torch.float32)
+    noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=1, use_antithetic=True)
+    rewards = RewardModels.build(device, tiny=args.small)
+    pop = args.pop_per_gpu * world
+    es_cfg = ESConfig(pop_size=pop, sigma=1e-2, lr_scale=1e-1, egg_rank=1, use_antithetic=True, promptnorm=True,
+                      theta_max_norm=40.0, max_step_norm=0.0)
+    engine = ESEngine(backend, rewards, noiser, es_cfg, device, DistInfo(rank, world, None))
+    return backend, engine, noiser, theta, pop
+
+
+def aux_kernel_rooflines(engine, noiser, theta, pop, device):
+    """HBM-bound kernels timed with HIP events on the current stream (algorithmic bytes)."""
+    from hyperscalees_t2i_amd import kernels as K
+    lay = noiser.layout
+    nb = noiser.n_base(pop)
+    out = {}
+
+    def t(fn, it=10):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(it):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / it * 1e-3
+
+    fac = noiser.sample_factors(pop, device, seed=0)
+    sec = t(lambda: K.noise_factors(0, nb, lay, device, out=fac))
+    byt = 4.0 * nb * lay.factor_len
+    out["noise_factors"] = {"us": sec * 1e6, "bytes": byt, "GBps": byt / sec / 1e9, "frac": byt / sec / 1e9 / HBM_PEAK_GBPS}
+    nl = engine.hi - engine.lo
+    sec = t(lambda: noiser.perturb(theta, fac, pop, engine.lo, engine.hi, out=engine.theta_pop[:nl]))
+    byt = 4.0 * (nl * lay.D + lay.D + nb * lay.factor_len)
+    out["perturb"] = {"us": sec * 1e6, "bytes": byt, "GBps": byt / sec / 1e9, "frac": byt / sec / 1e9 / HBM_PEAK_GBPS}
+    S = torch.randn(pop, 4, device=device) + 21
+    fit = K.fitness(S, True)
+    sec = t(lambda: K.fitness(S, True))
+    out["fitness"] = {"us": sec * 1e6, "note": "latency-bound single workgroup (64x4 input)"}
+    newt = torch.empty_like(theta)
+    sec = t(lambda: noiser.update_from_factors(theta, fac, fit, pop, 0.0, 40.0, out=newt))
+    byt = 4.0 * (nb * lay.factor_len + 2 * lay.D)
+    out["update"] = {"us": sec * 1e6, "bytes": byt, "GBps": byt / sec / 1e9, "frac": byt / sec / 1e9 / HBM_PEAK_GBPS}
+    return out
+
+
+def load_pmc_traffic():
+    f = ROOT / "profiles" / "pmc_lora_gemm.json"
+    if f.exists():
+        try:
+            return json.loads(f.read_text())
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_setup(args)
+    device = torch.device(f"cuda:{local}")
+    from hyperscalees_t2i_amd.lora import GemmTimer
+
+    backend, engine, noiser, theta, pop = build(args, world, rank, device)
+    guidance = backend.cfg.guidance_scale
+    for w in range(args.warmup):
+        theta, _ = engine.step(theta, seed=w, guidance_scale=guidance)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    GemmTimer.reset(True)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        theta, stats = engine.step(theta, seed=args.warmup + s, guidance_scale=guidance)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    GemmTimer.active = False
+    gemm = GemmTimer.summary()
+    # one extra instrumented epoch for the per-phase breakdown (not part of the timed region)
+    theta, _ = engine.step(theta, seed=10_000, guidance_scale=guidance, timing=True)
+    phases = dict(engine.timings)
+    aux = aux_kernel_rooflines(engine, noiser, theta, pop, device)
+
+    value = pop * args.steps / elapsed
+    per_launch_flops = gemm["flops"] / max(gemm["launches"], 1)
+    achieved = gemm["tflops"]
+    pmc = load_pmc_traffic()
+    roofline = {"kernel": "k_lora_gemm<2> (population LoRA GEMM + fused epilogue)", "bound": "mfma",
+                "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / BF16_DENSE_PEAK_TFLOPS,
+                "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                "launches": gemm["launches"], "avg_launch_us": gemm["avg_us"],
+                "flops_per_launch": per_launch_flops}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+        cpu = cpu_baseline.run(pop=pop, budget_s=15.0)
+        cpu.pop("es_breakdown_s", None)
+        cpu.pop("wall_s", None)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "member-evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init Sana-Sprint-1.6B/DC-AE/CLIP-H/CLIP-B weights, synthetic prompt embeds)",
+            "config": {"workload": ("tiny-arch smoke (INVALID as metric)" if args.small else
+                                    "sana_sprint_1.6b_onestep_1024px_es_epoch"),
+                       "pop_per_gpu": args.pop_per_gpu, "pop_total": pop, "images_per_member": 16,
+                       "prompts_per_gen": 4, "batches_per_gen": 4, "resolution_px": 32 * args.latent,
+                       "egg_rank": 1, "lora_r": 2, "lora_alpha": 8, "theta_D": noiser.num_params,
+                       "antithetic": True, "promptnorm": True, "reward": "PickScore(CLIP-H/14)+CLIP-B/32",
+                       "parallelism": f"member-shard x{world} (S all-gather)"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "phases_ms": phases,
+            "aux_kernels": aux,
+        }
+        print(json.dumps(line), flush=True)
+        if args.aux_out:
+            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

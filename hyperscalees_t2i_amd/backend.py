@@ -1,0 +1,199 @@
+"""ES backend interface and the Sana one-step backend (es_backend.py:16-292), MI355X edition.
+
+Same duck-typed surface as the reference (`init_and_attach_lora`, `compile_if_requested`,
+`collect_lora_params`, `save_lora`, `step_sampling_info`, `generate_flat`) so a
+unifed_es.py-shaped driver runs unchanged, plus the population entry point
+`generate_population(flat_ids, seed, guidance_scale, theta_pop)` that evaluates all local
+members in one batched forward (the reference loops over members, unifed_es.py:159-163).
+Errors are Python exceptions as in the reference (FileNotFoundError / RuntimeError / ValueError).
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+
+from .es import get_trainable_params_and_shapes, repeat_batches, sample_indices_unique
+from .lora import lora_modules
+from .pipeline import SanaOneStep
+from .sana import SANA_LORA_TARGETS, SANA_SPRINT_1_6B, SanaArch, attach_lora
+
+
+class ESBackend:
+    """es_backend.py:16-57."""
+
+    name: str
+
+    def init_and_attach_lora(self) -> None:
+        raise NotImplementedError
+
+    def compile_if_requested(self) -> None:
+        pass
+
+    def collect_lora_params(self) -> Tuple[List[torch.nn.Parameter], List[Tuple[int, ...]]]:
+        raise NotImplementedError
+
+    def save_lora(self, save_dir: Path) -> None:
+        raise NotImplementedError
+
+    def step_sampling_info(self, seed: int) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float) -> List[Any]:
+        raise NotImplementedError
+
+    def generate_population(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                            theta_pop: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+
+@dataclass
+class SanaConfig:
+    """es_backend.py:64-93 (+ synthetic-data / architecture knobs of this build)."""
+
+    model_name: str = "Efficient-Large-Model/Sana_Sprint_1.6B_1024px_diffusers"
+    backend_mode: str = "one_step"
+    prompts_txt_path: str = "prompts_train"
+    encoded_prompt_path: str = ""
+    auto_encode_if_missing: bool = False
+    encode_batch_size: int = 8
+    guidance_scale: float = 4.5
+    width_latent: int = 32            # 32 -> 1024 px (BASELINE configs); reference CLI default 16 -> 512 px
+    height_latent: int = 32
+    batch_size: int = 1
+    prompts_per_gen: int = 4
+    batches_per_gen: int = 4
+    max_log_batches: int = 1
+    torch_compile: bool = False
+    compile_mode: str = "max-autotune"
+    compile_fullgraph: bool = True
+    dtype_latents: str = "float16"
+    lora_r: int = 2
+    lora_alpha: int = 8
+    lora_dropout: float = 0.0
+    lora_target_modules: List[str] = field(default_factory=lambda: list(SANA_LORA_TARGETS))
+    # build-specific
+    arch: SanaArch = field(default_factory=lambda: SANA_SPRINT_1_6B)
+    vae_widths: Tuple[int, ...] = (128, 256, 512, 512, 1024, 1024)
+    vae_layers: Tuple[int, ...] = (3, 3, 3, 3, 3, 3)
+    vae_chunk: int = 8
+    synthetic_prompts: int = 4        # used when encoded_prompt_path is empty
+    lora_b_std: float = 0.02          # nonzero B so the LoRA path is live
+    lora_seed: int = 1234
+    weight_seed: int = 0
+
+
+def synthetic_prompt_data(P: int = 4, seq: int = 300, dim: int = 2304, seed: int = 0) -> Dict[str, Any]:
+    """Same dict format as encode_prompts_from_txt.py / SanaOneStep.encode_prompts:
+    prompts, prompt_embeds [P, 300, 2304] fp16, prompt_attention_mask [P, 300] (lengths U[8, 300])."""
+    g = torch.Generator().manual_seed(seed)
+    emb = torch.randn(P, seq, dim, generator=g).to(torch.float16)
+    lens = torch.randint(8, seq + 1, (P,), generator=g)
+    mask = (torch.arange(seq)[None, :] < lens[:, None]).to(torch.int64)
+    prompts = [f"synthetic prompt {i}: a detailed photo of object {i}" for i in range(P)]
+    return {"prompts": prompts, "prompt_embeds": emb, "prompt_attention_mask": mask}
+
+
+class SanaBackend(ESBackend):
+    def __init__(self, device: str, cfg: SanaConfig):
+        if cfg.backend_mode != "one_step":
+            raise ValueError(f"Unknown/unsupported Sana backend_mode: {cfg.backend_mode} (one_step only)")
+        self.name = f"sana_{cfg.backend_mode}"
+        self.device = device
+        self.cfg = cfg
+        self.es_model: Optional[SanaOneStep] = None
+        self.prompt_data = None
+        self.base_prompt_embeds = None
+        self.base_attention_mask = None
+        self.prompts_list = None
+        self._dev_prompts = None
+
+    def _dtype(self) -> torch.dtype:
+        return torch.bfloat16 if self.cfg.dtype_latents.lower() == "bfloat16" else torch.float16
+
+    def _load_or_encode_prompts(self):
+        """es_backend.py:112-170.  Loads with weights_only=True; no text encoder offline."""
+        if self.cfg.encoded_prompt_path:
+            enc = Path(self.cfg.encoded_prompt_path)
+            if not enc.is_file():
+                raise FileNotFoundError(f"encoded_prompt_path not found and auto_encode unsupported: {enc}")
+            self.prompt_data = torch.load(enc, map_location="cpu", weights_only=True)
+        else:
+            self.prompt_data = synthetic_prompt_data(self.cfg.synthetic_prompts)
+        self.base_prompt_embeds = self.prompt_data["prompt_embeds"]
+        self.base_attention_mask = self.prompt_data["prompt_attention_mask"]
+        self.prompts_list = self.prompt_data.get("prompts", None)
+        if not torch.is_tensor(self.base_prompt_embeds):
+            raise RuntimeError("Sana expects prompt_embeds as a Tensor [P, seq, dim].")
+        if not torch.is_tensor(self.base_attention_mask):
+            raise RuntimeError("Sana expects prompt_attention_mask as a Tensor [P, seq].")
+        self._dev_prompts = (self.base_prompt_embeds.to(self.device), self.base_attention_mask.to(self.device))
+
+    def init_and_attach_lora(self):
+        self._load_or_encode_prompts()
+        c = self.cfg
+        self.es_model = SanaOneStep(c.model_name, device=self.device, DTYPE=self._dtype(), sigma_data=0.5, arch=c.arch,
+                                    vae_widths=c.vae_widths, vae_layers=c.vae_layers, weight_seed=c.weight_seed,
+                                    vae_chunk=c.vae_chunk)
+        n = attach_lora(self.es_model.transformer, c.lora_r, c.lora_alpha, c.lora_target_modules)
+        if n == 0:
+            raise RuntimeError("no LoRA target module matched")
+        g = torch.Generator(device=self.device).manual_seed(c.lora_seed)
+        for m in lora_modules(self.es_model.transformer):
+            m.reset_lora(g, b_std=c.lora_b_std)
+        self.es_model.transformer.eval()
+
+    def collect_lora_params(self):
+        return get_trainable_params_and_shapes(self.es_model.transformer)
+
+    def save_lora(self, save_dir: Path) -> None:
+        """PEFT-style adapter dir: adapter_config.json + adapter_model.safetensors
+        (keys base_model.model.<module>.lora_{A,B}.weight)."""
+        from safetensors.torch import save_file
+        save_dir = Path(save_dir)
+        save_dir.mkdir(parents=True, exist_ok=True)
+        tensors = {}
+        for name, p in self.es_model.transformer.named_parameters():
+            if p.requires_grad:
+                tensors[f"base_model.model.{name}"] = p.detach().float().cpu().contiguous()
+        save_file(tensors, str(save_dir / "adapter_model.safetensors"))
+        cfg = {"peft_type": "LORA", "r": self.cfg.lora_r, "lora_alpha": self.cfg.lora_alpha,
+               "lora_dropout": self.cfg.lora_dropout, "target_modules": list(self.cfg.lora_target_modules),
+               "base_model_name_or_path": self.cfg.model_name, "bias": "none", "task_type": None}
+        (save_dir / "adapter_config.json").write_text(json.dumps(cfg, indent=2))
+
+    def step_sampling_info(self, seed: int) -> Dict[str, Any]:
+        """es_backend.py:234-263 (bit-exact indices: np.random.RandomState(seed).choice)."""
+        P = int(self.base_prompt_embeds.shape[0])
+        unique_ids = sample_indices_unique(seed=seed, total=P, k=self.cfg.prompts_per_gen)
+        flat_ids = repeat_batches(unique_ids, repeats=self.cfg.batches_per_gen)
+        pid_to_j = {pid: j for j, pid in enumerate(unique_ids)}
+        m = len(unique_ids)
+        name = (lambda pid: self.prompts_list[pid] if self.prompts_list is not None else f"prompt_{pid}")
+        log_batches = int(max(0, min(self.cfg.max_log_batches, self.cfg.batches_per_gen)))
+        return dict(unique_ids=unique_ids, flat_ids=flat_ids, unique_texts=[name(p) for p in unique_ids],
+                    flat_texts=[name(p) for p in flat_ids], pid_to_j=pid_to_j, m=m,
+                    total_imgs_per_indiv=len(flat_ids), total_imgs_for_logging=log_batches * m,
+                    log_batches=log_batches)
+
+    def _gather(self, flat_ids):
+        pe, am = self._dev_prompts
+        idx = torch.as_tensor(flat_ids, device=pe.device)
+        return pe.index_select(0, idx), am.index_select(0, idx)
+
+    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float) -> List[Any]:
+        """es_backend.py:265-292: one member (the transformer's current LoRA params), PIL images."""
+        pe, am = self._gather(flat_ids)
+        images, _ = self.es_model.generate(prompt_embeds=pe, prompt_attention_mask=am, latents=None, seed=seed,
+                                           guidance_scale=guidance_scale, width_latent=self.cfg.width_latent,
+                                           height_latent=self.cfg.height_latent)
+        return images
+
+    def generate_population(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                            theta_pop: torch.Tensor) -> torch.Tensor:
+        pe, am = self._gather(flat_ids)
+        return self.es_model.generate_population(pe, am, theta_pop, seed, guidance_scale, self.cfg.width_latent,
+                                                 self.cfg.height_latent)

@@ -311,31 +311,26 @@ int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta
     return EGGROLL_OK;
 }
 
-int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
-                            const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
-                            float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
-                            int64_t ldy, float* T_ws, void* stream) {
-    EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0, "lora_linear_pop: bad sizes M=%lld N=%lld K=%lld", (long long)M,
-                  (long long)N, (long long)K);
-    EGG_CHECK_ARG(K % 64 == 0, "lora_linear_pop: K=%lld must be a multiple of 64", (long long)K);
-    EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop: bad strides");
-    EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_linear_pop: r=%d out of range", r);
-    EGG_CHECK_ARG(rows_per_member > 0, "lora_linear_pop: rows_per_member must be > 0");
+int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                      const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                      int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, void* stream) {
+    EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0, "lora_gemm: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
+                  (long long)K);
+    EGG_CHECK_ARG(K % 64 == 0, "lora_gemm: K=%lld must be a multiple of 64", (long long)K);
+    EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_gemm: bad strides");
+    EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_gemm: r=%d out of range", r);
+    EGG_CHECK_ARG(rows_per_member > 0, "lora_gemm: rows_per_member must be > 0");
+    EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_gemm: M/N too large");
     const int64_t tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_linear_pop: grid too large");
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_gemm: grid too large");
     if (M == 0) return EGGROLL_OK;
-    EGG_CHECK_ARG(X && W && Y, "lora_linear_pop: NULL pointer");
+    EGG_CHECK_ARG(X && W && Y, "lora_gemm: NULL pointer");
+    EGG_CHECK_ARG(r == 0 || (T && theta_pop), "lora_gemm: T / theta_pop NULL with r > 0");
     hipStream_t st = as_stream(stream);
-    if (r > 0) {
-        EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop: theta_pop / T_ws NULL with r > 0");
-        int rc = eggroll_lora_project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T_ws, stream);
-        if (rc) return rc;
-    }
-    EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_linear_pop: M/N too large");
     const dim3 grid((unsigned)(tiles_m * tiles_n));
 #define EGG_GEMM(RV)                                                                                              \
     hipLaunchKernelGGL(k_lora_gemm<RV>, grid, dim3(256), 0, st, (const unsigned short*)X, ldx,                 \
-                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T_ws, theta_pop, ld_theta,   \
+                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T, theta_pop, ld_theta,      \
                        offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy)
     switch (r) {
         case 0: EGG_GEMM(0); break;
@@ -345,11 +340,27 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
         case 4: EGG_GEMM(4); break;
         case 8: EGG_GEMM(8); break;
         case 16: EGG_GEMM(16); break;
-        default: set_error("lora_linear_pop: r=%d unsupported (0,1,2,3,4,8,16)", r); return EGGROLL_ERR_UNSUPPORTED;
+        default: set_error("lora_gemm: r=%d unsupported (0,1,2,3,4,8,16)", r); return EGGROLL_ERR_UNSUPPORTED;
     }
 #undef EGG_GEMM
     EGG_CHECK_LAUNCH("lora_gemm");
     return EGGROLL_OK;
+}
+
+int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                            const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                            float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                            int64_t ldy, float* T_ws, void* stream) {
+    EGG_CHECK_ARG(K > 0 && K % 64 == 0, "lora_linear_pop: K=%lld must be a multiple of 64", (long long)K);
+    EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_linear_pop: r=%d out of range", r);
+    if (M == 0) return EGGROLL_OK;
+    if (r > 0) {
+        EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop: theta_pop / T_ws NULL with r > 0");
+        int rc = eggroll_lora_project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T_ws, stream);
+        if (rc) return rc;
+    }
+    return eggroll_lora_gemm(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K,
+                             Y, ldy, stream);
 }
 
 }  // extern "C"

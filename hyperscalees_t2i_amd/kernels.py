@@ -232,6 +232,23 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
     return out
 
 
+def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T: Optional[torch.Tensor],
+              theta_pop: Optional[torch.Tensor], offB: int, r: int, scale: float, rows_per_member: int,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The MFMA GEMM + fused LoRA epilogue alone, given T = X A_k^T (from lora_project)."""
+    _dev(x, "lora_gemm(x)", torch.bfloat16)
+    _dev(W, "lora_gemm(W)", torch.bfloat16)
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    ld_t = theta_pop.stride(0) if (r > 0 and theta_pop is not None) else 0
+    _lib.call("eggroll_lora_gemm", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
+              _p(T) if r > 0 else None, _p(theta_pop) if r > 0 else None, ld_t, offB, r, float(scale),
+              rows_per_member, M, N, K, out.data_ptr(), out.stride(0), _stream(x.device))
+    return out
+
+
 def lora_project(x: torch.Tensor, theta_pop: torch.Tensor, offA: int, r: int, rows_per_member: int,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _dev(x, "lora_project(x)", torch.bfloat16)

@@ -1,0 +1,165 @@
+"""Population-aware LoRA linear — the drop-in for PEFT `lora.Linear` on the ES hot path.
+
+Reference: PEFT LoRA injected by `get_peft_model(transformer, LoraConfig(r, alpha, dropout,
+target_modules))` (es_backend.py:193-200); forward `y = base(x) + lora_B(lora_A(dropout(x))) *
+alpha/r` with `lora_A.weight [r, in]`, `lora_B.weight [out, r]` (peft.tuners.lora.layer.Linear;
+third-party, unpinned, not vendored — the formula is restated, see oracle.ref_lora_linear).
+
+Two modes:
+  * single-member (reference semantics): uses this module's own lora_A / lora_B parameters,
+    i.e. whatever `unflatten_to_params` last wrote into them;
+  * population (engine): a shared `PopulationContext` holds theta_pop [n_members, D] (fp32,
+    one perturbed theta_k per member, written by the perturb kernel) and the rows of x are
+    member-major; one eggroll_lora_linear_pop call evaluates every member, reading the frozen
+    base weight through LDS once per tile for all members.
+The base weight / bias are frozen bf16 (requires_grad=False, like PEFT's base_layer), so
+`get_trainable_params_and_shapes` sees exactly (lora_A, lora_B) per layer in module order —
+the reference theta layout (utills.py:141-152).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Iterable, List, Optional
+
+import torch
+from torch import nn
+
+from . import kernels as K
+
+
+@dataclass
+class PopulationContext:
+    theta_pop: Optional[torch.Tensor] = None  # [n_members, ld] fp32 (perturbed theta per member)
+    n_members: int = 1
+    T_ws: Optional[torch.Tensor] = None       # reusable fp32 workspace for T = X A_k^T
+
+    def workspace(self, numel: int, device) -> torch.Tensor:
+        if self.T_ws is None or self.T_ws.numel() < numel or self.T_ws.device != torch.device(device):
+            self.T_ws = torch.empty(max(numel, 1), dtype=torch.float32, device=device)
+        return self.T_ws
+
+
+class GemmTimer:
+    """Opt-in live timing of every population LoRA GEMM launch with HIP events recorded on the
+    launching stream (bench.py's roofline leg).  Records (start, end, M, N, K, r)."""
+
+    active = False
+    records: List[tuple] = []
+
+    @classmethod
+    def reset(cls, active: bool):
+        cls.active, cls.records = active, []
+
+    @classmethod
+    def summary(cls) -> Dict[str, float]:
+        torch.cuda.synchronize()
+        ms = flops = 0.0
+        for s, e, M, N, Kd, r in cls.records:
+            ms += s.elapsed_time(e)
+            flops += 2.0 * M * N * Kd + 2.0 * M * N * r  # base GEMM + rank-r epilogue
+        n = len(cls.records)
+        return {"launches": n, "total_ms": ms, "flops": flops,
+                "avg_us": 1e3 * ms / n if n else float("nan"),
+                "tflops": flops / (ms * 1e9) if ms > 0 else float("nan")}
+
+
+class _Weight(nn.Module):
+    """Holder so parameter names read `...lora_A.weight` / `...lora_B.weight` (PEFT naming)."""
+
+    def __init__(self, shape):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(*shape, dtype=torch.float32))
+
+
+class LoRALinear(nn.Module):
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, r: int = 2, alpha: float = 8.0,
+                 lora: bool = True):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features, dtype=torch.bfloat16), requires_grad=False)
+        self.bias = (nn.Parameter(torch.zeros(out_features, dtype=torch.bfloat16), requires_grad=False)
+                     if bias else None)
+        self.r = r if lora else 0
+        self.scale = float(alpha) / r if lora else 0.0
+        if lora:
+            self.lora_A = _Weight((r, in_features))
+            self.lora_B = _Weight((out_features, r))
+        self.ctx: Optional[PopulationContext] = None
+        self.theta_off_A = -1  # element offsets of lora_A / lora_B inside theta (set by bind_theta_layout)
+        self.theta_off_B = -1
+
+    def reset_lora(self, gen: Optional[torch.Generator] = None, b_std: float = 0.0):
+        """PEFT default init: A ~ kaiming_uniform(a=sqrt(5)), B = 0 (b_std > 0: N(0, b_std), used by
+        the benchmark so the LoRA path carries signal — SURVEY §8d)."""
+        if not self.r:
+            return
+        bound = 1.0 / math.sqrt(self.in_features)  # kaiming_uniform_(a=sqrt(5)) on fan_in
+        with torch.no_grad():
+            self.lora_A.weight.uniform_(-bound, bound, generator=gen)
+            if b_std > 0:
+                self.lora_B.weight.normal_(0.0, b_std, generator=gen)
+            else:
+                self.lora_B.weight.zero_()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if x2.dtype != torch.bfloat16:
+            x2 = x2.to(torch.bfloat16)
+        x2 = x2.contiguous()
+        M = x2.shape[0]
+        ctx = self.ctx
+        if self.r and ctx is not None and ctx.theta_pop is not None:
+            if M % ctx.n_members:
+                raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")
+            rpm = M // ctx.n_members
+            T = ctx.workspace(M * self.r, x2.device)[: M * self.r].view(M, self.r)
+            K.lora_project(x2, ctx.theta_pop, self.theta_off_A, self.r, rpm, out=T)
+            if GemmTimer.active:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            y = K.lora_gemm(x2, self.weight, self.bias, T, ctx.theta_pop, self.theta_off_B, self.r, self.scale, rpm)
+            if GemmTimer.active:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                GemmTimer.records.append((e0, e1, M, self.out_features, self.in_features, self.r))
+        elif self.r:
+            # single member: this module's own (unflattened) lora_A / lora_B
+            A = self.lora_A.weight.detach()
+            B = self.lora_B.weight.detach()
+            if A.device != x2.device:
+                raise RuntimeError("LoRA parameters and input on different devices")
+            y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
+            T = K.lora_project(x2, A.contiguous().view(1, -1), 0, self.r, M)
+            K.lora_expand(T, B.contiguous().view(1, -1), 0, self.r, self.scale, M, y)
+        else:
+            y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
+        return y.view(*shp[:-1], self.out_features)
+
+
+def lora_modules(model: nn.Module) -> List[LoRALinear]:
+    return [m for m in model.modules() if isinstance(m, LoRALinear) and m.r]
+
+
+def bind_theta_layout(model: nn.Module) -> Dict[str, int]:
+    """Record each LoRA module's (lora_A, lora_B) offsets inside theta, following the trainable
+    parameter order of model.parameters() (utills.py:141-152).  Returns {param_name: offset}."""
+    offs, off = {}, 0
+    by_param = {}
+    for name, p in model.named_parameters():
+        if p.requires_grad:
+            offs[name] = off
+            by_param[id(p)] = off
+            off += p.numel()
+    for m in lora_modules(model):
+        m.theta_off_A = by_param[id(m.lora_A.weight)]
+        m.theta_off_B = by_param[id(m.lora_B.weight)]
+        if m.theta_off_A % 4:
+            raise RuntimeError("lora_A offset inside theta must be 16-byte aligned for the project kernel")
+    return offs
+
+
+def set_population(model: nn.Module, ctx: Optional[PopulationContext]) -> None:
+    for m in lora_modules(model):
+        m.ctx = ctx

@@ -1,0 +1,152 @@
+"""Reward contract of the reference (rewards.py:164-268), batched over all images of all local
+members and kept on the GPU (no PIL round trip, no per-image model calls).
+
+Per image the reference computes (compute_all_rewards, called once per image at
+unifed_es.py:175-191):
+  clip_aesthetic = (cos(img, AESTHETIC_TEXT) + 1) / 2           CLIP ViT-B/32
+  clip_text      = (cos(img, prompt) + 1) / 2                   CLIP ViT-B/32
+  no_artifacts   = 1 - (cos(img, NEGATIVE_TEXT) + 1) / 2        CLIP ViT-B/32
+  pickscore      = exp(logit_scale) * cos(text_emb, img_emb)    PickScore_v1 (CLIP ViT-H/14)
+  combined       = w_aes*aes + w_txt*txt + w_noart*noart + w_pick*pick
+Images reach the reward models as the reference's PIL path would deliver them: VAE output ->
+(x/2+0.5).clamp(0,1) -> *255 rounded to uint8 (PixArtImageProcessor.postprocess) -> CLIP fast
+processor: bicubic antialiased resize of the shortest edge to 224 -> center crop -> /255 ->
+CLIP mean/std normalisation.  Done here as tensor ops on the device.
+
+Weights: the hub checkpoints (openai/clip-vit-base-patch32, yuvalkirstain/PickScore_v1) are not
+available offline, so both models are built from their published configs with seeded random
+init (architecture- and FLOP-exact, scores meaningless); tokenisation is a deterministic
+synthetic word hash (no CLIP BPE vocab offline).  Reward-value parity is therefore UNPINNED;
+the reward *contract* (dict keys, per-image scalars, combination, S aggregation) is exact.
+"""
+from __future__ import annotations
+
+import zlib
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+AESTHETIC_TEXT = "a high quality, professional, beautiful, aesthetically pleasing image"
+NEGATIVE_TEXT = "blurry, low resolution, noisy, pixelated, washed out colors, oversaturated "
+CLIP_MEAN = (0.48145466, 0.4578275, 0.40821073)
+CLIP_STD = (0.26862954, 0.26130258, 0.27577711)
+
+CLIP_B32 = dict(
+    text_config=dict(hidden_size=512, intermediate_size=2048, num_hidden_layers=12, num_attention_heads=8,
+                     max_position_embeddings=77, vocab_size=49408, hidden_act="quick_gelu"),
+    vision_config=dict(hidden_size=768, intermediate_size=3072, num_hidden_layers=12, num_attention_heads=12,
+                       image_size=224, patch_size=32, hidden_act="quick_gelu"),
+    projection_dim=512)
+CLIP_H14 = dict(  # laion/CLIP-ViT-H-14-laion2B-s32B-b79K == PickScore_v1 architecture
+    text_config=dict(hidden_size=1024, intermediate_size=4096, num_hidden_layers=24, num_attention_heads=16,
+                     max_position_embeddings=77, vocab_size=49408, hidden_act="gelu"),
+    vision_config=dict(hidden_size=1280, intermediate_size=5120, num_hidden_layers=32, num_attention_heads=16,
+                       image_size=224, patch_size=14, hidden_act="gelu"),
+    projection_dim=1024)
+CLIP_TINY = dict(  # test-size config
+    text_config=dict(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                     max_position_embeddings=77, vocab_size=49408, hidden_act="quick_gelu"),
+    vision_config=dict(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                       image_size=224, patch_size=32, hidden_act="quick_gelu"),
+    projection_dim=32)
+
+
+def synthetic_tokenize(texts: Sequence[str], max_length: int = 77) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Deterministic stand-in for the CLIP BPE tokenizer: BOS + crc32(word) ids + EOS, padded."""
+    ids = torch.zeros(len(texts), max_length, dtype=torch.long)
+    mask = torch.zeros(len(texts), max_length, dtype=torch.long)
+    for i, t in enumerate(texts):
+        toks = [49406] + [1 + zlib.crc32(w.encode()) % 49000 for w in t.lower().split()][: max_length - 2] + [49407]
+        ids[i, :len(toks)] = torch.tensor(toks)
+        mask[i, :len(toks)] = 1
+        ids[i, len(toks):] = 49407
+    return ids, mask
+
+
+def postprocess_uint8(images: torch.Tensor) -> torch.Tensor:
+    """PixArtImageProcessor.postprocess(output_type='pil') pixel values, as float tensor of ints."""
+    return torch.round((images.float() / 2 + 0.5).clamp(0, 1) * 255.0)
+
+
+def clip_preprocess(u8: torch.Tensor, size: int = 224) -> torch.Tensor:
+    """CLIP fast image processor on uint8-valued images [n,3,H,W] -> normalized [n,3,224,224]."""
+    n, c, h, w = u8.shape
+    s = size / min(h, w)
+    nh, nw = max(size, round(h * s)), max(size, round(w * s))
+    x = F.interpolate(u8.float(), size=(nh, nw), mode="bicubic", antialias=True, align_corners=False)
+    x = torch.round(x).clamp(0, 255)
+    top, left = (nh - size) // 2, (nw - size) // 2
+    x = x[:, :, top:top + size, left:left + size] / 255.0
+    mean = torch.tensor(CLIP_MEAN, device=x.device).view(1, 3, 1, 1)
+    std = torch.tensor(CLIP_STD, device=x.device).view(1, 3, 1, 1)
+    return (x - mean) / std
+
+
+def build_clip(cfg: dict, device, seed: int, dtype=torch.bfloat16):
+    from transformers import CLIPConfig, CLIPModel
+    torch.manual_seed(seed)
+    with torch.device(device):
+        model = CLIPModel(CLIPConfig(**cfg))
+    return model.to(dtype).eval().requires_grad_(False)
+
+
+def _image_features(model, pixels: torch.Tensor) -> torch.Tensor:
+    out = model.vision_model(pixel_values=pixels.to(model.dtype))
+    return model.visual_projection(out.pooler_output).float()
+
+
+def _text_features(model, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    out = model.text_model(input_ids=ids, attention_mask=mask)
+    return model.text_projection(out.pooler_output).float()
+
+
+@dataclass
+class RewardModels:
+    clip: object
+    pick: object
+    mix_weights: Tuple[float, float, float, float] = (0.0, 0.0, 0.0, 1.0)  # unifed_es.py:360-363 defaults
+    image_batch: int = 64
+
+    @classmethod
+    def build(cls, device, mix_weights=(0.0, 0.0, 0.0, 1.0), tiny: bool = False, seed: int = 7):
+        clip = build_clip(CLIP_TINY if tiny else CLIP_B32, device, seed)
+        pick = build_clip(CLIP_TINY if tiny else CLIP_H14, device, seed + 1)
+        return cls(clip=clip, pick=pick, mix_weights=tuple(mix_weights))
+
+    @torch.no_grad()
+    def prompt_features(self, prompts: Sequence[str]) -> Dict[str, torch.Tensor]:
+        """Text features once per epoch (members share prompts: common random numbers)."""
+        dev = next(self.clip.parameters()).device
+        ids, mask = synthetic_tokenize([AESTHETIC_TEXT, NEGATIVE_TEXT] + list(prompts))
+        ids, mask = ids.to(dev), mask.to(dev)
+        t_clip = _text_features(self.clip, ids, mask)
+        t_clip = t_clip / t_clip.norm(dim=-1, keepdim=True).clamp_min(1e-6)   # rewards.py:100
+        t_pick = _text_features(self.pick, ids[2:], mask[2:])
+        t_pick = t_pick / t_pick.norm(dim=-1, keepdim=True)                   # rewards.py:153
+        return {"clip_aes": t_clip[0], "clip_neg": t_clip[1], "clip_prompt": t_clip[2:], "pick_prompt": t_pick}
+
+    @torch.no_grad()
+    def score(self, images: torch.Tensor, prompt_index: torch.Tensor, feats: Dict[str, torch.Tensor]
+              ) -> Dict[str, torch.Tensor]:
+        """images: VAE outputs [n,3,H,W] in [-1,1]; prompt_index [n] into feats' prompt rows.
+        Returns per-image fp32 tensors with the compute_all_rewards keys."""
+        n = images.shape[0]
+        e_clip, e_pick = [], []
+        for s in range(0, n, self.image_batch):
+            px = clip_preprocess(postprocess_uint8(images[s:s + self.image_batch]))
+            e_clip.append(_image_features(self.clip, px))
+            e_pick.append(_image_features(self.pick, px))
+        ic = torch.cat(e_clip)
+        ic = ic / ic.norm(dim=-1, keepdim=True).clamp_min(1e-6)  # rewards.py:99
+        ip = torch.cat(e_pick)
+        ip = ip / ip.norm(dim=-1, keepdim=True)                   # rewards.py:150
+        aes = (ic @ feats["clip_aes"] + 1.0) / 2.0
+        txt = ((ic * feats["clip_prompt"][prompt_index]).sum(-1) + 1.0) / 2.0
+        neg = (ic @ feats["clip_neg"] + 1.0) / 2.0
+        noart = 1.0 - neg
+        pick = self.pick.logit_scale.float().exp() * (ip * feats["pick_prompt"][prompt_index]).sum(-1)
+        w_aes, w_txt, w_no, w_pick = self.mix_weights
+        comb = w_aes * aes + w_txt * txt + w_no * noart + w_pick * pick
+        return {"clip_aesthetic": aes, "clip_text": txt, "no_artifacts": noart, "pickscore": pick, "combined": comb}

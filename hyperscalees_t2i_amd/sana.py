@@ -1,0 +1,273 @@
+"""Sana-Sprint transformer (SanaTransformer2DModel, Sana_Sprint_1.6B_1024px config) — the host
+module of the perturbed LoRA linears, bf16, token-major (channels-last) throughout.
+
+Reference: the reference loads `diffusers.SanaTransformer2DModel.from_pretrained(
+"Efficient-Large-Model/Sana_Sprint_1.6B_1024px_diffusers", subfolder="transformer")` in fp32
+(models/SanaSprint.py:35-39) and wraps it with PEFT.  diffusers is not installed and no weights
+exist offline, so this is a from-scratch restatement of the published architecture (20 blocks,
+hidden 2240 = 70 heads x 32, ReLU linear self-attention, 20 x 112 softmax cross-attention,
+GLUMBConv FFN with mlp_ratio 2.5, AdaLN-single modulation with guidance embedding, RMS q/k norm
+across heads).  Parity with diffusers numerics is UNPINNED (no weights / no diffusers here);
+shapes, FLOPs and the LoRA target set (168 linears, D = 1,515,456 at r=2) are exact.
+
+Non-LoRA ops run on PyTorch-ROCm (hipBLASLt GEMMs for the 1x1 convs, MIOpen depthwise conv,
+SDPA); every LoRA target runs through libeggroll's population kernel.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .lora import LoRALinear, bind_theta_layout
+
+
+@dataclass
+class SanaArch:
+    in_channels: int = 32
+    out_channels: int = 32
+    num_attention_heads: int = 70
+    attention_head_dim: int = 32
+    num_layers: int = 20
+    num_cross_attention_heads: int = 20
+    cross_attention_head_dim: int = 112
+    caption_channels: int = 2304
+    mlp_ratio: float = 2.5
+    norm_eps: float = 1e-6
+    guidance_embeds_scale: float = 0.1
+    sample_size: int = 32
+
+    @property
+    def inner_dim(self) -> int:
+        return self.num_attention_heads * self.attention_head_dim
+
+
+SANA_SPRINT_1_6B = SanaArch()
+SANA_LORA_TARGETS = ["to_q", "to_k", "to_v", "to_out.0", "linear_1", "linear_2", "proj_out", "linear"]  # unifed_es.py:391
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-5, bias: bool = False):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim, dtype=torch.bfloat16), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(dim, dtype=torch.bfloat16), requires_grad=False) if bias else None
+
+    def forward(self, x):
+        x = F.rms_norm(x, (x.shape[-1],), self.weight, self.eps)
+        return x + self.bias if self.bias is not None else x
+
+
+def timestep_embedding(t: torch.Tensor, dim: int = 256, max_period: float = 10000.0) -> torch.Tensor:
+    """diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0)."""
+    half = dim // 2
+    exponent = -math.log(max_period) * torch.arange(half, dtype=torch.float32, device=t.device) / half
+    emb = t.float()[:, None] * torch.exp(exponent)[None, :]
+    return torch.cat([torch.cos(emb), torch.sin(emb)], dim=-1)
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, in_dim: int, dim: int):
+        super().__init__()
+        self.linear_1 = LoRALinear(in_dim, dim, lora=False)
+        self.linear_2 = LoRALinear(dim, dim, lora=False)
+
+    def forward(self, x):
+        return self.linear_2(F.silu(self.linear_1(x)))
+
+
+class CombinedTimestepGuidanceEmbeddings(nn.Module):
+    """SanaCombinedTimestepGuidanceEmbeddings: returns (6*D modulation, D embedded timestep)."""
+
+    def __init__(self, dim: int):
+        super().__init__()
+        self.timestep_embedder = TimestepEmbedding(256, dim)
+        self.guidance_embedder = TimestepEmbedding(256, dim)
+        self.linear = LoRALinear(dim, 6 * dim, lora=False)
+
+    def forward(self, timestep, guidance):
+        t = self.timestep_embedder(timestep_embedding(timestep).to(torch.bfloat16))
+        g = self.guidance_embedder(timestep_embedding(guidance).to(torch.bfloat16))
+        cond = t + g
+        return self.linear(F.silu(cond)), cond
+
+
+class TextProjection(nn.Module):
+    """PixArtAlphaTextProjection: linear_1 -> GELU(tanh) -> linear_2."""
+
+    def __init__(self, in_features: int, hidden: int):
+        super().__init__()
+        self.linear_1 = LoRALinear(in_features, hidden, lora=False)
+        self.linear_2 = LoRALinear(hidden, hidden, lora=False)
+
+    def forward(self, x):
+        return self.linear_2(F.gelu(self.linear_1(x), approximate="tanh"))
+
+
+class LinearSelfAttention(nn.Module):
+    """attn1 with SanaLinearAttnProcessor2_0 (ReLU kernel, fp32 accumulation)."""
+
+    def __init__(self, dim: int, heads: int, head_dim: int, eps: float = 1e-5):
+        super().__init__()
+        self.heads, self.head_dim = heads, head_dim
+        inner = heads * head_dim
+        self.norm_q = RMSNorm(inner, eps)
+        self.norm_k = RMSNorm(inner, eps)
+        self.to_q = LoRALinear(dim, inner, bias=False, lora=False)
+        self.to_k = LoRALinear(dim, inner, bias=False, lora=False)
+        self.to_v = LoRALinear(dim, inner, bias=False, lora=False)
+        self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
+
+    def forward(self, x):  # x [B, N, D]
+        B, N, _ = x.shape
+        q = F.relu(self.norm_q(self.to_q(x))).view(B, N, self.heads, self.head_dim).float()
+        k = F.relu(self.norm_k(self.to_k(x))).view(B, N, self.heads, self.head_dim).float()
+        v = self.to_v(x).view(B, N, self.heads, self.head_dim).float()
+        kv = torch.einsum("bnhj,bnhi->bhji", k, v)                 # [B, H, d, d] = sum_n k v^T
+        ksum = k.sum(dim=1)                                         # [B, H, d]
+        num = torch.einsum("bnhj,bhji->bnhi", q, kv)
+        den = torch.einsum("bnhj,bhj->bnh", q, ksum).unsqueeze(-1)
+        out = (num / (den + 1e-15)).reshape(B, N, -1).to(torch.bfloat16)
+        return self.to_out[0](out)
+
+
+class CrossAttention(nn.Module):
+    """attn2: softmax cross-attention over the 300 caption tokens (SanaAttnProcessor2_0)."""
+
+    def __init__(self, dim: int, heads: int, head_dim: int, eps: float = 1e-5):
+        super().__init__()
+        self.heads, self.head_dim = heads, head_dim
+        inner = heads * head_dim
+        self.norm_q = RMSNorm(inner, eps)
+        self.norm_k = RMSNorm(inner, eps)
+        self.to_q = LoRALinear(dim, inner, bias=True, lora=False)
+        self.to_k = LoRALinear(dim, inner, bias=True, lora=False)
+        self.to_v = LoRALinear(dim, inner, bias=True, lora=False)
+        self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
+
+    def forward(self, x, enc, mask_bias):  # x [B,N,D], enc [B,L,D], mask_bias [B,1,1,L]
+        B, N, _ = x.shape
+        L = enc.shape[1]
+        q = self.norm_q(self.to_q(x)).view(B, N, self.heads, self.head_dim).transpose(1, 2)
+        k = self.norm_k(self.to_k(enc)).view(B, L, self.heads, self.head_dim).transpose(1, 2)
+        v = self.to_v(enc).view(B, L, self.heads, self.head_dim).transpose(1, 2)
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask_bias)
+        return self.to_out[0](o.transpose(1, 2).reshape(B, N, -1))
+
+
+class GLUMBConv(nn.Module):
+    """1x1 conv -> SiLU -> 3x3 depthwise -> GLU(SiLU gate) -> 1x1 conv (token-major layout)."""
+
+    def __init__(self, dim: int, hidden: int):
+        super().__init__()
+        self.hidden = hidden
+        self.w_inv = nn.Parameter(torch.empty(2 * hidden, dim, dtype=torch.bfloat16), requires_grad=False)
+        self.b_inv = nn.Parameter(torch.zeros(2 * hidden, dtype=torch.bfloat16), requires_grad=False)
+        self.w_dw = nn.Parameter(torch.empty(2 * hidden, 1, 3, 3, dtype=torch.bfloat16), requires_grad=False)
+        self.b_dw = nn.Parameter(torch.zeros(2 * hidden, dtype=torch.bfloat16), requires_grad=False)
+        self.w_point = nn.Parameter(torch.empty(dim, hidden, dtype=torch.bfloat16), requires_grad=False)
+
+    def forward(self, x, H: int, W: int):  # x [B, N, D]
+        B, N, _ = x.shape
+        h = F.silu(F.linear(x, self.w_inv, self.b_inv))                      # [B, N, 2h]
+        h = h.view(B, H, W, -1).permute(0, 3, 1, 2)                          # NCHW view, channels-last strides
+        h = F.conv2d(h, self.w_dw, self.b_dw, padding=1, groups=2 * self.hidden)
+        h = h.permute(0, 2, 3, 1).reshape(B, N, -1)
+        a, gate = h.chunk(2, dim=-1)
+        return F.linear(a * F.silu(gate), self.w_point)
+
+
+class SanaBlock(nn.Module):
+    def __init__(self, a: SanaArch):
+        super().__init__()
+        D = a.inner_dim
+        self.eps = a.norm_eps
+        self.attn1 = LinearSelfAttention(D, a.num_attention_heads, a.attention_head_dim)
+        self.attn2 = CrossAttention(D, a.num_cross_attention_heads, a.cross_attention_head_dim)
+        self.ff = GLUMBConv(D, int(a.mlp_ratio * D))
+        self.scale_shift_table = nn.Parameter(torch.randn(6, D).div(D ** 0.5).to(torch.bfloat16), requires_grad=False)
+
+    def forward(self, x, enc, mask_bias, timestep, H, W):
+        B = x.shape[0]
+        mods = (self.scale_shift_table[None] + timestep.view(B, 6, -1)).chunk(6, dim=1)
+        shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp = mods
+        n = F.layer_norm(x, (x.shape[-1],), eps=self.eps)
+        n = n * (1 + scale_msa) + shift_msa
+        x = x + gate_msa * self.attn1(n)
+        x = x + self.attn2(x, enc, mask_bias)
+        n = F.layer_norm(x, (x.shape[-1],), eps=self.eps)
+        n = n * (1 + scale_mlp) + shift_mlp
+        return x + gate_mlp * self.ff(n, H, W)
+
+
+class SanaTransformer2DModel(nn.Module):
+    def __init__(self, a: SanaArch = SANA_SPRINT_1_6B):
+        super().__init__()
+        self.config = a
+        D = a.inner_dim
+        # module registration order follows diffusers (theta layout = parameter order)
+        self.patch_w = nn.Parameter(torch.empty(D, a.in_channels, dtype=torch.bfloat16), requires_grad=False)
+        self.patch_b = nn.Parameter(torch.zeros(D, dtype=torch.bfloat16), requires_grad=False)
+        self.time_embed = CombinedTimestepGuidanceEmbeddings(D)
+        self.caption_projection = TextProjection(a.caption_channels, D)
+        self.caption_norm = RMSNorm(D, 1e-5)
+        self.transformer_blocks = nn.ModuleList([SanaBlock(a) for _ in range(a.num_layers)])
+        self.scale_shift_table = nn.Parameter(torch.randn(2, D).div(D ** 0.5).to(torch.bfloat16), requires_grad=False)
+        self.proj_out = LoRALinear(D, a.out_channels, lora=False)
+
+    @torch.no_grad()
+    def init_weights(self, seed: int = 0):
+        """Synthetic frozen weights (no checkpoints offline): N(0, 1/fan_in) so activations stay O(1)."""
+        g = torch.Generator(device=self.patch_w.device).manual_seed(seed)
+        for name, p in self.named_parameters():
+            if p.requires_grad:
+                continue
+            if name.endswith("scale_shift_table"):
+                p.copy_(torch.randn(p.shape, generator=g, device=p.device).div(p.shape[-1] ** 0.5))
+            elif p.ndim >= 2:
+                fan_in = p[0].numel()
+                std = 1.0 / math.sqrt(fan_in)
+                if name.endswith("to_out.0.weight") or name.endswith("w_point") or "proj_out" in name:
+                    std *= 0.5
+                p.copy_(torch.randn(p.shape, generator=g, device=p.device) * std)
+            elif name.endswith("weight"):
+                p.fill_(1.0)
+            else:
+                p.zero_()
+
+    def forward(self, hidden_states, timestep, encoder_hidden_states, encoder_attention_mask, guidance):
+        B, C, H, W = hidden_states.shape
+        a = self.config
+        x = hidden_states.to(torch.bfloat16).permute(0, 2, 3, 1).reshape(B, H * W, C)
+        x = F.linear(x, self.patch_w, self.patch_b)                                   # PatchEmbed (p = 1)
+        timestep6, emb_t = self.time_embed(timestep, guidance)
+        enc = self.caption_projection(encoder_hidden_states.to(torch.bfloat16))
+        enc = self.caption_norm(enc)
+        mask_bias = ((1.0 - encoder_attention_mask.to(torch.bfloat16)) * -10000.0).view(B, 1, 1, -1)
+        for blk in self.transformer_blocks:
+            x = blk(x, enc, mask_bias, timestep6, H, W)
+        shift, scale = (self.scale_shift_table[None] + emb_t[:, None]).chunk(2, dim=1)
+        x = F.layer_norm(x, (x.shape[-1],), eps=a.norm_eps) * (1 + scale) + shift
+        x = self.proj_out(x)
+        return x.view(B, H, W, a.out_channels).permute(0, 3, 1, 2)
+
+
+def attach_lora(model: nn.Module, r: int, alpha: float, targets: Sequence[str]) -> int:
+    """get_peft_model equivalent (es_backend.py:193-200): enable LoRA on every LoRALinear whose
+    qualified name equals or ends with '.<target>' (PEFT suffix matching)."""
+    n = 0
+    for name, m in model.named_modules():
+        if isinstance(m, LoRALinear) and any(name == t or name.endswith("." + t) for t in targets):
+            dev = m.weight.device
+            m.r, m.scale = r, float(alpha) / r
+            m.lora_A = nn.Module()
+            m.lora_A.weight = nn.Parameter(torch.zeros(r, m.in_features, device=dev))
+            m.lora_B = nn.Module()
+            m.lora_B.weight = nn.Parameter(torch.zeros(m.out_features, r, device=dev))
+            n += 1
+    bind_theta_layout(model)
+    return n

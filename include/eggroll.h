@@ -128,7 +128,12 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
                             void* Y, int64_t ldy, float* T_ws, void* stream);
 
 /* Pieces of (2), exported for A/B measurement and for hosts that run the base GEMM
- * elsewhere:  T = X Ak^T per member (fp32), and Y += scale * T Bk^T (bf16 in place).   */
+ * elsewhere:  T = X Ak^T per member (fp32); the MFMA GEMM + fused epilogue given T
+ * (T may be NULL when r == 0); and Y += scale * T Bk^T (bf16 in place).                  */
+int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                      const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
+                      int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
+                      int64_t K, void* Y, int64_t ldy, void* stream);
 int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
                          int64_t offA, int32_t r, int64_t rows_per_member, int64_t M, int64_t K,
                          float* T, void* stream);
