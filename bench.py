@@ -26,12 +26,13 @@ import sys
 import time
 from pathlib import Path
 
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 import torch  # noqa: E402
+
+torch.backends.cudnn.benchmark = True  # MIOpen Find per conv shape during warmup (FAST mode: 38 vs 700+ TF)
 
 METRIC = "ES member-evals/sec (whole node) Sana-Sprint 1.6B pop=64; % HBM/MFMA roofline"
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16

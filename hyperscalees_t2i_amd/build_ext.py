@@ -16,7 +16,7 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 BUILD = PKG / "_build"
 LIB = BUILD / "libeggroll.so"
-SOURCES = ["eggroll_es.hip", "eggroll_lora.hip"]
+SOURCES = ["eggroll_es.hip", "eggroll_lora.hip", "eggroll_model.hip"]
 ARCH = "gfx950"
 
 

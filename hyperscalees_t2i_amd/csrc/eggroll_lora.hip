@@ -66,27 +66,46 @@ __global__ __launch_bounds__(256) void k_lora_project(const unsigned short* __re
 }
 
 // ------------------------------------------------------------------------------------
-// Base GEMM + fused LoRA epilogue.
+// Base GEMM + fused LoRA epilogue, templated on the tile:
+//   Tile<BM, BN, WM, WN>: BM x BN output tile, BK = 64, WM x WN waves (wave tile (BM/WM) x (BN/WN)),
+//   2 LDS stages of (BM + BN) rows x 128 B, one barrier per K-tile: the global_load_lds of K-tile
+//   k+1 is issued right after the barrier and lands while the MFMAs of K-tile k run.
+//   kT128: 128x128, 4 waves (2 blocks/CU, 64 KiB LDS).  kT256: 256x256, 8 waves (1 block/CU,
+//   128 KiB LDS) — half the LDS bytes per FLOP.
 // ------------------------------------------------------------------------------------
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE_BYTES = BM * BK * 2;             // 16 KiB per operand tile
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;         // A + B
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;          // 2 stages = 64 KiB
+constexpr int BK = 64;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-// Stage one 128x64 bf16 tile (rows of a K-contiguous matrix) into LDS.  LDS image: row r at
+template <int BM_, int BN_, int WM_, int WN_>
+struct Tile {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+    static constexpr int WAVES = WM * WN, THREADS = 64 * WAVES;
+    static constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
+    static constexpr int FM = WTM / 16, FN = WTN / 16;   // 16x16 fragments per wave
+    static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+    static constexpr int STAGE = A_BYTES + B_BYTES;
+    static constexpr int LDS = 2 * STAGE;
+    static constexpr int GA = BM / 8 / WAVES, GB = BN / 8 / WAVES;   // glds per wave per K-tile
+    static constexpr int MIN_BLOCKS = (LDS <= 80 * 1024) ? 2 : 1;
+    static_assert(BM % (8 * WAVES) == 0 && BN % (8 * WAVES) == 0, "staging split");
+    static_assert(WTM * WTN * 2 <= LDS / WAVES, "epilogue staging must fit");
+};
+using kT128 = Tile<128, 128, 2, 2>;
+using kT256 = Tile<256, 256, 2, 4>;
+
+// Stage `nglds` x 8 rows of a K-contiguous bf16 matrix into an LDS tile.  LDS image: row r at
 // byte 128*r; 16-B slot s' of row r holds global chunk s' ^ (r & 7)  (conflict-free b128
-// fragment reads).  Each wave issues 4 global_load_lds_dwordx4 (1 KiB = 8 rows each).
-__device__ __forceinline__ void stage_tile(const unsigned short* __restrict__ G, int64_t ld, int64_t row0,
+// fragment reads).  One global_load_lds_dwordx4 = 1 KiB = 8 rows.
+template <int NG>
+__device__ __forceinline__ void stage_rows(const unsigned short* __restrict__ G, int64_t ld, int64_t row0,
                                            int64_t row_max, int64_t k0, char* lds_tile, int wave, int lane) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int R0 = (wave * 4 + i) * 8;
+    for (int i = 0; i < NG; ++i) {
+        const int R0 = (wave * NG + i) * 8;
         const int r = R0 + (lane >> 3);
-        const int slot = lane & 7;
-        const int chunk = slot ^ (r & 7);
+        const int chunk = (lane & 7) ^ (r & 7);
         int64_t gr = row0 + r;
         gr = gr < row_max ? gr : row_max;  // clamp: rows past the end are never stored
         const unsigned short* src = G + gr * ld + k0 + chunk * 8;
@@ -98,88 +117,112 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int c
     return *reinterpret_cast<const bf16x8*>(lds_tile + row * 128 + ((chunk ^ (row & 7)) << 4));
 }
 
-template <int R>
-__global__ __launch_bounds__(256, 2) void k_lora_gemm(const unsigned short* __restrict__ X, int64_t ldx,
-                                                      const unsigned short* __restrict__ W, int64_t ldw,
-                                                      const unsigned short* __restrict__ bias,
-                                                      const float* __restrict__ T,
-                                                      const float* __restrict__ theta_pop, int64_t ld_theta,
-                                                      int64_t offB, float scale, int rows_per_member,
-                                                      int M, int N, int64_t K, int tiles_n,
-                                                      unsigned short* __restrict__ Y, int64_t ldy) {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+template <int R, class TL>
+__global__ __launch_bounds__(TL::THREADS, TL::MIN_BLOCKS) void k_lora_gemm(
+    const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
+    const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
+    int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int M, int N, int64_t K, int tiles_n,
+    unsigned short* __restrict__ Y, int64_t ldy) {
+    constexpr int FM = TL::FM, FN = TL::FN;
+    __shared__ __attribute__((aligned(16))) char smem[TL::LDS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / TL::WN, wn = wave % TL::WN;
     // XCD-aware bijective remap: consecutive tile ids (sharing X rows) land on one XCD.
     const int nwg = gridDim.x;
     const int bid = blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
     const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0 = tm * TL::BM, n0 = tn * TL::BN;
 
-    f32x4 acc[4][4];
+    f32x4 acc[FM][FN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = (int)(K / BK);
-    stage_tile(X, ldx, m0, M - 1, 0, smem, wave, lane);
-    stage_tile(W, ldw, n0, N - 1, 0, smem + TILE_BYTES, wave, lane);
+    stage_rows<TL::GA>(X, ldx, m0, M - 1, 0, smem, wave, lane);
+    stage_rows<TL::GB>(W, ldw, n0, N - 1, 0, smem + TL::A_BYTES, wave, lane);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-        const char* cur = smem + (kt & 1) * STAGE_BYTES;
+        const char* cur = smem + (kt & 1) * TL::STAGE;
         if (kt + 1 < nk) {
-            char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-            stage_tile(X, ldx, m0, M - 1, (int64_t)(kt + 1) * BK, nxt, wave, lane);
-            stage_tile(W, ldw, n0, N - 1, (int64_t)(kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+            char* nxt = smem + ((kt + 1) & 1) * TL::STAGE;
+            stage_rows<TL::GA>(X, ldx, m0, M - 1, (int64_t)(kt + 1) * BK, nxt, wave, lane);
+            stage_rows<TL::GB>(W, ldw, n0, N - 1, (int64_t)(kt + 1) * BK, nxt + TL::A_BYTES, wave, lane);
         }
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int ch = kk * 4 + (lane >> 4);
-            bf16x8 a[4], b[4];
+            bf16x8 b[FN];
 #pragma unroll
-            for (int f = 0; f < 4; ++f) a[f] = read_frag(cur, wm * 64 + f * 16 + (lane & 15), ch);
+            for (int f = 0; f < FN; ++f) b[f] = read_frag(cur + TL::A_BYTES, wn * TL::WTN + f * 16 + (lane & 15), ch);
+            if constexpr (FM <= 4) {
+                bf16x8 a[FM];
 #pragma unroll
-            for (int f = 0; f < 4; ++f) b[f] = read_frag(cur + TILE_BYTES, wn * 64 + f * 16 + (lane & 15), ch);
-            __builtin_amdgcn_s_setprio(1);
+                for (int f = 0; f < FM; ++f) a[f] = read_frag(cur, wm * TL::WTM + f * 16 + (lane & 15), ch);
+                __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+            } else {
+                // large wave tile: stream A fragments two at a time to bound register pressure
+#pragma unroll
+                for (int i = 0; i < FM; i += 2) {
+                    const bf16x8 a0 = read_frag(cur, wm * TL::WTM + i * 16 + (lane & 15), ch);
+                    const bf16x8 a1 = read_frag(cur, wm * TL::WTM + (i + 1) * 16 + (lane & 15), ch);
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i + 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b[j], acc[i + 1][j], 0, 0, 0);
+                }
+            }
         }
         __syncthreads();
     }
 
     // ---- epilogue: + bias[n] + scale * T[row,:] . B_k[n,:]  ->  bf16 via LDS, 16-B stores ----
     const int col_l = lane & 15, rq = (lane >> 4) * 4;
-    float bv[4];
-    int colv[4];
+    float bv[FN];
+    int colv[FN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + j * 16 + col_l;
+    for (int j = 0; j < FN; ++j) {
+        const int col = n0 + wn * TL::WTN + j * 16 + col_l;
         colv[j] = col < N ? col : N - 1;
         bv[j] = bias ? bf16_to_f32(bias[colv[j]]) : 0.0f;
     }
+    // stage this wave's WTM x WTN bf16 sub-tile in LDS (rows of WTN*2 bytes, 16-B slots XOR-swizzled);
+    // the LoRA term is added row by row so accumulators retire as they are written.
+    constexpr int ROWB = TL::WTN * 2, SLOTS = ROWB / 16;
+    char* ctile = smem + wave * (TL::WTM * ROWB);
+    float bk[FN][R > 0 ? R : 1];
+    bool one_member = true;
     if constexpr (R > 0) {
         const int first = m0 / rows_per_member;
-        const int last_row = (m0 + BM - 1 < M ? m0 + BM - 1 : M - 1);
-        const bool one_member = (last_row / rows_per_member) == first;
-        float bk[4][R];
-        if (one_member) {
-            const float* Bk = theta_pop + (int64_t)first * ld_theta + offB;
+        const int last_row = (m0 + TL::BM - 1 < M ? m0 + TL::BM - 1 : M - 1);
+        one_member = (last_row / rows_per_member) == first;
+        const float* Bk = theta_pop + (int64_t)first * ld_theta + offB;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
-                for (int qq = 0; qq < R; ++qq) bk[j][qq] = Bk[colv[j] * R + qq];
-        }
+            for (int qq = 0; qq < R; ++qq) bk[j][qq] = Bk[colv[j] * R + qq];
+    }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < FM; ++i) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                int row = m0 + wm * 64 + i * 16 + rq + e;
+        for (int e = 0; e < 4; ++e) {
+            const int rr = i * 16 + rq + e;
+            float add[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) add[j] = bv[j];
+            if constexpr (R > 0) {
+                int row = m0 + wm * TL::WTM + rr;
                 row = row < M ? row : M - 1;
                 float t[R];
 #pragma unroll
@@ -187,49 +230,36 @@ __global__ __launch_bounds__(256, 2) void k_lora_gemm(const unsigned short* __re
                 if (!one_member) {
                     const float* Bk = theta_pop + (int64_t)(row / rows_per_member) * ld_theta + offB;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < FN; ++j)
 #pragma unroll
                         for (int qq = 0; qq < R; ++qq) bk[j][qq] = Bk[colv[j] * R + qq];
                 }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < FN; ++j) {
                     float d = 0.0f;
 #pragma unroll
                     for (int qq = 0; qq < R; ++qq) d += t[qq] * bk[j][qq];
-                    acc[i][j][e] += bv[j] + scale * d;
+                    add[j] += scale * d;
                 }
             }
-        }
-    } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[i][j][e] += bv[j];
-    }
-    // stage this wave's 64x64 bf16 sub-tile in LDS (128-B rows, 16-B slots XOR-swizzled by row)
-    char* ctile = smem + wave * (64 * 128);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int rr = i * 16 + rq + e;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int cc = j * 16 + col_l;  // element column within the wave tile
-                const int slot = (cc >> 3) ^ (rr & 7);
-                *reinterpret_cast<unsigned short*>(ctile + rr * 128 + slot * 16 + (cc & 7) * 2) = f32_to_bf16(acc[i][j][e]);
+            for (int j = 0; j < FN; ++j) {
+                const int cc = j * 16 + col_l;
+                const int slot = (cc >> 3) ^ (rr & (SLOTS - 1));
+                *reinterpret_cast<unsigned short*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) =
+                    f32_to_bf16(acc[i][j][e] + add[j]);
             }
         }
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+    constexpr int ROWS_PER_IT = 64 / SLOTS;
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int rr = it * 8 + (lane >> 3), sl = lane & 7;
-        const int row = m0 + wm * 64 + rr;
-        const int col = n0 + wn * 64 + sl * 8;
+    for (int it = 0; it < TL::WTM / ROWS_PER_IT; ++it) {
+        const int rr = it * ROWS_PER_IT + lane / SLOTS, sl = lane % SLOTS;
+        const int row = m0 + wm * TL::WTM + rr;
+        const int col = n0 + wn * TL::WTN + sl * 8;
         if (row >= M || col >= N) continue;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * 128 + ((sl ^ (rr & 7)) << 4));
+        const u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
         unsigned short* dst = Y + (int64_t)row * ldy + col;
         if (col + 8 <= N && (((uintptr_t)dst) & 15) == 0) {
             *reinterpret_cast<u16x8*>(dst) = v;
@@ -283,6 +313,34 @@ static int project(const void* X, int64_t ldx, const float* tp, int64_t ldt, int
     return EGGROLL_OK;
 }
 
+static int g_tile_override = 0;
+
+template <class TL>
+static int launch_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                       const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                       int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, hipStream_t st) {
+    const int64_t tiles_m = (M + TL::BM - 1) / TL::BM, tiles_n = (N + TL::BN - 1) / TL::BN;
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_gemm: grid too large");
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+#define EGG_GEMM(RV)                                                                                              \
+    hipLaunchKernelGGL((k_lora_gemm<RV, TL>), grid, dim3(TL::THREADS), 0, st, (const unsigned short*)X, ldx,      \
+                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T, theta_pop, ld_theta,      \
+                       offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy)
+    switch (r) {
+        case 0: EGG_GEMM(0); break;
+        case 1: EGG_GEMM(1); break;
+        case 2: EGG_GEMM(2); break;
+        case 3: EGG_GEMM(3); break;
+        case 4: EGG_GEMM(4); break;
+        case 8: EGG_GEMM(8); break;
+        case 16: EGG_GEMM(16); break;
+        default: set_error("lora_gemm: r=%d unsupported (0,1,2,3,4,8,16)", r); return EGGROLL_ERR_UNSUPPORTED;
+    }
+#undef EGG_GEMM
+    EGG_CHECK_LAUNCH("lora_gemm");
+    return EGGROLL_OK;
+}
+
 }  // namespace eggroll
 
 using namespace eggroll;
@@ -321,29 +379,21 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
     EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_gemm: r=%d out of range", r);
     EGG_CHECK_ARG(rows_per_member > 0, "lora_gemm: rows_per_member must be > 0");
     EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_gemm: M/N too large");
-    const int64_t tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_gemm: grid too large");
     if (M == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(X && W && Y, "lora_gemm: NULL pointer");
     EGG_CHECK_ARG(r == 0 || (T && theta_pop), "lora_gemm: T / theta_pop NULL with r > 0");
     hipStream_t st = as_stream(stream);
-    const dim3 grid((unsigned)(tiles_m * tiles_n));
-#define EGG_GEMM(RV)                                                                                              \
-    hipLaunchKernelGGL(k_lora_gemm<RV>, grid, dim3(256), 0, st, (const unsigned short*)X, ldx,                 \
-                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T, theta_pop, ld_theta,      \
-                       offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy)
-    switch (r) {
-        case 0: EGG_GEMM(0); break;
-        case 1: EGG_GEMM(1); break;
-        case 2: EGG_GEMM(2); break;
-        case 3: EGG_GEMM(3); break;
-        case 4: EGG_GEMM(4); break;
-        case 8: EGG_GEMM(8); break;
-        case 16: EGG_GEMM(16); break;
-        default: set_error("lora_gemm: r=%d unsupported (0,1,2,3,4,8,16)", r); return EGGROLL_ERR_UNSUPPORTED;
-    }
-#undef EGG_GEMM
-    EGG_CHECK_LAUNCH("lora_gemm");
+    // tile choice: 256x256 when the grid still fills the chip, else 128x128
+    const int tsel = g_tile_override ? g_tile_override : ((M / 256) * ((N + 255) / 256) >= 512 ? 256 : 128);
+    return tsel == 256 ? launch_gemm<kT256>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
+                                            rows_per_member, M, N, K, Y, ldy, st)
+                       : launch_gemm<kT128>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
+                                            rows_per_member, M, N, K, Y, ldy, st);
+}
+
+extern "C" int eggroll_lora_gemm_tile(int32_t tile) {
+    EGG_CHECK_ARG(tile == 0 || tile == 128 || tile == 256, "lora_gemm_tile: tile must be 0 (auto), 128 or 256");
+    g_tile_override = tile;
     return EGGROLL_OK;
 }
 

@@ -1,4 +1,4 @@
-"""DC-AE f32c32 decoder (AutoencoderDC of Sana_Sprint_1.6B_1024px) in bf16, channels-last.
+"""DC-AE f32c32 decoder (AutoencoderDC of Sana_Sprint_1.6B_1024px) in bf16, NHWC activations.
 
 Reference: `AutoencoderDC.from_pretrained(model, subfolder="vae", torch_dtype=float32)` and
 `vae.decode(pred_x0 / scaling_factor)` (models/SanaSprint.py:44-49, 157-160).  Restated from
@@ -6,8 +6,11 @@ the published dc-ae-f32c32-sana-1.0 architecture (decoder block widths 128/256/5
 3 layers per stage, ResBlocks at the three high-resolution stages and EfficientViT blocks with
 ReLU multiscale linear attention at the three low-resolution stages, interpolate-upsampling with
 pixel-shuffle shortcuts, RMSNorm).  No weights exist offline: parity with diffusers is UNPINNED;
-shapes and FLOPs (~7.5 TFLOP per 1024^2 image) follow the architecture.  Runs on PyTorch-ROCm
-(MIOpen convolutions) — it is not one of the libeggroll hot-path kernels.
+shapes and FLOPs (~7.5 TFLOP per 1024^2 image) follow the architecture.
+
+Execution (not one of the ES hot-path kernels): activations stay NHWC
+contiguous; dense 3x3 convs go to MIOpen on channels-last views, 1x1 convs to hipBLASLt, and
+depthwise convs (+SiLU / GLU gate) to libeggroll's eggroll_dwconv_nhwc.
 """
 from __future__ import annotations
 
@@ -18,43 +21,50 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-CL = torch.channels_last
+from . import kernels as K
 
 
 def _p(*shape, dtype=torch.bfloat16):
     return nn.Parameter(torch.empty(*shape, dtype=dtype), requires_grad=False)
 
 
-class RMSNormC(nn.Module):
-    """RMSNorm over channels of an NCHW (channels-last) tensor, with weight and bias."""
+def nchw(x):  # NHWC-contiguous -> NCHW view with channels-last strides (no copy)
+    return x.permute(0, 3, 1, 2)
 
+
+def nhwc(x):  # channels-last NCHW -> NHWC view (contiguous when x is channels-last)
+    return x.permute(0, 2, 3, 1)
+
+
+class RMSNormC(nn.Module):
     def __init__(self, c: int, eps: float = 1e-5):
         super().__init__()
         self.eps = eps
         self.weight = _p(c)
         self.bias = _p(c)
 
-    def forward(self, x):
-        y = F.rms_norm(x.permute(0, 2, 3, 1), (x.shape[1],), self.weight, self.eps) + self.bias
-        return y.permute(0, 3, 1, 2)
+    def forward(self, x):  # NHWC
+        return F.rms_norm(x, (x.shape[-1],), self.weight, self.eps) + self.bias
 
 
-class Conv(nn.Module):
-    def __init__(self, cin: int, cout: int, k: int, groups: int = 1, bias: bool = True):
+class Conv3x3(nn.Module):
+    def __init__(self, cin: int, cout: int, bias: bool = True):
         super().__init__()
-        self.k, self.groups = k, groups
-        self.weight = _p(cout, cin // groups, k, k)
+        self.weight = nn.Parameter(torch.empty(cout, cin, 3, 3, dtype=torch.bfloat16).contiguous(
+            memory_format=torch.channels_last), requires_grad=False)
         self.bias = _p(cout) if bias else None
 
-    def forward(self, x):
-        return F.conv2d(x, self.weight, self.bias, padding=self.k // 2, groups=self.groups)
+    def forward(self, x):  # NHWC -> NHWC
+        y = F.conv2d(nchw(x.contiguous()), self.weight, self.bias, padding=1)
+        y = nhwc(y)
+        return y if y.is_contiguous() else y.contiguous()
 
 
 class ResBlock(nn.Module):
     def __init__(self, c: int):
         super().__init__()
-        self.conv1 = Conv(c, c, 3)
-        self.conv2 = Conv(c, c, 3, bias=False)
+        self.conv1 = Conv3x3(c, c)
+        self.conv2 = Conv3x3(c, c, bias=False)
         self.norm = RMSNormC(c)
 
     def forward(self, x):
@@ -62,18 +72,20 @@ class ResBlock(nn.Module):
 
 
 class GLUMBConvC(nn.Module):
+    """conv_inverted (1x1) -> SiLU -> dw3x3 -> GLU -> conv_point (1x1) -> RMSNorm, + residual."""
+
     def __init__(self, c: int, expand: int = 4):
         super().__init__()
         h = c * expand
-        self.conv_inverted = Conv(c, 2 * h, 1)
-        self.conv_depth = Conv(2 * h, 2 * h, 3, groups=2 * h)
-        self.conv_point = Conv(h, c, 1, bias=False)
+        self.w_inv, self.b_inv = _p(2 * h, c), _p(2 * h)
+        self.w_dw, self.b_dw = _p(9, 2 * h), _p(2 * h)      # [tap][C]
+        self.w_point = _p(c, h)
         self.norm = RMSNormC(c)
 
-    def forward(self, x):
-        h = self.conv_depth(F.silu(self.conv_inverted(x)))
-        a, g = h.chunk(2, dim=1)
-        return self.norm(self.conv_point(a * F.silu(g))) + x
+    def forward(self, x):  # NHWC
+        h = F.linear(x, self.w_inv, self.b_inv)
+        g = K.dwconv_nhwc(h, self.w_dw, self.b_dw, 3, pre_silu=True, glu=True)
+        return self.norm(F.linear(g, self.w_point)) + x
 
 
 class MultiscaleLinearAttention(nn.Module):
@@ -81,32 +93,34 @@ class MultiscaleLinearAttention(nn.Module):
 
     def __init__(self, c: int, head_dim: int = 32, scales: Sequence[int] = (5,)):
         super().__init__()
-        self.heads = c // head_dim
-        self.hd = head_dim
+        self.heads, self.hd = c // head_dim, head_dim
         inner = self.heads * head_dim
-        self.to_q = _p(inner, c)
-        self.to_k = _p(inner, c)
-        self.to_v = _p(inner, c)
-        self.ms_in = nn.ModuleList([Conv(3 * inner, 3 * inner, k, groups=3 * inner, bias=False) for k in scales])
-        self.ms_out = nn.ModuleList([Conv(3 * inner, 3 * inner, 1, groups=3 * self.heads, bias=False) for _ in scales])
-        self.to_out = _p(c, inner * (1 + len(scales)))
+        self.w_qkv = _p(3 * inner, c)                            # to_q | to_k | to_v (no bias)
+        self.ms_dw = nn.ParameterList([_p(k * k, 3 * inner) for k in scales])   # depthwise, [tap][C]
+        self.ms_pw = nn.ParameterList([_p(3 * self.heads, head_dim, head_dim) for _ in scales])  # grouped 1x1
+        self.scales = list(scales)
+        self.w_out = _p(c, inner * (1 + len(scales)))
         self.norm_out = RMSNormC(c)
 
-    def forward(self, x):
-        B, C, H, W = x.shape
-        t = x.permute(0, 2, 3, 1)                                               # [B,H,W,C]
-        qkv = torch.cat([F.linear(t, self.to_q), F.linear(t, self.to_k), F.linear(t, self.to_v)], dim=-1)
-        qkv = qkv.permute(0, 3, 1, 2)                                           # NCHW view, CL strides
-        branches = [qkv] + [o(i(qkv)) for i, o in zip(self.ms_in, self.ms_out)]
-        outs = []
-        for br in branches:                                                     # [B, 3*inner, H, W]
-            br = br.permute(0, 2, 3, 1).reshape(B, H * W, 3, self.heads, self.hd).float()
-            q, k, v = F.relu(br[:, :, 0]), F.relu(br[:, :, 1]), br[:, :, 2]
-            kv = torch.einsum("bnhj,bnhi->bhji", k, v)
-            num = torch.einsum("bnhj,bhji->bnhi", q, kv)
-            den = torch.einsum("bnhj,bhj->bnh", q, k.sum(1)).unsqueeze(-1)
-            outs.append((num / (den + 1e-15)).reshape(B, H, W, -1).to(torch.bfloat16))
-        y = F.linear(torch.cat(outs, dim=-1), self.to_out).permute(0, 3, 1, 2)
+    def _attend(self, br):  # br [B,H,W,3*inner] -> [B,H,W,inner]
+        B, H, W, _ = br.shape
+        t = br.reshape(B, H * W, -1, 3 * self.hd).float()         # heads-major q|k|v per head group
+        q, k, v = F.relu(t[..., :self.hd]), F.relu(t[..., self.hd:2 * self.hd]), t[..., 2 * self.hd:]
+        kv = torch.einsum("bnhj,bnhi->bhji", k, v)
+        num = torch.einsum("bnhj,bhji->bnhi", q, kv)
+        den = torch.einsum("bnhj,bhj->bnh", q, k.sum(1)).unsqueeze(-1)
+        return (num / (den + 1e-15)).reshape(B, H, W, -1).to(torch.bfloat16)
+
+    def forward(self, x):  # NHWC
+        B, H, W, C = x.shape
+        qkv = F.linear(x, self.w_qkv)                             # [B,H,W,3*inner]
+        outs = [self._attend(qkv)]
+        for ks, wdw, wpw in zip(self.scales, self.ms_dw, self.ms_pw):
+            d = K.dwconv_nhwc(qkv, wdw, None, ks, pre_silu=False, glu=False)
+            g = d.view(B * H * W, 3 * self.heads, self.hd).transpose(0, 1)       # [G, n, 32]
+            p = torch.bmm(g, wpw.transpose(1, 2)).transpose(0, 1).reshape(B, H, W, -1)
+            outs.append(self._attend(p))
+        y = F.linear(torch.cat(outs, dim=-1), self.w_out)
         return self.norm_out(y) + x
 
 
@@ -125,13 +139,14 @@ class UpBlock(nn.Module):
 
     def __init__(self, cin: int, cout: int):
         super().__init__()
-        self.conv = Conv(cin, cout, 3)
+        self.conv = Conv3x3(cin, cout)
         self.repeats = cout * 4 // cin
 
-    def forward(self, x):
-        y = self.conv(F.interpolate(x, scale_factor=2, mode="nearest"))
-        s = F.pixel_shuffle(x.repeat_interleave(self.repeats, dim=1), 2)
-        return y + s
+    def forward(self, x):  # NHWC
+        up = F.interpolate(nchw(x), scale_factor=2, mode="nearest")
+        y = self.conv(nhwc(up).contiguous())
+        s = F.pixel_shuffle(nchw(x).repeat_interleave(self.repeats, dim=1), 2)
+        return y + nhwc(s)
 
 
 class DCAEDecoder(nn.Module):
@@ -140,7 +155,7 @@ class DCAEDecoder(nn.Module):
         super().__init__()
         self.scaling_factor = scaling_factor
         self.latent_channels = latent_channels
-        self.conv_in = Conv(latent_channels, widths[-1], 3)
+        self.conv_in = Conv3x3(latent_channels, widths[-1])
         self.in_repeats = widths[-1] // latent_channels
         stages = []
         for i in reversed(range(len(widths))):
@@ -152,24 +167,29 @@ class DCAEDecoder(nn.Module):
             stages.append(nn.Sequential(*blocks))
         self.stages = nn.ModuleList(stages)  # lowest resolution first
         self.norm_out = RMSNormC(widths[0])
-        self.conv_out = Conv(widths[0], 3, 3)
+        self.conv_out = Conv3x3(widths[0], 3)
 
     @torch.no_grad()
     def init_weights(self, seed: int = 1):
         g = torch.Generator(device=self.conv_in.weight.device).manual_seed(seed)
         for name, p in self.named_parameters():
             if p.ndim >= 2:
-                std = 1.0 / math.sqrt(p[0].numel())
-                p.copy_(torch.randn(p.shape, generator=g, device=p.device) * std * 0.5)
+                if "ms_dw" in name or name.endswith("w_dw"):
+                    fan_in = p.shape[0]
+                elif "ms_pw" in name:
+                    fan_in = p.shape[-1]
+                else:
+                    fan_in = p[0].numel()
+                p.copy_(torch.randn(p.shape, generator=g, device=p.device) * (0.5 / math.sqrt(fan_in)))
             elif name.endswith("weight"):
                 p.fill_(1.0)
             else:
                 p.zero_()
 
-    def forward(self, z):  # z [B, 32, h, w] -> image [B, 3, 32h, 32w] in ~[-1, 1]
-        z = z.to(torch.bfloat16).contiguous(memory_format=CL)
-        x = self.conv_in(z) + z.repeat_interleave(self.in_repeats, dim=1)
+    def forward(self, z):  # z [B, 32, h, w] -> image [B, 3, 32h, 32w] (channels-last) in ~[-1, 1]
+        zt = nhwc(z.to(torch.bfloat16)).contiguous()
+        x = self.conv_in(zt) + zt.repeat_interleave(self.in_repeats, dim=-1)
         for st in self.stages:
             x = st(x)
         x = F.relu(self.norm_out(x))
-        return self.conv_out(x)
+        return nchw(self.conv_out(x))

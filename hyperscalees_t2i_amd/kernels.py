@@ -269,3 +269,26 @@ def lora_expand(T: torch.Tensor, theta_pop: torch.Tensor, offB: int, r: int, sca
     _lib.call("eggroll_lora_expand", T.data_ptr(), theta_pop.data_ptr(), theta_pop.stride(0), offB, r, float(scale),
               rows_per_member, M, N, y.data_ptr(), y.stride(0), _stream(y.device))
     return y
+
+
+# ---------------------------------------------------------------------------------------
+# model-side fused op: channels-last depthwise conv (+SiLU on load, +GLU gate)
+# ---------------------------------------------------------------------------------------
+
+
+def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], ks: int, pre_silu: bool,
+                glu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [B,H,W,C] bf16 contiguous; w_t [ks*ks, C] bf16; returns [B,H,W,C or C/2]."""
+    _dev(x, "dwconv(x)", torch.bfloat16)
+    _dev(w_t, "dwconv(w_t)", torch.bfloat16)
+    B, H, W, C = x.shape
+    if w_t.shape != (ks * ks, C):
+        raise ValueError(f"w_t {tuple(w_t.shape)} != ({ks * ks}, {C})")
+    if bias is not None:
+        _dev(bias, "dwconv(bias)", torch.bfloat16)
+    co = C // 2 if glu else C
+    if out is None:
+        out = torch.empty((B, H, W, co), dtype=torch.bfloat16, device=x.device)
+    _lib.call("eggroll_dwconv_nhwc", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu), int(glu),
+              out.data_ptr(), _stream(x.device))
+    return out

@@ -23,6 +23,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from . import kernels as K
 from .lora import LoRALinear, bind_theta_layout
 
 
@@ -167,18 +168,15 @@ class GLUMBConv(nn.Module):
         self.hidden = hidden
         self.w_inv = nn.Parameter(torch.empty(2 * hidden, dim, dtype=torch.bfloat16), requires_grad=False)
         self.b_inv = nn.Parameter(torch.zeros(2 * hidden, dtype=torch.bfloat16), requires_grad=False)
-        self.w_dw = nn.Parameter(torch.empty(2 * hidden, 1, 3, 3, dtype=torch.bfloat16), requires_grad=False)
+        self.w_dw = nn.Parameter(torch.empty(9, 2 * hidden, dtype=torch.bfloat16), requires_grad=False)  # [tap][C]
         self.b_dw = nn.Parameter(torch.zeros(2 * hidden, dtype=torch.bfloat16), requires_grad=False)
         self.w_point = nn.Parameter(torch.empty(dim, hidden, dtype=torch.bfloat16), requires_grad=False)
 
     def forward(self, x, H: int, W: int):  # x [B, N, D]
         B, N, _ = x.shape
-        h = F.silu(F.linear(x, self.w_inv, self.b_inv))                      # [B, N, 2h]
-        h = h.view(B, H, W, -1).permute(0, 3, 1, 2)                          # NCHW view, channels-last strides
-        h = F.conv2d(h, self.w_dw, self.b_dw, padding=1, groups=2 * self.hidden)
-        h = h.permute(0, 2, 3, 1).reshape(B, N, -1)
-        a, gate = h.chunk(2, dim=-1)
-        return F.linear(a * F.silu(gate), self.w_point)
+        h = F.linear(x, self.w_inv, self.b_inv).view(B, H, W, -1)           # pre-activation [B,H,W,2h]
+        g = K.dwconv_nhwc(h, self.w_dw, self.b_dw, 3, pre_silu=True, glu=True)  # silu->dw3x3->GLU fused
+        return F.linear(g.view(B, N, -1), self.w_point)
 
 
 class SanaBlock(nn.Module):
@@ -228,6 +226,8 @@ class SanaTransformer2DModel(nn.Module):
                 continue
             if name.endswith("scale_shift_table"):
                 p.copy_(torch.randn(p.shape, generator=g, device=p.device).div(p.shape[-1] ** 0.5))
+            elif name.endswith("w_dw"):
+                p.copy_(torch.randn(p.shape, generator=g, device=p.device) / 3.0)   # fan_in 9
             elif p.ndim >= 2:
                 fan_in = p[0].numel()
                 std = 1.0 / math.sqrt(fan_in)

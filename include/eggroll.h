@@ -134,12 +134,25 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
                       const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
                       int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
                       int64_t K, void* Y, int64_t ldy, void* stream);
+/* Tile selection of the LoRA GEMM for A/B measurement: 0 = automatic (256x256 when the grid
+ * fills the chip, else 128x128), 128 or 256 force a tile.  Process-global; not thread-safe.   */
+int eggroll_lora_gemm_tile(int32_t tile);
 int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
                          int64_t offA, int32_t r, int64_t rows_per_member, int64_t M, int64_t K,
                          float* T, void* stream);
 int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
                         int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
                         void* Y, int64_t ldy, void* stream);
+
+/* Model-side fused op of the Sana / DC-AE host (not part of the reference ES interface):
+ * channels-last depthwise ks x ks conv (stride 1, zero pad ks/2) of in [B,H,W,C] bf16 with
+ * weights w_t [ks*ks][C] bf16 (tap-major), optional bias [C]; pre_silu applies SiLU to the
+ * input on load; glu writes out[.., c] = y[c] * silu(y[c + C/2]) for c < C/2 (out [B,H,W,C/2]),
+ * else out [B,H,W,C].  Replaces silu(conv_inverted) -> conv_depth -> chunk -> gate of the
+ * reference's diffusers GLUMBConv (models/SanaSprint.py transformer FFN and DC-AE blocks).      */
+int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
+                        int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -193,6 +193,14 @@ def _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm):
                                  scale, rpm)
 
 
+@pytest.fixture(params=[128, 256], ids=["tile128", "tile256"])
+def gemm_tile(request):
+    from hyperscalees_t2i_amd import _lib
+    _lib.call("eggroll_lora_gemm_tile", request.param)
+    yield request.param
+    _lib.call("eggroll_lora_gemm_tile", 0)
+
+
 @pytest.mark.parametrize("M,N,Kd,r,rpm", [
     (300, 200, 128, 2, 100),      # ragged M, N; members not tile-aligned
     (257, 128, 64, 1, 257),       # single member, one row over a tile
@@ -200,7 +208,7 @@ def _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm):
     (512, 96, 192, 4, 128),       # r = 4 (VAR-like lora rank)
     (64, 32, 2240, 2, 16),        # proj_out-like N = 32, time-embed rows per member = 16
 ])
-def test_lora_linear_pop_vs_fp64(dev, M, N, Kd, r, rpm):
+def test_lora_linear_pop_vs_fp64(dev, gemm_tile, M, N, Kd, r, rpm):
     x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm)
     scale = 8.0 / r
     y = K.lora_linear_pop(x, W, b, tp, offA, offB, r, scale, rpm)
@@ -212,7 +220,7 @@ def test_lora_linear_pop_vs_fp64(dev, M, N, Kd, r, rpm):
     assert (np.abs(got - ref) <= tol + 1e-3).all(), float(np.abs(got - ref).max())
 
 
-def test_lora_linear_no_lora_matches_torch_matmul(dev):
+def test_lora_linear_no_lora_matches_torch_matmul(dev, gemm_tile):
     x, W, b, tp, *_ = _lora_case(dev, 640, 384, 512, 2, 640)
     y = K.lora_linear_pop(x, W, b, None, 0, 0, 0, 0.0, 640)
     ref = torch.nn.functional.linear(x.float(), W.float(), b.float())
@@ -232,7 +240,7 @@ def test_lora_project_expand_compose(dev):
     np.testing.assert_allclose(T.cpu().numpy(), Tref, rtol=1e-4, atol=1e-3)
 
 
-def test_lora_linear_sana_shape_sampled_rows(dev):
+def test_lora_linear_sana_shape_sampled_rows(dev, gemm_tile):
     """Full Sana attention shape (K = N = 2240) at 2 members x 16384 rows; rows sampled vs fp64."""
     M, N, Kd, r, rpm = 2 * 16384, 2240, 2240, 2, 16384
     x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm)
@@ -249,3 +257,25 @@ def test_lora_linear_sana_shape_sampled_rows(dev):
     got = y[rows.to(dev)].float().cpu().numpy()
     err = np.abs(got - ref)
     assert (err <= 2 ** -8 * np.abs(ref) + 2e-2).all(), float(err.max())
+
+
+# ---------------------------------------------------------------------------------- dwconv (model op)
+@pytest.mark.parametrize("B,H,W,C,ks,pre,glu", [(2, 32, 32, 64, 3, True, True), (3, 7, 5, 48, 3, False, False),
+                                                (1, 16, 16, 96, 5, False, False), (2, 9, 11, 32, 5, True, True),
+                                                (4, 32, 32, 11200, 3, True, True)])
+def test_dwconv_nhwc_vs_torch(dev, B, H, W, C, ks, pre, glu):
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(ks * ks, C, generator=g) / ks).to(torch.bfloat16).to(dev)
+    b = torch.randn(C, generator=g).to(torch.bfloat16).to(dev)
+    got = K.dwconv_nhwc(x, w, b, ks, pre, glu).float()
+    xin = x.float()
+    if pre:
+        xin = torch.nn.functional.silu(xin)
+    wc = w.float().t().reshape(C, 1, ks, ks)
+    y = torch.nn.functional.conv2d(xin.permute(0, 3, 1, 2), wc, b.float(), padding=ks // 2, groups=C).permute(0, 2, 3, 1)
+    if glu:
+        a, gt = y.chunk(2, dim=-1)
+        y = a * torch.nn.functional.silu(gt)
+    err = (got - y).abs()
+    assert (err <= 1e-2 * y.abs() + 2e-2).all(), float(err.max())
