@@ -43,8 +43,8 @@ class RMSNormC(nn.Module):
         self.weight = _p(c)
         self.bias = _p(c)
 
-    def forward(self, x):  # NHWC
-        return F.rms_norm(x, (x.shape[-1],), self.weight, self.eps) + self.bias
+    def forward(self, x, res=None, act=None):  # NHWC; fused norm * w + b [act] [+ res]
+        return K.rownorm(x.contiguous(), self.eps, layer=False, w=self.weight, b=self.bias, act=act, res=res)
 
 
 class Conv3x3(nn.Module):
@@ -68,7 +68,7 @@ class ResBlock(nn.Module):
         self.norm = RMSNormC(c)
 
     def forward(self, x):
-        return self.norm(self.conv2(F.silu(self.conv1(x)))) + x
+        return self.norm(self.conv2(F.silu(self.conv1(x))), res=x)
 
 
 class GLUMBConvC(nn.Module):
@@ -85,7 +85,7 @@ class GLUMBConvC(nn.Module):
     def forward(self, x):  # NHWC
         h = F.linear(x, self.w_inv, self.b_inv)
         g = K.dwconv_nhwc(h, self.w_dw, self.b_dw, 3, pre_silu=True, glu=True)
-        return self.norm(F.linear(g, self.w_point)) + x
+        return self.norm(F.linear(g, self.w_point), res=x)
 
 
 class MultiscaleLinearAttention(nn.Module):
@@ -121,7 +121,7 @@ class MultiscaleLinearAttention(nn.Module):
             p = torch.bmm(g, wpw.transpose(1, 2)).transpose(0, 1).reshape(B, H, W, -1)
             outs.append(self._attend(p))
         y = F.linear(torch.cat(outs, dim=-1), self.w_out)
-        return self.norm_out(y) + x
+        return self.norm_out(y, res=x)
 
 
 class EfficientViTBlock(nn.Module):
@@ -145,8 +145,7 @@ class UpBlock(nn.Module):
     def forward(self, x):  # NHWC
         up = F.interpolate(nchw(x), scale_factor=2, mode="nearest")
         y = self.conv(nhwc(up).contiguous())
-        s = F.pixel_shuffle(nchw(x).repeat_interleave(self.repeats, dim=1), 2)
-        return y + nhwc(s)
+        return K.upshortcut_add_(y, x.contiguous())
 
 
 class DCAEDecoder(nn.Module):
@@ -191,5 +190,5 @@ class DCAEDecoder(nn.Module):
         x = self.conv_in(zt) + zt.repeat_interleave(self.in_repeats, dim=-1)
         for st in self.stages:
             x = st(x)
-        x = F.relu(self.norm_out(x))
+        x = self.norm_out(x, act="relu")
         return nchw(self.conv_out(x))

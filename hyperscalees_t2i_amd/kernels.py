@@ -292,3 +292,62 @@ def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor]
     _lib.call("eggroll_dwconv_nhwc", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu), int(glu),
               out.data_ptr(), _stream(x.device))
     return out
+
+
+def _row_ptr(t: Optional[torch.Tensor], what: str, C: int):
+    """Pointer + row stride of a [groups, C]-shaped (possibly strided) bf16 view."""
+    if t is None:
+        return None, 0
+    if t.device.type != "cuda" or t.dtype != torch.bfloat16 or t.stride(-1) != 1:
+        raise _lib.EggrollError(f"{what}: expected a bf16 device view with unit inner stride")
+    stride = t.stride(0) if t.dim() > 1 and t.shape[0] > 1 else C
+    return t.data_ptr(), stride
+
+
+ACT = {None: 0, "none": 0, "relu": 1, "silu": 2}
+
+
+def rownorm(x: torch.Tensor, eps: float, layer: bool = False, w: Optional[torch.Tensor] = None,
+            b: Optional[torch.Tensor] = None, mscale: Optional[torch.Tensor] = None,
+            mshift: Optional[torch.Tensor] = None, rows_per_group: int = 1, act=None,
+            res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused (RMS|Layer)Norm over the last dim [+w][*(1+mscale[g])][+mshift[g]][+b][act][+res].
+    mscale / mshift: [groups, C] views (rows `mstride` apart), g = row // rows_per_group."""
+    _dev(x, "rownorm(x)", torch.bfloat16)
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if out is None:
+        out = torch.empty_like(x)
+    for t, nm in ((w, "w"), (b, "b"), (res, "res")):
+        if t is not None:
+            _dev(t, f"rownorm({nm})", torch.bfloat16)
+    ps, st1 = _row_ptr(mscale, "rownorm(mscale)", C)
+    ph, st2 = _row_ptr(mshift, "rownorm(mshift)", C)
+    if ps is not None and ph is not None and st1 != st2:
+        raise ValueError("mscale / mshift must share a row stride")
+    _lib.call("eggroll_rownorm", x.data_ptr(), rows, C, float(eps), int(bool(layer)), _p(w), _p(b), ps, ph,
+              st1 or st2 or C, int(rows_per_group), ACT[act], _p(res), out.data_ptr(), _stream(x.device))
+    return out
+
+
+def gated_residual_(x: torch.Tensor, y: torch.Tensor, gate: torch.Tensor, rows_per_group: int) -> torch.Tensor:
+    """x += gate[g] * y in place (g = row // rows_per_group); gate a [groups, C] view."""
+    _dev(x, "gated_residual(x)", torch.bfloat16)
+    _dev(y, "gated_residual(y)", torch.bfloat16)
+    C = x.shape[-1]
+    pg, st = _row_ptr(gate, "gated_residual(gate)", C)
+    _lib.call("eggroll_gated_residual", x.data_ptr(), y.data_ptr(), pg, st, x.numel() // C, C, int(rows_per_group),
+              _stream(x.device))
+    return x
+
+
+def upshortcut_add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """y [B,2H,2W,Cout] += pixel_shuffle(repeat_interleave(x [B,H,W,Cin])) in place (NHWC)."""
+    _dev(y, "upshortcut(y)", torch.bfloat16)
+    _dev(x, "upshortcut(x)", torch.bfloat16)
+    B, H, W, Cin = x.shape
+    Cout = y.shape[-1]
+    if y.shape[:3] != (B, 2 * H, 2 * W):
+        raise ValueError(f"upshortcut: y {tuple(y.shape)} vs x {tuple(x.shape)}")
+    _lib.call("eggroll_upshortcut_add", y.data_ptr(), x.data_ptr(), B, H, W, Cin, Cout, _stream(x.device))
+    return y

@@ -10,8 +10,9 @@ GLUMBConv FFN with mlp_ratio 2.5, AdaLN-single modulation with guidance embeddin
 across heads).  Parity with diffusers numerics is UNPINNED (no weights / no diffusers here);
 shapes, FLOPs and the LoRA target set (168 linears, D = 1,515,456 at r=2) are exact.
 
-Non-LoRA ops run on PyTorch-ROCm (hipBLASLt GEMMs for the 1x1 convs, MIOpen depthwise conv,
-SDPA); every LoRA target runs through libeggroll's population kernel.
+Non-LoRA ops run on PyTorch-ROCm (hipBLASLt GEMMs for the 1x1 convs, SDPA) or on libeggroll's
+model-side fused kernels (dwconv+GLU, RMS/AdaLN row norms, gated residual); every LoRA target runs
+through libeggroll's population kernel.
 """
 from __future__ import annotations
 
@@ -58,9 +59,8 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(dim, dtype=torch.bfloat16), requires_grad=False)
         self.bias = nn.Parameter(torch.zeros(dim, dtype=torch.bfloat16), requires_grad=False) if bias else None
 
-    def forward(self, x):
-        x = F.rms_norm(x, (x.shape[-1],), self.weight, self.eps)
-        return x + self.bias if self.bias is not None else x
+    def forward(self, x, act=None):
+        return K.rownorm(x.contiguous(), self.eps, layer=False, w=self.weight, b=self.bias, act=act)
 
 
 def timestep_embedding(t: torch.Tensor, dim: int = 256, max_period: float = 10000.0) -> torch.Tensor:
@@ -125,8 +125,8 @@ class LinearSelfAttention(nn.Module):
 
     def forward(self, x):  # x [B, N, D]
         B, N, _ = x.shape
-        q = F.relu(self.norm_q(self.to_q(x))).view(B, N, self.heads, self.head_dim).float()
-        k = F.relu(self.norm_k(self.to_k(x))).view(B, N, self.heads, self.head_dim).float()
+        q = self.norm_q(self.to_q(x), act="relu").view(B, N, self.heads, self.head_dim).float()
+        k = self.norm_k(self.to_k(x), act="relu").view(B, N, self.heads, self.head_dim).float()
         v = self.to_v(x).view(B, N, self.heads, self.head_dim).float()
         kv = torch.einsum("bnhj,bnhi->bhji", k, v)                 # [B, H, d, d] = sum_n k v^T
         ksum = k.sum(dim=1)                                         # [B, H, d]
@@ -190,16 +190,15 @@ class SanaBlock(nn.Module):
         self.scale_shift_table = nn.Parameter(torch.randn(6, D).div(D ** 0.5).to(torch.bfloat16), requires_grad=False)
 
     def forward(self, x, enc, mask_bias, timestep, H, W):
-        B = x.shape[0]
-        mods = (self.scale_shift_table[None] + timestep.view(B, 6, -1)).chunk(6, dim=1)
-        shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp = mods
-        n = F.layer_norm(x, (x.shape[-1],), eps=self.eps)
-        n = n * (1 + scale_msa) + shift_msa
-        x = x + gate_msa * self.attn1(n)
+        B, N, D = x.shape
+        # [B, 6, D]: shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
+        mods = (self.scale_shift_table[None] + timestep.view(B, 6, -1)).contiguous()
+        n = K.rownorm(x, self.eps, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=N)
+        K.gated_residual_(x, self.attn1(n), mods[:, 2], rows_per_group=N)
         x = x + self.attn2(x, enc, mask_bias)
-        n = F.layer_norm(x, (x.shape[-1],), eps=self.eps)
-        n = n * (1 + scale_mlp) + shift_mlp
-        return x + gate_mlp * self.ff(n, H, W)
+        n = K.rownorm(x, self.eps, layer=True, mscale=mods[:, 4], mshift=mods[:, 3], rows_per_group=N)
+        K.gated_residual_(x, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
+        return x
 
 
 class SanaTransformer2DModel(nn.Module):
@@ -243,15 +242,15 @@ class SanaTransformer2DModel(nn.Module):
         B, C, H, W = hidden_states.shape
         a = self.config
         x = hidden_states.to(torch.bfloat16).permute(0, 2, 3, 1).reshape(B, H * W, C)
-        x = F.linear(x, self.patch_w, self.patch_b)                                   # PatchEmbed (p = 1)
+        x = F.linear(x, self.patch_w, self.patch_b).contiguous()                      # PatchEmbed (p = 1)
         timestep6, emb_t = self.time_embed(timestep, guidance)
         enc = self.caption_projection(encoder_hidden_states.to(torch.bfloat16))
         enc = self.caption_norm(enc)
         mask_bias = ((1.0 - encoder_attention_mask.to(torch.bfloat16)) * -10000.0).view(B, 1, 1, -1)
         for blk in self.transformer_blocks:
             x = blk(x, enc, mask_bias, timestep6, H, W)
-        shift, scale = (self.scale_shift_table[None] + emb_t[:, None]).chunk(2, dim=1)
-        x = F.layer_norm(x, (x.shape[-1],), eps=a.norm_eps) * (1 + scale) + shift
+        mods = (self.scale_shift_table[None] + emb_t[:, None]).contiguous()     # [B, 2, D]: shift, scale
+        x = K.rownorm(x, a.norm_eps, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=H * W)
         x = self.proj_out(x)
         return x.view(B, H, W, a.out_channels).permute(0, 3, 1, 2)
 

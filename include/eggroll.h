@@ -154,6 +154,22 @@ int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64
                         int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
                         void* stream);
 
+/* Model-side fused row normalisation of x [rows, C] bf16 (C % 8 == 0, C <= 4096):
+ *   y = (x - mean·layer) * rsqrt(var + eps) [* w] [* (1 + mscale[g])] [+ mshift[g]] [+ b];
+ *   y = act(y) (0 none, 1 relu, 2 silu); y += res (optional);  g = row / rows_per_group,
+ *   modulation rows mstride elements apart.  Replaces RMSNorm / LayerNorm + AdaLN modulate /
+ *   bias / residual chains of the Sana blocks and the DC-AE decoder.                         */
+int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps, int32_t layer, const void* w,
+                    const void* b, const void* mscale, const void* mshift, int64_t mstride,
+                    int64_t rows_per_group, int32_t act, const void* res, void* out, void* stream);
+/* x[r, :] += gate[r / rows_per_group, :] * y[r, :]  (bf16, in place; gate rows gstride apart). */
+int eggroll_gated_residual(void* x, const void* y, const void* gate, int64_t gstride, int64_t rows,
+                           int64_t C, int64_t rows_per_group, void* stream);
+/* DC-AE up-block shortcut, NHWC: y[b,2h+i,2w+j,c] += x[b,h,w,(4c+2i+j)/(4*Cout/Cin)]
+ * (pixel_shuffle(repeat_interleave(x)) without materialising it).                            */
+int eggroll_upshortcut_add(void* y, const void* x, int64_t B, int64_t H, int64_t W, int64_t Cin,
+                           int64_t Cout, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -260,7 +260,7 @@ def test_lora_linear_sana_shape_sampled_rows(dev, gemm_tile):
 
 
 # ---------------------------------------------------------------------------------- dwconv (model op)
-@pytest.mark.parametrize("B,H,W,C,ks,pre,glu", [(2, 32, 32, 64, 3, True, True), (3, 7, 5, 48, 3, False, False),
+@pytest.mark.parametrize("B,H,W,C,ks,pre,glu", [(2, 32, 32, 64, 3, True, True), (3, 7, 5, 64, 3, False, False),
                                                 (1, 16, 16, 96, 5, False, False), (2, 9, 11, 32, 5, True, True),
                                                 (4, 32, 32, 11200, 3, True, True)])
 def test_dwconv_nhwc_vs_torch(dev, B, H, W, C, ks, pre, glu):
@@ -279,3 +279,56 @@ def test_dwconv_nhwc_vs_torch(dev, B, H, W, C, ks, pre, glu):
         y = a * torch.nn.functional.silu(gt)
     err = (got - y).abs()
     assert (err <= 1e-2 * y.abs() + 2e-2).all(), float(err.max())
+
+
+def test_dwconv_rejects_unsupported_channels(dev):
+    from hyperscalees_t2i_amd import _lib
+    x = torch.zeros(1, 4, 4, 48, dtype=torch.bfloat16, device=dev)
+    w = torch.zeros(9, 48, dtype=torch.bfloat16, device=dev)
+    with pytest.raises(_lib.EggrollError, match="multiple of 32"):
+        K.dwconv_nhwc(x, w, None, 3, False, False)
+
+
+# ---------------------------------------------------------------------------------- fused row ops (model)
+@pytest.mark.parametrize("C", [32, 128, 256, 512, 1024, 2240])
+@pytest.mark.parametrize("mode", ["rms_w_b_res", "rms_relu", "layer_adaln"])
+def test_rownorm_vs_torch(dev, C, mode):
+    g = torch.Generator().manual_seed(C)
+    rows, rpg = 96, 24
+    x = (torch.randn(rows, C, generator=g) * 2 + 0.5).to(torch.bfloat16).to(dev)
+    w = torch.randn(C, generator=g).to(torch.bfloat16).to(dev)
+    b = torch.randn(C, generator=g).to(torch.bfloat16).to(dev)
+    res = torch.randn(rows, C, generator=g).to(torch.bfloat16).to(dev)
+    mods = (torch.randn(rows // rpg, 6, C, generator=g) * 0.3).to(torch.bfloat16).to(dev)
+    xf = x.float()
+    if mode == "rms_w_b_res":
+        got = K.rownorm(x, 1e-5, w=w, b=b, res=res)
+        ref = torch.nn.functional.rms_norm(xf, (C,), w.float(), 1e-5) + b.float() + res.float()
+    elif mode == "rms_relu":
+        got = K.rownorm(x, 1e-5, w=w, act="relu")
+        ref = torch.relu(torch.nn.functional.rms_norm(xf, (C,), w.float(), 1e-5))
+    else:
+        got = K.rownorm(x, 1e-6, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=rpg)
+        sc = mods[:, 1].float().repeat_interleave(rpg, 0)
+        sh = mods[:, 0].float().repeat_interleave(rpg, 0)
+        ref = torch.nn.functional.layer_norm(xf, (C,), eps=1e-6) * (1 + sc) + sh
+    err = (got.float() - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 3e-2).all(), float(err.max())
+
+
+def test_gated_residual_and_upshortcut(dev):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4 * 16, 64, generator=g).to(torch.bfloat16).to(dev)
+    y = torch.randn(4 * 16, 64, generator=g).to(torch.bfloat16).to(dev)
+    mods = torch.randn(4, 6, 64, generator=g).to(torch.bfloat16).to(dev)
+    ref = x.float() + mods[:, 2].float().repeat_interleave(16, 0) * y.float()
+    K.gated_residual_(x, y, mods[:, 2], rows_per_group=16)
+    assert (x.float() - ref).abs().max().item() < 0.05
+    for cin, cout in ((64, 64), (64, 32), (32, 16)):
+        xs = torch.randn(2, 5, 7, cin, generator=g).to(torch.bfloat16).to(dev)
+        ys = torch.randn(2, 10, 14, cout, generator=g).to(torch.bfloat16).to(dev)
+        rep = cout * 4 // cin
+        sc = torch.nn.functional.pixel_shuffle(xs.permute(0, 3, 1, 2).float().repeat_interleave(rep, dim=1), 2)
+        ref = ys.float() + sc.permute(0, 2, 3, 1)
+        K.upshortcut_add_(ys, xs)
+        assert (ys.float() - ref).abs().max().item() < 0.05
