@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void k_lora_project(const unsigned short* __re
 //   128 KiB LDS) — half the LDS bytes per FLOP.
 // ------------------------------------------------------------------------------------
 constexpr int BK = 64;
+constexpr int GROUP_M = 8;  // row-tiles per rasterisation group
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
@@ -132,7 +133,14 @@ __global__ __launch_bounds__(TL::THREADS, TL::MIN_BLOCKS) void k_lora_gemm(
     const int bid = blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
     const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
-    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    // grouped rasterisation: consecutive tiles (one XCD's concurrently resident set) walk GROUP_M
+    // row-tiles before moving to the next column-tile, so X and W panels are both reused in L2.
+    const int tiles_m = (M + TL::BM - 1) / TL::BM;
+    const int per_group = GROUP_M * tiles_n;
+    const int grp = tile / per_group, first_m = grp * GROUP_M;
+    const int gsize = (tiles_m - first_m) < GROUP_M ? (tiles_m - first_m) : GROUP_M;
+    const int in_grp = tile - grp * per_group;
+    const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
     const int m0 = tm * TL::BM, n0 = tn * TL::BN;
 
     f32x4 acc[FM][FN];
