@@ -161,7 +161,7 @@ __global__ __launch_bounds__(TL::THREADS, TL::MIN_BLOCKS) void k_lora_gemm(
             stage_rows<TL::GB>(W, ldw, n0, N - 1, (int64_t)(kt + 1) * BK, nxt + TL::A_BYTES, wave, lane);
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+        for (int kk = 0; kk < (FM <= 4 ? 2 : 0); ++kk) {
             const int ch = kk * 4 + (lane >> 4);
             bf16x8 b[FN];
 #pragma unroll
@@ -178,17 +178,48 @@ __global__ __launch_bounds__(TL::THREADS, TL::MIN_BLOCKS) void k_lora_gemm(
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
                 __builtin_amdgcn_s_setprio(0);
             } else {
-                // large wave tile: stream A fragments two at a time to bound register pressure
+                // large wave tile: handled below as one software-pipelined K-tile
+            }
+        }
+        if constexpr (FM > 4) {
+            // 8 steps per K-tile (2 k-substeps x 4 A-fragment pairs); the operands of step s+1
+            // are read from LDS before the 8 MFMAs of step s are issued, so LDS latency hides
+            // under MFMA work (counted lgkmcnt) instead of a full drain per fragment pair.
+            const char* bt = cur + TL::A_BYTES;
+            const int rA = wm * TL::WTM + (lane & 15), rB = wn * TL::WTN + (lane & 15);
+            const int ch0 = lane >> 4, ch1 = 4 + (lane >> 4);
+            bf16x8 b[FN], bn[FN], a0, a1, n0, n1;
 #pragma unroll
-                for (int i = 0; i < FM; i += 2) {
-                    const bf16x8 a0 = read_frag(cur, wm * TL::WTM + i * 16 + (lane & 15), ch);
-                    const bf16x8 a1 = read_frag(cur, wm * TL::WTM + (i + 1) * 16 + (lane & 15), ch);
+            for (int f = 0; f < FN; ++f) b[f] = read_frag(bt, rB + f * 16, ch0);
+            a0 = read_frag(cur, rA, ch0);
+            a1 = read_frag(cur, rA + 16, ch0);
 #pragma unroll
-                    for (int j = 0; j < FN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b[j], acc[i][j], 0, 0, 0);
+            for (int st = 0; st < 8; ++st) {
+                const int pair = st & 3;
+                if (st < 7) {
+                    const int np = (st + 1) & 3, nch = ((st + 1) >> 2) ? ch1 : ch0;
+                    if (np == 0) {
 #pragma unroll
-                    for (int j = 0; j < FN; ++j)
-                        acc[i + 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b[j], acc[i + 1][j], 0, 0, 0);
+                        for (int f = 0; f < FN; ++f) bn[f] = read_frag(bt, rB + f * 16, nch);
+                    }
+                    n0 = read_frag(cur, rA + (2 * np) * 16, nch);
+                    n1 = read_frag(cur, rA + (2 * np + 1) * 16, nch);
+                }
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[2 * pair][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b[j], acc[2 * pair][j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[2 * pair + 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b[j], acc[2 * pair + 1][j], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+                if (st < 7) {
+                    a0 = n0;
+                    a1 = n1;
+                    if (((st + 1) & 3) == 0) {
+#pragma unroll
+                        for (int f = 0; f < FN; ++f) b[f] = bn[f];
+                    }
                 }
             }
         }
