@@ -190,15 +190,18 @@ def main():
     aux = aux_kernel_rooflines(engine, noiser, theta, pop, device)
 
     value = pop * args.steps / elapsed
-    per_launch_flops = gemm["flops"] / max(gemm["launches"], 1)
-    achieved = gemm["tflops"]
+    variants = {k: v for k, v in gemm.items() if k != "all"}
+    dom_name = max(variants, key=lambda k: variants[k]["total_ms"]) if variants else "all"
+    dom = gemm.get(dom_name, {"launches": 0, "flops": 0.0, "avg_us": float("nan"), "tflops": float("nan")})
+    achieved = dom["tflops"]
     pmc = load_pmc_traffic()
-    roofline = {"kernel": "k_lora_gemm<2> (population LoRA GEMM + fused epilogue)", "bound": "mfma",
+    roofline = {"kernel": f"{dom_name} (population LoRA GEMM + fused LoRA epilogue)", "bound": "mfma",
                 "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / BF16_DENSE_PEAK_TFLOPS,
                 "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                "launches": gemm["launches"], "avg_launch_us": gemm["avg_us"],
-                "flops_per_launch": per_launch_flops}
+                "launches": dom["launches"], "avg_launch_us": dom["avg_us"],
+                "flops_per_launch": dom["flops"] / max(dom["launches"], 1),
+                "all_variants": gemm.get("all")}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline

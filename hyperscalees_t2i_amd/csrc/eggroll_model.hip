@@ -231,6 +231,25 @@ __global__ __launch_bounds__(256) void k_gated_residual(unsigned short* __restri
     *reinterpret_cast<u16x8m*>(x + row * C + c0) = o;
 }
 
+// y = act(bf16(y + bias[c])) in place (conv bias folded into the activation pass; torch's conv2d
+// with bias on MIOpen runs the bias as its own add_ pass).  act: 0 none, 1 relu, 2 silu.
+__global__ __launch_bounds__(256) void k_bias_act(unsigned short* __restrict__ y, const unsigned short* __restrict__ bias,
+                                                  unsigned nch, int act, unsigned total_chunks) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total_chunks) return;
+    const unsigned c0 = (i % nch) * 8;
+    u16x8m yv = *reinterpret_cast<const u16x8m*>(y + (size_t)i * 8);
+    const u16x8m bv = *reinterpret_cast<const u16x8m*>(bias + c0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        float v = b2f(f2b(b2f(yv[k]) + b2f(bv[k])));
+        if (act == 1) v = v > 0.f ? v : 0.f;
+        else if (act == 2) v = v / (1.0f + __expf(-v));
+        yv[k] = f2b(v);
+    }
+    *reinterpret_cast<u16x8m*>(y + (size_t)i * 8) = yv;
+}
+
 // DCUpBlock2d shortcut, NHWC: y[b, 2h+i, 2w+j, c] += x[b, h, w, (4c + 2i + j) / rep]
 // (= pixel_shuffle(repeat_interleave(x, rep, channel), 2) without materialising it).
 // One thread = one output pixel x 8 channels; 32-bit index math.
@@ -252,6 +271,145 @@ __global__ __launch_bounds__(256) void k_upshortcut_add(unsigned short* __restri
 #pragma unroll
     for (int i = 0; i < 8; ++i) yv[i] = f2b(b2f(yv[i]) + b2f(src[(4 * (c0 + i) + k) / rep]));
     *reinterpret_cast<u16x8m*>(dst) = yv;
+}
+
+// Sub-pixel up-block output, NHWC: out[b, 2h+i, 2w+j, c] = y4[b, h+i, w+j, (2i+j)*Cout + c]
+//                                                      + x[b, h, w, (4c + 2i + j) / rep]
+// y4 = conv2d(x, W4, pad 1) with 2x2 phase kernels [B, H+1, W+1, 4*Cout]: equal to
+// conv3x3(upsample_nearest_x2(x)) + pixel_shuffle(repeat_interleave(x)) (DCUpBlock2d).
+__global__ __launch_bounds__(256) void k_subpixel_shortcut(const unsigned short* __restrict__ y4,
+                                                           const unsigned short* __restrict__ x,
+                                                           unsigned short* __restrict__ out, int H, int W, int Cin,
+                                                           int Cout, int rep, int pix_total) {
+    const int groups = Cout >> 3;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int pix = t / groups;
+    if (pix >= pix_total) return;
+    const int c0 = (t - pix * groups) << 3;
+    const int W2 = 2 * W, HW4 = 4 * H * W;
+    const int bb = pix / HW4;
+    const int r = pix - bb * HW4;
+    const int Y = r / W2, X = r - Y * W2;
+    const int i = Y & 1, j = X & 1, h = Y >> 1, w = X >> 1;
+    const int k = 2 * i + j;
+    const unsigned short* src = x + ((int64_t)(bb * H + h) * W + w) * Cin;
+    const u16x8m yv = *reinterpret_cast<const u16x8m*>(
+        y4 + ((int64_t)(bb * (H + 1) + h + i) * (W + 1) + (w + j)) * (4 * Cout) + k * Cout + c0);
+    u16x8m o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2b(b2f(yv[q]) + b2f(src[(4 * (c0 + q) + k) / rep]));
+    *reinterpret_cast<u16x8m*>(out + (int64_t)pix * Cout + c0) = o;
+}
+
+// ------------------------------------------------------------------------------------
+// ReLU linear attention, head dim 32 (SanaLinearAttnProcessor2_0 / DC-AE multiscale attention):
+//   kv[i][j] = sum_n v[n,i] relu(k[n,j]),  ksum[j] = sum_n relu(k[n,j])     (per image, head)
+//   out[n,i] = (sum_j relu(q[n,j]) kv[i][j]) / (sum_j relu(q[n,j]) ksum[j] + 1e-15)
+// fp32 accumulation.  Pass 1: per (image*head, token chunk) partial kv/ksum -> workspace;
+// pass 2: per (image*head, token chunk) fixed-order sum of the partials in LDS, then one token
+// per thread.  q/k/v are strided views (row stride, head stride) of the projection outputs.
+// ------------------------------------------------------------------------------------
+constexpr int LA_D = 32;
+constexpr int LA_PART = LA_D * LA_D + LA_D;   // kv + ksum floats per partial
+constexpr int LA_T = 256;                     // tokens per chunk
+
+__global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict__ k, const unsigned short* __restrict__ v,
+                                               int64_t ld, int64_t hstride, int heads, int N, int nchunk, int relu,
+                                               float* __restrict__ part) {
+    __shared__ float sk[LA_T][LA_D + 1];
+    __shared__ float sv[LA_T][LA_D + 1];
+    const int bh = blockIdx.x / nchunk, c = blockIdx.x - bh * nchunk;
+    const int b = bh / heads, h = bh - b * heads;
+    const int n0 = c * LA_T;
+    const int cnt = (N - n0) < LA_T ? (N - n0) : LA_T;
+    const int tid = threadIdx.x;
+    // stage LA_T tokens x 32 dims of k and v (16-B loads: 4 per token row per tensor)
+    for (int u = tid; u < LA_T * 4; u += 256) {
+        const int t = u >> 2, q4 = u & 3;
+        float kf[8], vf[8];
+        if (t < cnt) {
+            const int64_t off = ((int64_t)b * N + n0 + t) * ld + (int64_t)h * hstride + q4 * 8;
+            const u16x8m kv8 = *reinterpret_cast<const u16x8m*>(k + off);
+            const u16x8m vv8 = *reinterpret_cast<const u16x8m*>(v + off);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                float kk = b2f(kv8[i]);
+                kf[i] = relu ? (kk > 0.f ? kk : 0.f) : kk;
+                vf[i] = b2f(vv8[i]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kf[i] = vf[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            sk[t][q4 * 8 + i] = kf[i];
+            sv[t][q4 * 8 + i] = vf[i];
+        }
+    }
+    __syncthreads();
+    // thread -> row i = tid / 8, columns j0 = (tid % 8) * 4 .. +3 of kv; threads < 32 also do ksum
+    const int i = tid >> 3, j0 = (tid & 7) * 4;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, ks = 0.f;
+    for (int t = 0; t < cnt; ++t) {
+        const float vi = sv[t][i];
+        a0 += vi * sk[t][j0];
+        a1 += vi * sk[t][j0 + 1];
+        a2 += vi * sk[t][j0 + 2];
+        a3 += vi * sk[t][j0 + 3];
+        if (tid < LA_D) ks += sk[t][tid];
+    }
+    float* dst = part + (int64_t)blockIdx.x * LA_PART;
+    dst[i * LA_D + j0] = a0;
+    dst[i * LA_D + j0 + 1] = a1;
+    dst[i * LA_D + j0 + 2] = a2;
+    dst[i * LA_D + j0 + 3] = a3;
+    if (tid < LA_D) dst[LA_D * LA_D + tid] = ks;
+}
+
+__global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict__ q, int64_t ld, int64_t hstride,
+                                                int heads, int N, int nchunk, int relu, const float* __restrict__ part,
+                                                unsigned short* __restrict__ out, int64_t ldo) {
+    __shared__ float skv[LA_PART];
+    const int bh = blockIdx.x / nchunk, c = blockIdx.x - bh * nchunk;
+    const int b = bh / heads, h = bh - b * heads;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < LA_PART; e += 256) {
+        float s = 0.f;
+        for (int cc = 0; cc < nchunk; ++cc) s += part[((int64_t)bh * nchunk + cc) * LA_PART + e];
+        skv[e] = s;
+    }
+    __syncthreads();
+    const int n = c * LA_T + tid;
+    if (n >= N) return;
+    const int64_t row = (int64_t)b * N + n;
+    float qv[LA_D];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+        const u16x8m q8 = *reinterpret_cast<const u16x8m*>(q + row * ld + (int64_t)h * hstride + q4 * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float x = b2f(q8[i]);
+            qv[q4 * 8 + i] = relu ? (x > 0.f ? x : 0.f) : x;
+        }
+    }
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j < LA_D; ++j) den += qv[j] * skv[LA_D * LA_D + j];
+    const float inv = 1.0f / (den + 1e-15f);
+    unsigned short* o = out + row * ldo + h * LA_D;
+#pragma unroll
+    for (int i0 = 0; i0 < LA_D; i0 += 8) {
+        u16x8m o8;
+#pragma unroll
+        for (int ii = 0; ii < 8; ++ii) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < LA_D; ++j) s += qv[j] * skv[(i0 + ii) * LA_D + j];
+            o8[ii] = f2b(s * inv);
+        }
+        *reinterpret_cast<u16x8m*>(o + i0) = o8;
+    }
 }
 
 }  // namespace eggroll
@@ -361,5 +519,62 @@ extern "C" int eggroll_upshortcut_add(void* y, const void* x, int64_t B, int64_t
                        (unsigned short*)y, (const unsigned short*)x, (int)H, (int)W, (int)Cin, (int)Cout,
                        (int)(4 * Cout / Cin), (int)pix);
     EGG_CHECK_LAUNCH("upshortcut_add");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, void* out, int64_t B, int64_t H, int64_t W,
+                                         int64_t Cin, int64_t Cout, void* stream) {
+    EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && (4 * Cout) % Cin == 0 && Cout % 8 == 0,
+                  "subpixel_shortcut: bad sizes");
+    EGG_CHECK_ARG(B * 4 * H * W * Cout < (1ll << 31) && B * (H + 1) * (W + 1) * 4 * Cout < (1ll << 31),
+                  "subpixel_shortcut: tensor too large");
+    if (B == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(y4 && x && out, "subpixel_shortcut: NULL pointer");
+    const int64_t pix = B * 4 * H * W;
+    const int64_t threads = pix * (Cout / 8);
+    hipLaunchKernelGGL(k_subpixel_shortcut, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       (const unsigned short*)y4, (const unsigned short*)x, (unsigned short*)out, (int)H, (int)W,
+                       (int)Cin, (int)Cout, (int)(4 * Cout / Cin), (int)pix);
+    EGG_CHECK_LAUNCH("subpixel_shortcut");
+    return EGGROLL_OK;
+}
+
+extern "C" int64_t eggroll_linear_attention_workspace_bytes(int64_t B, int64_t N, int64_t heads) {
+    const int64_t nchunk = (N + LA_T - 1) / LA_T;
+    return B * heads * nchunk * LA_PART * (int64_t)sizeof(float);
+}
+
+extern "C" int eggroll_linear_attention(const void* q, const void* k, const void* v, int64_t ld, int64_t hstride,
+                                        int64_t B, int64_t N, int64_t heads, int32_t relu_qk, void* out, int64_t ldo,
+                                        void* workspace, void* stream) {
+    EGG_CHECK_ARG(B >= 0 && N > 0 && heads > 0 && ld % 8 == 0 && hstride % 8 == 0 && ldo % 8 == 0,
+                  "linear_attention: bad sizes/strides");
+    EGG_CHECK_ARG(((uintptr_t)q & 15) == 0 && ((uintptr_t)k & 15) == 0 && ((uintptr_t)v & 15) == 0 &&
+                  ((uintptr_t)out & 15) == 0, "linear_attention: pointers must be 16-byte aligned");
+    if (B == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(q && k && v && out && workspace, "linear_attention: NULL pointer");
+    const int64_t nchunk = (N + LA_T - 1) / LA_T;
+    const int64_t blocks = B * heads * nchunk;
+    EGG_CHECK_ARG(blocks < (1ll << 31), "linear_attention: grid too large");
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_la_kv, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)k,
+                       (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
+                       (float*)workspace);
+    EGG_CHECK_LAUNCH("linear_attention_kv");
+    hipLaunchKernelGGL(k_la_out, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)q, ld, hstride,
+                       (int)heads, (int)N, (int)nchunk, relu_qk, (const float*)workspace, (unsigned short*)out, ldo);
+    EGG_CHECK_LAUNCH("linear_attention_out");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_bias_act(void* y, const void* bias, int64_t rows, int64_t C, int32_t act, void* stream) {
+    EGG_CHECK_ARG(rows >= 0 && C > 0 && C % 8 == 0 && act >= 0 && act <= 2, "bias_act: bad sizes/act");
+    if (rows == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(y && bias, "bias_act: NULL pointer");
+    const int64_t total = rows * (C / 8);
+    EGG_CHECK_ARG(total < (1ll << 32) - 256, "bias_act: tensor too large for 32-bit chunk index");
+    hipLaunchKernelGGL(k_bias_act, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       (unsigned short*)y, (const unsigned short*)bias, (unsigned)(C / 8), act, (unsigned)total);
+    EGG_CHECK_LAUNCH("bias_act");
     return EGGROLL_OK;
 }

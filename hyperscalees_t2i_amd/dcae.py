@@ -68,6 +68,12 @@ class ResBlock(nn.Module):
         self.norm = RMSNormC(c)
 
     def forward(self, x):
+        c1 = self.conv1
+        h = nhwc(F.conv2d(nchw(x.contiguous()), c1.weight, None, padding=1)).contiguous()
+        h = K.bias_act_(h, c1.bias, "silu")                       # bias + SiLU in one pass
+        return self.norm(self.conv2(h), res=x)
+
+    def forward_reference(self, x):
         return self.norm(self.conv2(F.silu(self.conv1(x))), res=x)
 
 
@@ -102,14 +108,13 @@ class MultiscaleLinearAttention(nn.Module):
         self.w_out = _p(c, inner * (1 + len(scales)))
         self.norm_out = RMSNormC(c)
 
-    def _attend(self, br):  # br [B,H,W,3*inner] -> [B,H,W,inner]
-        B, H, W, _ = br.shape
-        t = br.reshape(B, H * W, -1, 3 * self.hd).float()         # heads-major q|k|v per head group
-        q, k, v = F.relu(t[..., :self.hd]), F.relu(t[..., self.hd:2 * self.hd]), t[..., 2 * self.hd:]
-        kv = torch.einsum("bnhj,bnhi->bhji", k, v)
-        num = torch.einsum("bnhj,bhji->bnhi", q, kv)
-        den = torch.einsum("bnhj,bhj->bnh", q, k.sum(1)).unsqueeze(-1)
-        return (num / (den + 1e-15)).reshape(B, H, W, -1).to(torch.bfloat16)
+    def _attend(self, br):  # br [B,H,W,3*inner]: per head group h, channels [q | k | v] of 32 each
+        B, H, W, C3 = br.shape
+        flat = br.reshape(B * H * W, C3)
+        hs = 3 * self.hd
+        o = K.linear_attention(flat, flat[:, self.hd:], flat[:, 2 * self.hd:], B, H * W, self.heads, hs,
+                               relu_qk=True)
+        return o.view(B, H, W, -1)
 
     def forward(self, x):  # NHWC
         B, H, W, C = x.shape
@@ -134,15 +139,47 @@ class EfficientViTBlock(nn.Module):
         return self.conv_out(self.attn(x))
 
 
+def subpixel_phase_weights(w3: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] kernel of conv3x3(nearest_up_x2(x)) -> [4*Cout, Cin, 2, 2] phase kernels of
+    an equivalent pad-1 2x2 conv on x: phase (i, j) sums the 3x3 taps that land on the same
+    low-resolution pixel (i=0: rows {0} | {1,2}; i=1: rows {0,1} | {2}; likewise columns)."""
+    groups = {0: ([0], [1, 2]), 1: ([0, 1], [2])}
+    out = []
+    for i in (0, 1):
+        for j in (0, 1):
+            k = torch.zeros(w3.shape[0], w3.shape[1], 2, 2, dtype=torch.float32, device=w3.device)
+            for a in (0, 1):
+                for b in (0, 1):
+                    k[:, :, a, b] = w3.float()[:, :, groups[i][a]][:, :, :, groups[j][b]].sum(dim=(2, 3))
+            out.append(k)
+    return torch.cat(out, dim=0)
+
+
 class UpBlock(nn.Module):
-    """DCUpBlock2d(interpolate=True, shortcut=True): nearest x2 + 3x3 conv, + pixel-shuffle shortcut."""
+    """DCUpBlock2d(interpolate=True, shortcut=True): nearest x2 + 3x3 conv + pixel-shuffle shortcut.
+    Executed as a pad-1 2x2 conv with 4*Cout sub-pixel phase outputs on the LOW-resolution input
+    (4/9 of the FLOPs, no upsampled tensor) and one fused interleave + shortcut kernel; exact up to
+    summation order (tests/test_gpu_kernels.py::test_subpixel_upblock_matches_reference)."""
 
     def __init__(self, cin: int, cout: int):
         super().__init__()
-        self.conv = Conv3x3(cin, cout)
+        self.conv = Conv3x3(cin, cout)           # the architecture's 3x3 weights (source of truth)
         self.repeats = cout * 4 // cin
+        self.w4 = None
+
+    def refresh_phase_weights(self):
+        w4 = subpixel_phase_weights(self.conv.weight)
+        self.w4 = w4.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        self.b4 = self.conv.bias.repeat(4) if self.conv.bias is not None else None
 
     def forward(self, x):  # NHWC
+        if self.w4 is None:
+            self.refresh_phase_weights()
+        x = x.contiguous()
+        y4 = nhwc(F.conv2d(nchw(x), self.w4, self.b4, padding=1))
+        return K.subpixel_shortcut(y4.contiguous(), x)
+
+    def forward_reference(self, x):  # the literal architecture (for tests)
         up = F.interpolate(nchw(x), scale_factor=2, mode="nearest")
         y = self.conv(nhwc(up).contiguous())
         return K.upshortcut_add_(y, x.contiguous())
@@ -184,6 +221,9 @@ class DCAEDecoder(nn.Module):
                 p.fill_(1.0)
             else:
                 p.zero_()
+        for m in self.modules():
+            if isinstance(m, UpBlock):
+                m.refresh_phase_weights()
 
     def forward(self, z):  # z [B, 32, h, w] -> image [B, 3, 32h, 32w] (channels-last) in ~[-1, 1]
         zt = nhwc(z.to(torch.bfloat16)).contiguous()

@@ -249,6 +249,11 @@ def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T:
     return out
 
 
+def gemm_tile_for(M: int, N: int) -> int:
+    """Tile libeggroll's automatic choice uses for an M x N LoRA GEMM (mirrors eggroll_lora_gemm)."""
+    return 256 if (M // 256) * ((N + 255) // 256) >= 512 else 128
+
+
 def lora_project(x: torch.Tensor, theta_pop: torch.Tensor, offA: int, r: int, rows_per_member: int,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _dev(x, "lora_project(x)", torch.bfloat16)
@@ -350,4 +355,55 @@ def upshortcut_add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     if y.shape[:3] != (B, 2 * H, 2 * W):
         raise ValueError(f"upshortcut: y {tuple(y.shape)} vs x {tuple(x.shape)}")
     _lib.call("eggroll_upshortcut_add", y.data_ptr(), x.data_ptr(), B, H, W, Cin, Cout, _stream(x.device))
+    return y
+
+
+def subpixel_shortcut(y4: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y4 [B,H+1,W+1,4*Cout] (phase conv output), x [B,H,W,Cin] -> out [B,2H,2W,Cout] (NHWC)."""
+    _dev(y4, "subpixel(y4)", torch.bfloat16)
+    _dev(x, "subpixel(x)", torch.bfloat16)
+    B, H, W, Cin = x.shape
+    if y4.shape[:3] != (B, H + 1, W + 1) or y4.shape[3] % 4:
+        raise ValueError(f"subpixel: y4 {tuple(y4.shape)} vs x {tuple(x.shape)}")
+    Cout = y4.shape[3] // 4
+    if out is None:
+        out = torch.empty((B, 2 * H, 2 * W, Cout), dtype=torch.bfloat16, device=x.device)
+    _lib.call("eggroll_subpixel_shortcut", y4.data_ptr(), x.data_ptr(), out.data_ptr(), B, H, W, Cin, Cout,
+              _stream(x.device))
+    return out
+
+
+_LA_WS: Dict[str, torch.Tensor] = {}
+
+
+def linear_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, N: int, heads: int,
+                     hstride: int, relu_qk: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ReLU linear attention (head dim 32) over strided bf16 views q/k/v [B*N, ...] whose head h
+    starts at column h*hstride.  Returns [B*N, heads*32] bf16."""
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        if t.device.type != "cuda" or t.dtype != torch.bfloat16 or t.stride(-1) != 1:
+            raise _lib.EggrollError(f"linear_attention({nm}): expected a bf16 device view with unit inner stride")
+    ld = q.stride(0)
+    if k.stride(0) != ld or v.stride(0) != ld:
+        raise ValueError("linear_attention: q/k/v must share a row stride")
+    if out is None:
+        out = torch.empty((B * N, heads * 32), dtype=torch.bfloat16, device=q.device)
+    nbytes = int(_lib.load().eggroll_linear_attention_workspace_bytes(B, N, heads))
+    key = str(q.device)
+    ws = _LA_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = _LA_WS[key] = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=q.device)
+    _lib.call("eggroll_linear_attention", q.data_ptr(), k.data_ptr(), v.data_ptr(), ld, hstride, B, N, heads,
+              int(bool(relu_qk)), out.data_ptr(), out.stride(0), ws.data_ptr(), _stream(q.device))
+    return out
+
+
+def bias_act_(y: torch.Tensor, bias: torch.Tensor, act: Optional[str]) -> torch.Tensor:
+    """y = act(y + bias) in place over the last (channel) dim of a contiguous bf16 tensor."""
+    _dev(y, "bias_act(y)", torch.bfloat16)
+    _dev(bias, "bias_act(bias)", torch.bfloat16)
+    if not y.is_contiguous() or bias.numel() != y.shape[-1]:
+        raise ValueError("bias_act: y must be contiguous with bias over its last dim")
+    C = y.shape[-1]
+    _lib.call("eggroll_bias_act", y.data_ptr(), bias.data_ptr(), y.numel() // C, C, ACT[act], _stream(y.device))
     return y

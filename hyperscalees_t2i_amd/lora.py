@@ -52,16 +52,23 @@ class GemmTimer:
         cls.active, cls.records = active, []
 
     @classmethod
-    def summary(cls) -> Dict[str, float]:
+    def summary(cls) -> Dict[str, Dict[str, float]]:
+        """Per kernel variant (the tile libeggroll picks for each shape, i.e. what rocprof names
+        k_lora_gemm<r, Tile<t,...>>) and "all": launches, total/avg time, algorithmic FLOP."""
         torch.cuda.synchronize()
-        ms = flops = 0.0
+        out: Dict[str, Dict[str, float]] = {}
         for s, e, M, N, Kd, r in cls.records:
-            ms += s.elapsed_time(e)
-            flops += 2.0 * M * N * Kd + 2.0 * M * N * r  # base GEMM + rank-r epilogue
-        n = len(cls.records)
-        return {"launches": n, "total_ms": ms, "flops": flops,
-                "avg_us": 1e3 * ms / n if n else float("nan"),
-                "tflops": flops / (ms * 1e9) if ms > 0 else float("nan")}
+            ms = s.elapsed_time(e)
+            fl = 2.0 * M * N * Kd + 2.0 * M * N * r  # base GEMM + rank-r epilogue
+            for key in (f"k_lora_gemm<{r},Tile<{K.gemm_tile_for(M, N)}>>", "all"):
+                d = out.setdefault(key, {"launches": 0, "total_ms": 0.0, "flops": 0.0})
+                d["launches"] += 1
+                d["total_ms"] += ms
+                d["flops"] += fl
+        for d in out.values():
+            d["avg_us"] = 1e3 * d["total_ms"] / d["launches"]
+            d["tflops"] = d["flops"] / (d["total_ms"] * 1e9) if d["total_ms"] > 0 else float("nan")
+        return out
 
 
 class _Weight(nn.Module):

@@ -114,6 +114,8 @@ class LinearSelfAttention(nn.Module):
 
     def __init__(self, dim: int, heads: int, head_dim: int, eps: float = 1e-5):
         super().__init__()
+        if head_dim != 32:
+            raise ValueError("LinearSelfAttention: eggroll_linear_attention is specialised for head_dim 32")
         self.heads, self.head_dim = heads, head_dim
         inner = heads * head_dim
         self.norm_q = RMSNorm(inner, eps)
@@ -124,16 +126,12 @@ class LinearSelfAttention(nn.Module):
         self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
 
     def forward(self, x):  # x [B, N, D]
-        B, N, _ = x.shape
-        q = self.norm_q(self.to_q(x), act="relu").view(B, N, self.heads, self.head_dim).float()
-        k = self.norm_k(self.to_k(x), act="relu").view(B, N, self.heads, self.head_dim).float()
-        v = self.to_v(x).view(B, N, self.heads, self.head_dim).float()
-        kv = torch.einsum("bnhj,bnhi->bhji", k, v)                 # [B, H, d, d] = sum_n k v^T
-        ksum = k.sum(dim=1)                                         # [B, H, d]
-        num = torch.einsum("bnhj,bhji->bnhi", q, kv)
-        den = torch.einsum("bnhj,bhj->bnh", q, ksum).unsqueeze(-1)
-        out = (num / (den + 1e-15)).reshape(B, N, -1).to(torch.bfloat16)
-        return self.to_out[0](out)
+        B, N, D = x.shape
+        q = self.norm_q(self.to_q(x), act="relu").view(B * N, -1)   # RMS norm + ReLU fused
+        k = self.norm_k(self.to_k(x), act="relu").view(B * N, -1)
+        v = self.to_v(x).view(B * N, -1)
+        o = K.linear_attention(q, k, v, B, N, self.heads, self.head_dim, relu_qk=False)
+        return self.to_out[0](o.view(B, N, -1))
 
 
 class CrossAttention(nn.Module):

@@ -170,6 +170,28 @@ int eggroll_gated_residual(void* x, const void* y, const void* gate, int64_t gst
 int eggroll_upshortcut_add(void* y, const void* x, int64_t B, int64_t H, int64_t W, int64_t Cin,
                            int64_t Cout, void* stream);
 
+/* DC-AE up-block via sub-pixel phases, NHWC: out[b,2h+i,2w+j,c] = y4[b,h+i,w+j,(2i+j)*Cout+c]
+ * + x[b,h,w,(4c+2i+j)/(4*Cout/Cin)], where y4 [B,H+1,W+1,4*Cout] = conv2d(x, 2x2 phase kernels,
+ * pad 1).  Equals conv3x3(nearest_upsample_x2(x)) + pixel_shuffle(repeat_interleave(x)) at
+ * 4/9 of the conv FLOPs and without the upsampled tensor (reference DCUpBlock2d).             */
+int eggroll_subpixel_shortcut(const void* y4, const void* x, void* out, int64_t B, int64_t H,
+                              int64_t W, int64_t Cin, int64_t Cout, void* stream);
+
+/* y[row, c] = act(bf16(y[row, c] + bias[c])) in place; y bf16 [rows, C] contiguous, C % 8 == 0,
+ * act 0 none / 1 relu / 2 silu.  (Conv bias + activation of the DC-AE ResBlock in one pass.)   */
+int eggroll_bias_act(void* y, const void* bias, int64_t rows, int64_t C, int32_t act, void* stream);
+
+/* ReLU linear attention with head dim 32 (diffusers SanaLinearAttnProcessor2_0 and DC-AE
+ * SanaMultiscaleLinearAttention): for every image b and head h over its N tokens,
+ *   out[n, h*32+i] = sum_j q'[n,j] kv[i][j] / (sum_j q'[n,j] ksum[j] + 1e-15),
+ *   kv[i][j] = sum_n v[n,i] k'[n,j],  ksum[j] = sum_n k'[n,j],  x' = relu(x) if relu_qk.
+ * q/k/v: bf16 views, element (b*N + n, h, d) at ptr[(b*N+n)*ld + h*hstride + d]; out bf16 with
+ * row stride ldo.  fp32 accumulation; workspace >= eggroll_linear_attention_workspace_bytes.   */
+int64_t eggroll_linear_attention_workspace_bytes(int64_t B, int64_t N, int64_t heads);
+int eggroll_linear_attention(const void* q, const void* k, const void* v, int64_t ld, int64_t hstride,
+                             int64_t B, int64_t N, int64_t heads, int32_t relu_qk, void* out, int64_t ldo,
+                             void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

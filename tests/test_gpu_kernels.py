@@ -332,3 +332,78 @@ def test_gated_residual_and_upshortcut(dev):
         ref = ys.float() + sc.permute(0, 2, 3, 1)
         K.upshortcut_add_(ys, xs)
         assert (ys.float() - ref).abs().max().item() < 0.05
+
+
+def test_subpixel_upblock_matches_reference(dev):
+    """Sub-pixel phase conv + fused interleave/shortcut == nearest-x2 upsample + 3x3 conv + shortcut."""
+    from hyperscalees_t2i_amd.dcae import UpBlock
+    torch.manual_seed(0)
+    for cin, cout, H, W in ((64, 32, 6, 5), (32, 32, 8, 8), (64, 64, 4, 7)):
+        with torch.device(dev):
+            up = UpBlock(cin, cout)
+        with torch.no_grad():
+            up.conv.weight.copy_(torch.randn_like(up.conv.weight, dtype=torch.float32) * 0.1)
+            up.conv.bias.copy_(torch.randn_like(up.conv.bias, dtype=torch.float32) * 0.1)
+        up.refresh_phase_weights()
+        x = torch.randn(2, H, W, cin, device=dev).to(torch.bfloat16)
+        got = up(x).float()
+        ref = up.forward_reference(x).float()
+        rel = ((got - ref).norm() / ref.norm()).item()
+        assert got.shape == ref.shape and rel < 1e-2, rel
+
+
+def _linear_attention_ref(q, k, v, relu):
+    """fp32 restatement of diffusers SanaLinearAttnProcessor2_0 (q,k,v [B, N, heads, 32])."""
+    q, k, v = q.float(), k.float(), v.float()
+    if relu:
+        q, k = q.clamp_min(0), k.clamp_min(0)
+    kv = torch.einsum("bnhj,bnhi->bhij", k, v)
+    ks = k.sum(dim=1)                                   # [B, heads, 32]
+    num = torch.einsum("bnhj,bhij->bnhi", q, kv)
+    den = torch.einsum("bnhj,bhj->bnh", q, ks).unsqueeze(-1)
+    return num / (den + 1e-15)
+
+
+@pytest.mark.parametrize("B,N,heads", [(2, 1024, 3), (3, 300, 2), (1, 17, 1), (2, 4096, 4)])
+def test_linear_attention_separate_qkv(dev, B, N, heads):
+    g = torch.Generator().manual_seed(B * N + heads)
+    q, k, v = (torch.randn(B, N, heads, 32, generator=g).to(torch.bfloat16).to(dev) for _ in range(3))
+    k = k.abs()   # post-ReLU keys, as the Sana attn1 feeds them
+    q = q.abs()
+    got = K.linear_attention(q.view(B * N, -1), k.view(B * N, -1), v.view(B * N, -1), B, N, heads, 32,
+                             relu_qk=False).float().view(B, N, heads, 32)
+    ref = _linear_attention_ref(q, k, v, relu=False)
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 8e-3, rel   # bf16 output rounding (2^-8) dominates
+
+
+def test_linear_attention_interleaved_relu(dev):
+    """DC-AE layout: per head h, channels [q | k | v] of 32 each in one [B*N, 3*heads*32] tensor."""
+    B, N, heads = 2, 257, 4
+    g = torch.Generator().manual_seed(11)
+    qkv = torch.randn(B, N, heads, 3, 32, generator=g).to(torch.bfloat16).to(dev)
+    flat = qkv.view(B * N, -1)
+    got = K.linear_attention(flat, flat[:, 32:], flat[:, 64:], B, N, heads, 96, relu_qk=True)
+    ref = _linear_attention_ref(qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2], relu=True)
+    rel = ((got.float().view(B, N, heads, 32) - ref).norm() / ref.norm()).item()
+    assert rel < 8e-3, rel
+
+
+def test_bias_act_and_resblock(dev):
+    g = torch.Generator().manual_seed(5)
+    y = torch.randn(3, 5, 7, 64, generator=g).to(torch.bfloat16).to(dev)
+    b = torch.randn(64, generator=g).to(torch.bfloat16).to(dev)
+    for act, fn in (("silu", torch.nn.functional.silu), ("relu", torch.relu), (None, lambda t: t)):
+        ref = fn(y + b).float()
+        got = K.bias_act_(y.clone(), b, act).float()
+        assert (got - ref).abs().max().item() <= 0.02 * max(1.0, ref.abs().max().item())
+    from hyperscalees_t2i_amd.dcae import ResBlock
+    torch.manual_seed(1)
+    with torch.device(dev):
+        rb = ResBlock(64)
+    with torch.no_grad():
+        for p in rb.parameters():
+            p.copy_(torch.randn_like(p, dtype=torch.float32) * 0.05)
+    x = torch.randn(2, 9, 6, 64, device=dev).to(torch.bfloat16)
+    got, ref = rb(x).float(), rb.forward_reference(x).float()
+    assert ((got - ref).norm() / ref.norm()).item() < 1e-2
