@@ -27,12 +27,31 @@ import time
 from pathlib import Path
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")  # see hyperscalees_t2i_amd/__init__.py
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 import torch  # noqa: E402
 
 torch.backends.cudnn.benchmark = True  # MIOpen Find per conv shape during warmup (FAST mode: 38 vs 700+ TF)
+T_START = time.perf_counter()
+
+
+def log(msg: str) -> None:
+    print(f"[bench +{time.perf_counter() - T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def start_heartbeat(period_s: float = 30.0) -> None:
+    """Progress line every `period_s` on stderr (MIOpen Find during warmup can run for minutes
+    without returning to Python; torch releases the GIL inside ops, so this thread keeps ticking)."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(period_s)
+            log("heartbeat")
+
+    threading.Thread(target=beat, daemon=True).start()
 
 METRIC = "ES member-evals/sec (whole node) Sana-Sprint 1.6B pop=64; % HBM/MFMA roofline"
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16
@@ -162,13 +181,18 @@ def load_pmc_traffic():
 def main():
     args = parse()
     rank, world, local = dist_setup(args)
+    if rank == 0:
+        start_heartbeat()
     device = torch.device(f"cuda:{local}")
     from hyperscalees_t2i_amd.lora import GemmTimer
 
     backend, engine, noiser, theta, pop = build(args, world, rank, device)
+    log(f"rank {rank}: built (pop {pop}, D {noiser.num_params})")
     guidance = backend.cfg.guidance_scale
     for w in range(args.warmup):
         theta, _ = engine.step(theta, seed=w, guidance_scale=guidance)
+        torch.cuda.synchronize()
+        log(f"rank {rank}: warmup epoch {w} done")
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -181,6 +205,7 @@ def main():
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    log(f"rank {rank}: timed {args.steps} epochs in {elapsed:.3f}s")
     GemmTimer.active = False
     marker()  # timed region ends
     gemm = GemmTimer.summary()

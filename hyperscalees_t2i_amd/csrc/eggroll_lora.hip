@@ -309,6 +309,296 @@ __global__ __launch_bounds__(TL::THREADS, TL::MIN_BLOCKS) void k_lora_gemm(
 }
 
 // ------------------------------------------------------------------------------------
+// 8-phase 256x256x64 variant (the large-M path).  8 waves = 2 groups of 4 (wm = 0 / 1), each
+// wave owns a 128x64 output sub-tile = 4 C-quadrants of 64x32 (16 MFMA 16x16x32 per K-tile each).
+// Every K-tile is split into 4 LDS half-tile regions by quadrant: A0 / A1 = rows of quadrant-row
+// qa = 0 / 1 of both wave rows, B0 / B1 = columns of quadrant-column qb = 0 / 1 of all four wave
+// columns.  One phase = {ds_read the quadrant's fragments, issue one half-tile prefetch (2 glds),
+// lgkmcnt(0), s_barrier, 16 MFMA, s_barrier}; group 1 runs one barrier behind group 0, so on every
+// SIMD one wave does MFMA while its partner reads LDS / issues DMA.  Quadrant order per K-tile
+// (0,0) (0,1) (1,1) (1,0): A0+B0 read in phase 1, B1 in 2, A1 in 3, B0 again in 4, and each
+// region is restaged in the phase after its last read (lgkmcnt(0) before the barrier retired those
+// reads).  The prefetch of K-tile t+1 therefore spans phases (t,2)..(t,4)+(t+1,1) and the counted
+// vmcnt(6) that retires a buffer leaves 3 half-tiles (6 glds) in flight across the barrier; nothing
+// drains vmcnt to 0 inside the loop (cdna_hip_programming.md §5 "256² 8-phase template", T3/T4).
+// ------------------------------------------------------------------------------------
+namespace p8 {
+constexpr int HALF = 128 * 128;  // one half-tile region: 128 rows x 64 bf16 (16 KiB)
+constexpr int BUF = 4 * HALF;    // A0 | A1 | B0 | B1
+constexpr int LDS = 2 * BUF;     // 128 KiB, two K-tile buffers
+constexpr int RA0 = 0, RA1 = HALF, RB0 = 2 * HALF, RB1 = 3 * HALF;
+}  // namespace p8
+
+// Per-thread staging descriptor of one half-tile region: 2 DMAs (buffer_load_dwordx4 ... lds), each
+// 8 rows x 128 B.  `off[i]` is the lane's 32-bit BYTE offset (row * ld + swizzled chunk) at k = 0;
+// the K-tile's byte offset goes in the wave-uniform soffset.  The host guarantees rows*ld*2 < 2^31.
+struct HalfStage {
+    uint32_t off[2];
+};
+
+template <bool IS_A>
+__device__ __forceinline__ HalfStage make_stage(int base_row, int row_max, int64_t ld, int h, int wave, int lane) {
+    HalfStage s;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int j = (i * 8 + wave) * 8 + (lane >> 3);               // region row
+        const int chunk = (lane & 7) ^ (j & 7);
+        const int tr = IS_A ? ((j >> 6) * 128 + h * 64 + (j & 63))   // A: wave row wm = j/64
+                            : ((j >> 5) * 64 + h * 32 + (j & 31));   // B: wave col wn = j/32
+        int gr = base_row + tr;
+        gr = gr < row_max ? gr : row_max;  // clamp: rows past the end are never stored
+        s.off[i] = ((uint32_t)gr * (uint32_t)ld + chunk * 8) * 2;
+    }
+    return s;
+}
+
+__device__ __forceinline__ void issue_half(__amdgpu_buffer_rsrc_t rs, const HalfStage& s, int kbytes, char* region,
+                                           int wave) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(region + (i * 8 + wave) * 1024), 16, s.off[i], kbytes,
+                                                 0, 0);
+}
+
+#define P8_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#define P8_VM6() asm volatile("s_waitcnt vmcnt(6)" ::: "memory")
+#define P8_VM0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+// s_barrier as a full compiler fence: the builtin alone is IntrNoMem, so IR passes may move the
+// next phase's ds_reads (or this phase's MFMAs) across it.
+#define P8_BAR()                              \
+    do {                                      \
+        asm volatile("" ::: "memory");        \
+        __builtin_amdgcn_sched_barrier(0);    \
+        __builtin_amdgcn_s_barrier();         \
+        __builtin_amdgcn_sched_barrier(0);    \
+        asm volatile("" ::: "memory");        \
+    } while (0)
+
+template <int QA, int QB>
+__device__ __forceinline__ void p8_mma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+                acc[QA * 4 + f][QB * 2 + g] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f][kk], b[g][kk], acc[QA * 4 + f][QB * 2 + g], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+}
+
+// Fragment reads with one per-lane base per k-substep: row r = r0 + 16 f keeps (r & 7) fixed, so
+// fragment f is base[kk] + 2048 f (an immediate offset) — no per-fragment address registers.
+__device__ __forceinline__ void p8_read_a(bf16x8 (&a)[4][2], const char* region, const int (&off)[2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) a[f][kk] = *reinterpret_cast<const bf16x8*>(region + off[kk] + f * 2048);
+}
+__device__ __forceinline__ void p8_read_b(bf16x8 (&b)[2][2], const char* region, const int (&off)[2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) b[g][kk] = *reinterpret_cast<const bf16x8*>(region + off[kk] + g * 2048);
+}
+__device__ __forceinline__ void p8_frag_offsets(int (&off)[2], int r0, int lane) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) off[kk] = r0 * 128 + ((((kk * 4) + (lane >> 4)) ^ (r0 & 7)) << 4);
+}
+
+#define P8_LGKM0_ asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// One phase: read the quadrant's fragments (RD: 0 = A+B, 1 = B only, 2 = A only), issue one
+// half-tile DMA, [vmcnt(6)], retire the reads, barrier, 16 MFMA, barrier.
+template <int QA, int QB, int RD, bool VM>
+__device__ __forceinline__ void p8_phase(f32x4 (&acc)[8][4], bf16x8 (&a)[4][2], bf16x8 (&b)[2][2], const char* buf,
+                                         const int (&oA)[2], const int (&oB)[2], __amdgpu_buffer_rsrc_t rs,
+                                         const HalfStage& st, int kbytes, char* dst, int wave) {
+    if (RD != 2) p8_read_b(b, buf + (QB ? p8::RB1 : p8::RB0), oB);
+    if (RD != 1) p8_read_a(a, buf + (QA ? p8::RA1 : p8::RA0), oA);
+    issue_half(rs, st, kbytes, dst, wave);
+    if (VM) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    P8_LGKM0_;
+    P8_BAR();
+    p8_mma<QA, QB>(acc, a, b);
+    P8_BAR();
+}
+
+// Epilogue shared by the 256x256 kernels: + bias[n] + scale * T[row,:] . B_k[n,:], bf16 via a
+// per-wave LDS staging tile (16-B slots XOR-swizzled by row), 16-B stores.
+template <int R, int WTM, int WTN>
+__device__ __forceinline__ void lora_epilogue(f32x4 (&acc)[WTM / 16][WTN / 16], char* smem, int wave, int lane,
+                                              int m0, int n0, int rbase, int cbase, const unsigned short* __restrict__ bias,
+                                              const float* __restrict__ T, const float* __restrict__ theta_pop,
+                                              int64_t ld_theta, int64_t offB, float scale, int rows_per_member,
+                                              int BMtile, int M, int N, unsigned short* __restrict__ Y, int64_t ldy) {
+    constexpr int FM = WTM / 16, FN = WTN / 16;
+    const int col_l = lane & 15, rq = (lane >> 4) * 4;
+    float bv[FN];
+    int colv[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int col = n0 + cbase + j * 16 + col_l;
+        colv[j] = col < N ? col : N - 1;
+        bv[j] = bias ? bf16_to_f32(bias[colv[j]]) : 0.0f;
+    }
+    constexpr int ROWB = WTN * 2, SLOTS = ROWB / 16;
+    char* ctile = smem + wave * (WTM * ROWB);
+    float bk[FN][R > 0 ? R : 1];
+    bool one_member = true;
+    if constexpr (R > 0) {
+        const int first = m0 / rows_per_member;
+        const int last_row = (m0 + BMtile - 1 < M ? m0 + BMtile - 1 : M - 1);
+        one_member = (last_row / rows_per_member) == first;
+        const float* Bk = theta_pop + (int64_t)first * ld_theta + offB;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int qq = 0; qq < R; ++qq) bk[j][qq] = Bk[colv[j] * R + qq];
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int rr = i * 16 + rq + e;
+            float add[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) add[j] = bv[j];
+            if constexpr (R > 0) {
+                int row = m0 + rbase + rr;
+                row = row < M ? row : M - 1;
+                float t[R];
+#pragma unroll
+                for (int qq = 0; qq < R; ++qq) t[qq] = T[(int64_t)row * R + qq];
+                if (!one_member) {
+                    const float* Bk = theta_pop + (int64_t)(row / rows_per_member) * ld_theta + offB;
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+#pragma unroll
+                        for (int qq = 0; qq < R; ++qq) bk[j][qq] = Bk[colv[j] * R + qq];
+                }
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    float d = 0.0f;
+#pragma unroll
+                    for (int qq = 0; qq < R; ++qq) d += t[qq] * bk[j][qq];
+                    add[j] += scale * d;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int cc = j * 16 + col_l;
+                const int slot = (cc >> 3) ^ (rr & (SLOTS - 1));
+                *reinterpret_cast<unsigned short*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) =
+                    f32_to_bf16(acc[i][j][e] + add[j]);
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+    constexpr int ROWS_PER_IT = 64 / SLOTS;
+#pragma unroll
+    for (int it = 0; it < WTM / ROWS_PER_IT; ++it) {
+        const int rr = it * ROWS_PER_IT + lane / SLOTS, sl = lane % SLOTS;
+        const int row = m0 + rbase + rr;
+        const int col = n0 + cbase + sl * 8;
+        if (row >= M || col >= N) continue;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+        unsigned short* dst = Y + (int64_t)row * ldy + col;
+        if (col + 8 <= N && (((uintptr_t)dst) & 15) == 0) {
+            *reinterpret_cast<u16x8*>(dst) = v;
+        } else {
+            for (int u = 0; u < 8 && col + u < N; ++u) dst[u] = v[u];
+        }
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(512, 1) void k_lora_gemm8(
+    const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
+    const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
+    int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int M, int N, int64_t K, int tiles_n,
+    unsigned short* __restrict__ Y, int64_t ldy) {
+    __shared__ __attribute__((aligned(16))) char smem[p8::LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    // XCD-aware bijective remap + grouped rasterisation (as k_lora_gemm).
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+    const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+    const int tiles_m = (M + 255) / 256;
+    const int per_group = GROUP_M * tiles_n;
+    const int grp = tile / per_group, first_m = grp * GROUP_M;
+    const int gsize = (tiles_m - first_m) < GROUP_M ? (tiles_m - first_m) : GROUP_M;
+    const int in_grp = tile - grp * per_group;
+    const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
+    const int m0 = tm * 256, n0 = tn * 256;
+
+    const HalfStage sA0 = make_stage<true>(m0, M - 1, ldx, 0, wave, lane);
+    const HalfStage sA1 = make_stage<true>(m0, M - 1, ldx, 1, wave, lane);
+    const HalfStage sB0 = make_stage<false>(n0, N - 1, ldw, 0, wave, lane);
+    const HalfStage sB1 = make_stage<false>(n0, N - 1, ldw, 1, wave, lane);
+    char* const e_buf = smem;
+    char* const o_buf = smem + p8::BUF;
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, 0x7fffffff, 0x00020000);
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a[4][2], b[2][2];
+    int oA[2], oB[2];
+    p8_frag_offsets(oA, wm * 64 + (lane & 15), lane);
+    p8_frag_offsets(oB, wn * 32 + (lane & 15), lane);
+
+    const int nk = (int)(K / BK);
+    // K-tile byte offset; tiles past the end re-load the last K-tile (into regions nothing reads
+    // again), so every phase issues exactly 2 DMAs and the vmcnt counts stay static.
+    auto kb = [nk](int t) -> int { return (t < nk ? t : nk - 1) * (BK * 2); };
+    // prologue: K-tile 0 complete, K-tile 1 minus its B0 half (issued in phase 1)
+    issue_half(rX, sA0, 0, e_buf + p8::RA0, wave);
+    issue_half(rW, sB1, 0, e_buf + p8::RB1, wave);
+    issue_half(rX, sA1, 0, e_buf + p8::RA1, wave);
+    issue_half(rW, sB0, 0, e_buf + p8::RB0, wave);
+    issue_half(rX, sA0, kb(1), o_buf + p8::RA0, wave);
+    issue_half(rW, sB1, kb(1), o_buf + p8::RB1, wave);
+    issue_half(rX, sA1, kb(1), o_buf + p8::RA1, wave);
+    P8_VM6();
+    P8_BAR();
+    if (wm == 1) P8_BAR();  // stagger: group 1 runs one barrier behind
+
+    // Phase p restages the region last read in phase p-1 (quadrant order (0,0) (0,1) (1,1) (1,0)):
+    //   1: B0 of t+1 (odd)  2: A0 of t+2  3: B1 of t+2  4: A1 of t+2 + vmcnt(6) retires t+1
+    //   5: B0 of t+2 (even) 6: A0 of t+3  7: B1 of t+3  8: A1 of t+3 + vmcnt(6) retires t+2
+    int t0 = 0;
+    for (; t0 + 1 < nk; t0 += 2) {
+        const int k1 = kb(t0 + 1), k2 = kb(t0 + 2), k3 = kb(t0 + 3);
+        p8_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
+        p8_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
+        p8_phase<1, 0, 1, true>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
+        p8_phase<0, 0, 0, false>(acc, a, b, o_buf, oA, oB, rW, sB0, k2, e_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false>(acc, a, b, o_buf, oA, oB, rX, sA0, k3, o_buf + p8::RA0, wave);
+        p8_phase<1, 1, 2, false>(acc, a, b, o_buf, oA, oB, rW, sB1, k3, o_buf + p8::RB1, wave);
+        p8_phase<1, 0, 1, true>(acc, a, b, o_buf, oA, oB, rX, sA1, k3, o_buf + p8::RA1, wave);
+    }
+    if (t0 < nk) {  // odd K-tile count: the last tile is in the even buffer (retired by phase 8)
+        const int k1 = kb(t0 + 1), k2 = kb(t0 + 2);
+        p8_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
+        p8_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
+        p8_phase<1, 0, 1, false>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
+    }
+    if (wm == 0) P8_BAR();  // balance the stagger
+    P8_VM0();
+    __syncthreads();  // every wave is past its last LDS read: the epilogue reuses the ring
+
+    lora_epilogue<R, 128, 64>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, bias, T, theta_pop, ld_theta, offB,
+                              scale, rows_per_member, 256, M, N, Y, ldy);
+}
+
+// ------------------------------------------------------------------------------------
 // Y += scale * T B_k^T   (8 bf16 per thread)
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_lora_expand(const float* __restrict__ T, const float* __restrict__ theta_pop,
@@ -353,6 +643,31 @@ static int project(const void* X, int64_t ldx, const float* tp, int64_t ldt, int
 }
 
 static int g_tile_override = 0;
+
+static int launch_gemm8(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                        const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                        int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, hipStream_t st) {
+    const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_gemm: grid too large");
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+#define EGG_GEMM8(RV)                                                                                            \
+    hipLaunchKernelGGL((k_lora_gemm8<RV>), grid, dim3(512), 0, st, (const unsigned short*)X, ldx,                \
+                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T, theta_pop, ld_theta,      \
+                       offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy)
+    switch (r) {
+        case 0: EGG_GEMM8(0); break;
+        case 1: EGG_GEMM8(1); break;
+        case 2: EGG_GEMM8(2); break;
+        case 3: EGG_GEMM8(3); break;
+        case 4: EGG_GEMM8(4); break;
+        case 8: EGG_GEMM8(8); break;
+        case 16: EGG_GEMM8(16); break;
+        default: set_error("lora_gemm: r=%d unsupported (0,1,2,3,4,8,16)", r); return EGGROLL_ERR_UNSUPPORTED;
+    }
+#undef EGG_GEMM8
+    EGG_CHECK_LAUNCH("lora_gemm8");
+    return EGGROLL_OK;
+}
 
 template <class TL>
 static int launch_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
@@ -422,8 +737,11 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
     EGG_CHECK_ARG(X && W && Y, "lora_gemm: NULL pointer");
     EGG_CHECK_ARG(r == 0 || (T && theta_pop), "lora_gemm: T / theta_pop NULL with r > 0");
     hipStream_t st = as_stream(stream);
-    // tile choice: 256x256 when the grid still fills the chip, else 128x128
-    const int tsel = g_tile_override ? g_tile_override : ((M / 256) * ((N + 255) / 256) >= 512 ? 256 : 128);
+    // tile choice: the 8-phase 256x256 kernel when the grid still fills the chip, else 128x128
+    const int tsel = g_tile_override ? g_tile_override : ((M / 256) * ((N + 255) / 256) >= 512 ? 8 : 128);
+    if (tsel == 8)
+        return launch_gemm8(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
+                            ldy, st);
     return tsel == 256 ? launch_gemm<kT256>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
                                             rows_per_member, M, N, K, Y, ldy, st)
                        : launch_gemm<kT128>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
@@ -431,7 +749,8 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
 }
 
 extern "C" int eggroll_lora_gemm_tile(int32_t tile) {
-    EGG_CHECK_ARG(tile == 0 || tile == 128 || tile == 256, "lora_gemm_tile: tile must be 0 (auto), 128 or 256");
+    EGG_CHECK_ARG(tile == 0 || tile == 8 || tile == 128 || tile == 256,
+                  "lora_gemm_tile: tile must be 0 (auto), 8 (8-phase 256x256), 128 or 256");
     g_tile_override = tile;
     return EGGROLL_OK;
 }

@@ -193,7 +193,7 @@ def _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm):
                                  scale, rpm)
 
 
-@pytest.fixture(params=[128, 256], ids=["tile128", "tile256"])
+@pytest.fixture(params=[128, 256, 8], ids=["tile128", "tile256", "tile256x8phase"])
 def gemm_tile(request):
     from hyperscalees_t2i_amd import _lib
     _lib.call("eggroll_lora_gemm_tile", request.param)

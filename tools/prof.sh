@@ -4,5 +4,8 @@
 set -o pipefail
 name=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/$name -o run --output-format csv -- python3 bench.py "$@" > gpurun_out/$name.log 2>&1
-echo "rc=$?" >> gpurun_out/$name.log
+mkdir -p gpurun_out
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/$name -o run --output-format csv -- python3 -u bench.py "$@" > gpurun_out/$name.log 2>&1
+rc=$?
+echo "rc=$rc" >> gpurun_out/$name.log
+exit $rc
