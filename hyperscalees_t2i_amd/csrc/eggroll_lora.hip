@@ -126,7 +126,7 @@ __global__ __launch_bounds__(TL::THREADS, TL::MIN_BLOCKS) void k_lora_gemm(
     unsigned short* __restrict__ Y, int64_t ldy) {
     constexpr int FM = TL::FM, FN = TL::FN;
     __shared__ __attribute__((aligned(16))) char smem[TL::LDS];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / TL::WN, wn = wave % TL::WN;
     // XCD-aware bijective remap: consecutive tile ids (sharing X rows) land on one XCD.
     const int nwg = gridDim.x;
@@ -374,7 +374,9 @@ __device__ __forceinline__ void issue_half(__amdgpu_buffer_rsrc_t rs, const Half
         asm volatile("" ::: "memory");        \
     } while (0)
 
-template <int QA, int QB>
+// TR: W as the MFMA A-operand, i.e. the fragment is computed transposed: lane l holds Y row (l & 15),
+// columns 4 (l >> 4) .. +3 — one 8-byte LDS write in the epilogue instead of four 2-byte ones.
+template <int QA, int QB, bool TR>
 __device__ __forceinline__ void p8_mma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -384,7 +386,8 @@ __device__ __forceinline__ void p8_mma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 acc[QA * 4 + f][QB * 2 + g] =
-                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f][kk], b[g][kk], acc[QA * 4 + f][QB * 2 + g], 0, 0, 0);
+                    TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[g][kk], a[f][kk], acc[QA * 4 + f][QB * 2 + g], 0, 0, 0)
+                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f][kk], b[g][kk], acc[QA * 4 + f][QB * 2 + g], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
 }
 
@@ -410,7 +413,7 @@ __device__ __forceinline__ void p8_frag_offsets(int (&off)[2], int r0, int lane)
 #define P8_LGKM0_ asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 // One phase: read the quadrant's fragments (RD: 0 = A+B, 1 = B only, 2 = A only), issue one
 // half-tile DMA, [vmcnt(6)], retire the reads, barrier, 16 MFMA, barrier.
-template <int QA, int QB, int RD, bool VM>
+template <int QA, int QB, int RD, bool VM, bool TR>
 __device__ __forceinline__ void p8_phase(f32x4 (&acc)[8][4], bf16x8 (&a)[4][2], bf16x8 (&b)[2][2], const char* buf,
                                          const int (&oA)[2], const int (&oB)[2], __amdgpu_buffer_rsrc_t rs,
                                          const HalfStage& st, int kbytes, char* dst, int wave) {
@@ -420,7 +423,7 @@ __device__ __forceinline__ void p8_phase(f32x4 (&acc)[8][4], bf16x8 (&a)[4][2], 
     if (VM) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     P8_LGKM0_;
     P8_BAR();
-    p8_mma<QA, QB>(acc, a, b);
+    p8_mma<QA, QB, TR>(acc, a, b);
     P8_BAR();
 }
 
@@ -512,14 +515,122 @@ __device__ __forceinline__ void lora_epilogue(f32x4 (&acc)[WTM / 16][WTN / 16], 
     }
 }
 
-template <int R>
+// Store of a transposed (TR) 128x64 wave tile: acc[i][j][e] = Y[rbase + 16 i + (l & 15)]
+// [cbase + 16 j + 4 (l >> 4) + e]; 4 columns -> one ds_write_b64 into the wave's swizzled LDS
+// staging tile, then 16-B global stores of whole 128-B row segments.
+__device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int m0, int n0,
+                                             int rbase, int cbase, int M, int N, unsigned short* __restrict__ Y,
+                                             int64_t ldy) {
+    constexpr int ROWB = 128, SLOTS = 8;
+    char* ctile = smem + wave * (128 * ROWB);
+    const int r_l = lane & 15, c_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int rr = i * 16 + r_l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int cc = j * 16 + c_l;
+            const int slot = (cc >> 3) ^ (rr & (SLOTS - 1));
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = f32_to_bf16(acc[i][j][e]);
+            *reinterpret_cast<u16x4*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) = o;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int rr = it * 8 + (lane >> 3), sl = lane & 7;
+        const int row = m0 + rbase + rr;
+        const int col = n0 + cbase + sl * 8;
+        if (row >= M || col >= N) continue;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+        unsigned short* dst = Y + (int64_t)row * ldy + col;
+        if (col + 8 <= N && (((uintptr_t)dst) & 15) == 0) {
+            *reinterpret_cast<u16x8*>(dst) = v;
+        } else {
+            for (int u = 0; u < 8 && col + u < N; ++u) dst[u] = v[u];
+        }
+    }
+}
+
+__device__ __forceinline__ short bf16_bits(float f) { return (short)f32_to_bf16(f); }
+
+// acc[i][j] += L_i . R_j over one 32-deep k-step, which adds bias[n] + scale * T[m,:] . B_k[n,:] to
+// every element of the wave's 128x64 tile.  k-slots 0..7 (lanes 0-15 of a fragment) carry the
+// tile's first member a = m0 / rows_per_member, slots 8..15 (lanes 16-31) the next member b (a tile
+// spans at most two members when rows_per_member >= 256); each row puts its data in its own
+// member's block and zeros in the other:
+//   L[m] = [Th_q (R) | Tl_q (R) | Th_q (R) | 1 | 0..]      R[n] = [sBh_q | sBh_q | sBl_q | bias | 0..]
+// with T = Th + Tl and s*B = sBh + sBl split into bf16 pairs, so the product is
+// Th.sBh + Tl.sBh + Th.sBl + bias: fp32-accurate to ~2^-16 relative (the Tl.sBl term is dropped).
+// TL: T comes from the fused projection's LDS rows [256][member a q0 q1 | member b q0 q1] instead of
+// the global [M][R] array of k_lora_project.
+template <int R, bool TL = false>
+__device__ __forceinline__ void lora_mfma_addend(f32x4 (&acc)[8][4], int lane, int m0, int n0, int rbase, int cbase,
+                                                 const unsigned short* __restrict__ bias, const float* __restrict__ T,
+                                                 const float* __restrict__ theta_pop, int64_t ld_theta, int64_t offB,
+                                                 float scale, int rows_per_member, int M, int N) {
+    static_assert(3 * R + 1 <= 8, "MFMA epilogue needs 3R+1 <= 8 k-slots per member");
+    const int h = lane >> 4, l16 = lane & 15;
+    const int ma = m0 / rows_per_member;
+    const int last = (m0 + 255 < M ? m0 + 255 : M - 1);
+    const bool straddle = last / rows_per_member != ma;
+    bf16x8 rf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int col = n0 + cbase + j * 16 + l16;
+        col = col < N ? col : N - 1;
+        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (h == 0 || (h == 1 && straddle)) {
+            if constexpr (R > 0) {
+                const float* Bk = theta_pop + (int64_t)(ma + h) * ld_theta + offB;
+#pragma unroll
+                for (int q = 0; q < R; ++q) {
+                    const float sb = scale * Bk[col * R + q];
+                    const short hi = bf16_bits(sb);
+                    v[q] = hi;
+                    v[R + q] = hi;
+                    v[2 * R + q] = bf16_bits(sb - bf16_to_f32((unsigned short)hi));
+                }
+            }
+            v[3 * R] = bias ? (short)bias[col] : (short)0;
+        }
+        rf[j] = *reinterpret_cast<bf16x8*>(v);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        int row = m0 + rbase + i * 16 + l16;
+        row = row < M ? row : M - 1;
+        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (h == row / rows_per_member - ma) {
+            if constexpr (R > 0) {
+#pragma unroll
+                for (int q = 0; q < R; ++q) {
+                    const float t = TL ? T[(row - m0) * 4 + h * 2 + q] : T[(int64_t)row * R + q];
+                    const short th = bf16_bits(t);
+                    v[q] = th;
+                    v[R + q] = bf16_bits(t - bf16_to_f32((unsigned short)th));
+                    v[2 * R + q] = th;
+                }
+            }
+            v[3 * R] = (short)0x3F80;  // 1.0
+        }
+        const bf16x8 lf = *reinterpret_cast<bf16x8*>(v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)  // transposed fragments (TR main loop): D[n][m]
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rf[j], lf, acc[i][j], 0, 0, 0);
+    }
+}
+
+template <int R, bool MF, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
     const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
     int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int M, int N, int64_t K, int tiles_n,
     unsigned short* __restrict__ Y, int64_t ldy) {
     __shared__ __attribute__((aligned(16))) char smem[p8::LDS];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     // XCD-aware bijective remap + grouped rasterisation (as k_lora_gemm).
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -533,6 +644,10 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
     const int m0 = tm * 256, n0 = tn * 256;
 
+    if constexpr (DIAG == 2) {  // diagnostic: desynchronise the first round by half a tile on odd blocks
+        if (bid < 256 && (bid & 1))
+            for (int z = 0; z < 6; ++z) __builtin_amdgcn_s_sleep(127);
+    }
     const HalfStage sA0 = make_stage<true>(m0, M - 1, ldx, 0, wave, lane);
     const HalfStage sA1 = make_stage<true>(m0, M - 1, ldx, 1, wave, lane);
     const HalfStage sB0 = make_stage<false>(n0, N - 1, ldw, 0, wave, lane);
@@ -574,28 +689,43 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     int t0 = 0;
     for (; t0 + 1 < nk; t0 += 2) {
         const int k1 = kb(t0 + 1), k2 = kb(t0 + 2), k3 = kb(t0 + 3);
-        p8_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
-        p8_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
-        p8_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
-        p8_phase<1, 0, 1, true>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
-        p8_phase<0, 0, 0, false>(acc, a, b, o_buf, oA, oB, rW, sB0, k2, e_buf + p8::RB0, wave);
-        p8_phase<0, 1, 1, false>(acc, a, b, o_buf, oA, oB, rX, sA0, k3, o_buf + p8::RA0, wave);
-        p8_phase<1, 1, 2, false>(acc, a, b, o_buf, oA, oB, rW, sB1, k3, o_buf + p8::RB1, wave);
-        p8_phase<1, 0, 1, true>(acc, a, b, o_buf, oA, oB, rX, sA1, k3, o_buf + p8::RA1, wave);
+        p8_phase<0, 0, 0, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false, MF>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
+        p8_phase<1, 1, 2, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
+        p8_phase<1, 0, 1, true, MF>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
+        p8_phase<0, 0, 0, false, MF>(acc, a, b, o_buf, oA, oB, rW, sB0, k2, e_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false, MF>(acc, a, b, o_buf, oA, oB, rX, sA0, k3, o_buf + p8::RA0, wave);
+        p8_phase<1, 1, 2, false, MF>(acc, a, b, o_buf, oA, oB, rW, sB1, k3, o_buf + p8::RB1, wave);
+        p8_phase<1, 0, 1, true, MF>(acc, a, b, o_buf, oA, oB, rX, sA1, k3, o_buf + p8::RA1, wave);
     }
     if (t0 < nk) {  // odd K-tile count: the last tile is in the even buffer (retired by phase 8)
         const int k1 = kb(t0 + 1), k2 = kb(t0 + 2);
-        p8_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
-        p8_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
-        p8_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
-        p8_phase<1, 0, 1, false>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
+        p8_phase<0, 0, 0, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false, MF>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
+        p8_phase<1, 1, 2, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
+        p8_phase<1, 0, 1, false, MF>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
     }
     if (wm == 0) P8_BAR();  // balance the stagger
     P8_VM0();
     __syncthreads();  // every wave is past its last LDS read: the epilogue reuses the ring
 
-    lora_epilogue<R, 128, 64>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, bias, T, theta_pop, ld_theta, offB,
-                              scale, rows_per_member, 256, M, N, Y, ldy);
+    if constexpr (DIAG == 1) {  // diagnostic: main loop only (acc kept live, one store per lane)
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (sum == 1234.5f) Y[tid] = 1;
+        return;
+    }
+    if constexpr (MF) {  // bias + LoRA term as one extra MFMA k-step, then a plain bf16 store
+        lora_mfma_addend<R>(acc, lane, m0, n0, wm * 128, wn * 64, bias, T, theta_pop, ld_theta, offB, scale,
+                            rows_per_member, M, N);
+        store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, M, N, Y, ldy);
+    } else {
+        lora_epilogue<R, 128, 64>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, bias, T, theta_pop, ld_theta,
+                                  offB, scale, rows_per_member, 256, M, N, Y, ldy);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -642,8 +772,249 @@ static int project(const void* X, int64_t ldx, const float* tp, int64_t ldt, int
     return EGGROLL_OK;
 }
 
+// ------------------------------------------------------------------------------------
+// Fused-projection variant of the 8-phase kernel (r <= 2, rows_per_member >= 256): T = X A_k^T is
+// computed inside the GEMM from the X fragments already in registers, so X is read from HBM once
+// per LoRA linear instead of twice (k_lora_project's pre-pass is gone).
+//   AK[k][16][K] bf16 (k_lora_ak): rows q < R hold hi(A_k[q]), rows R+q lo(A_k[q] - hi), rest 0.
+//   Per K-tile a 2 KiB AK block is DMA'd next to the half-tiles: LDS rows 0..7 = member a (the
+//   tile's first member), rows 8..15 = member b (the next one; a tile spans at most two).
+//   In phases 2 and 4 (resp. 6, 8) wave (wm, wn) runs one extra transposed MFMA per k-substep on
+//   its X fragment f = wn:  D[q][m] += AK[q, k] X[m, k]  -> 4 MFMA per K-tile per wave (+6.25 %).
+//   At the end T[m][q] = D[q] + D[R + q] (hi + lo) per member goes to LDS for the MFMA epilogue.
+// ------------------------------------------------------------------------------------
+namespace p8f {
+constexpr int AKB = 2048;                  // AK block per K-tile: 16 rows x 64 bf16
+constexpr int BUF = p8::BUF + AKB;         // 66 KiB per K-tile buffer
+constexpr int RK = p8::BUF;                // AK region inside a buffer
+constexpr int TOFF = 2 * BUF;              // T rows after the ring: [256][4] fp32
+constexpr int LDS = TOFF + 256 * 4 * 4;    // 136 KiB
+}  // namespace p8f
+
+__global__ __launch_bounds__(256) void k_lora_ak(const float* __restrict__ theta_pop, int64_t ld_theta, int64_t offA,
+                                                 int R, int64_t K, int n_members, unsigned short* __restrict__ AK) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one thread per 8 elements
+    const int64_t per_row = K / 8, total = (int64_t)n_members * 16 * per_row;
+    if (idx >= total) return;
+    const int64_t c = (idx % per_row) * 8;
+    const int row = (int)((idx / per_row) % 16);
+    const int k = (int)(idx / (per_row * 16));
+    u16x8 o;
+    if (row < 2 * R) {
+        const int q = row % R;
+        const float* A = theta_pop + (int64_t)k * ld_theta + offA + (int64_t)q * K + c;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const unsigned short hi = f32_to_bf16(A[u]);
+            o[u] = row < R ? hi : f32_to_bf16(A[u] - bf16_to_f32(hi));
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = 0;
+    }
+    *reinterpret_cast<u16x8*>(AK + ((int64_t)k * 16 + row) * K + c) = o;
+}
+
+template <int R>
+__global__ __launch_bounds__(512, 1) void k_lora_gemm8f(
+    const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
+    const unsigned short* __restrict__ bias, const unsigned short* __restrict__ AK, const float* __restrict__ theta_pop,
+    int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int n_members, int M, int N, int64_t K,
+    int tiles_n, unsigned short* __restrict__ Y, int64_t ldy) {
+    __shared__ __attribute__((aligned(16))) char smem[p8f::LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+    const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+    const int tiles_m = (M + 255) / 256;
+    const int per_group = GROUP_M * tiles_n;
+    const int grp = tile / per_group, first_m = grp * GROUP_M;
+    const int gsize = (tiles_m - first_m) < GROUP_M ? (tiles_m - first_m) : GROUP_M;
+    const int in_grp = tile - grp * per_group;
+    const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
+    const int m0 = tm * 256, n0 = tn * 256;
+
+    const HalfStage sA0 = make_stage<true>(m0, M - 1, ldx, 0, wave, lane);
+    const HalfStage sA1 = make_stage<true>(m0, M - 1, ldx, 1, wave, lane);
+    const HalfStage sB0 = make_stage<false>(n0, N - 1, ldw, 0, wave, lane);
+    const HalfStage sB1 = make_stage<false>(n0, N - 1, ldw, 1, wave, lane);
+    // AK DMA: one dword per lane per K-tile; wave w fills LDS AK rows 2w, 2w+1 (swizzled like the tiles)
+    const int ma = m0 / rows_per_member;
+    const int mb = (ma + 1 < n_members) ? ma + 1 : ma;
+    uint32_t akoff;
+    {
+        const int row = 2 * wave + (lane >> 5), d = lane & 31, slot = d >> 2;
+        const int src_row = (row < 8 ? ma : mb) * 16 + (row & 7);
+        const int chunk = slot ^ (row & 7);
+        akoff = ((uint32_t)src_row * (uint32_t)K + chunk * 8 + (d & 3) * 2) * 2;
+    }
+    char* const e_buf = smem;
+    char* const o_buf = smem + p8f::BUF;
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rK = __builtin_amdgcn_make_buffer_rsrc((void*)AK, (short)0, 0x7fffffff, 0x00020000);
+    auto issue_ak = [&](int kbytes, char* buf) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (lds_void*)(buf + p8f::RK + wave * 256), 4, akoff, kbytes, 0, 0);
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 tacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    bf16x8 a[4][2], b[2][2], ak[2];
+    int oA[2], oB[2], oK[2];
+    p8_frag_offsets(oA, wm * 64 + (lane & 15), lane);
+    p8_frag_offsets(oB, wn * 32 + (lane & 15), lane);
+    p8_frag_offsets(oK, lane & 15, lane);
+
+    auto tmma = [&](int h) {  // T-MFMA on this wave's X fragment f = wn (wave-uniform branches, no selects)
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            if (wn == 0) tacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak[kk], a[0][kk], tacc[h], 0, 0, 0);
+            else if (wn == 1) tacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak[kk], a[1][kk], tacc[h], 0, 0, 0);
+            else if (wn == 2) tacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak[kk], a[2][kk], tacc[h], 0, 0, 0);
+            else tacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak[kk], a[3][kk], tacc[h], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto read_ak = [&](const char* buf) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) ak[kk] = *reinterpret_cast<const bf16x8*>(buf + p8f::RK + oK[kk]);
+    };
+
+    const int nk = (int)(K / BK);
+    auto kb = [nk](int t) -> int { return (t < nk ? t : nk - 1) * (BK * 2); };
+    issue_half(rX, sA0, 0, e_buf + p8::RA0, wave);
+    issue_half(rW, sB1, 0, e_buf + p8::RB1, wave);
+    issue_ak(0, e_buf);
+    issue_half(rX, sA1, 0, e_buf + p8::RA1, wave);
+    issue_half(rW, sB0, 0, e_buf + p8::RB0, wave);
+    issue_half(rX, sA0, kb(1), o_buf + p8::RA0, wave);
+    issue_half(rW, sB1, kb(1), o_buf + p8::RB1, wave);
+    issue_ak(kb(1), o_buf);
+    issue_half(rX, sA1, kb(1), o_buf + p8::RA1, wave);
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    P8_BAR();
+    if (wm == 1) P8_BAR();
+
+    // As k_lora_gemm8, plus: AK read in phase 2/6 (last read -> restaged with B1 in phase 3/7),
+    // T-MFMA on A0 in phase 2/6 and on A1 in phase 4/8; 7 DMAs issued after a buffer's last one.
+#define P8F_K(buf_, dst_, kA, kB, DO_TAIL)                                                          \
+    /* phase 1 */                                                                                   \
+    p8_read_b(b, buf_ + p8::RB0, oB);                                                               \
+    p8_read_a(a, buf_ + p8::RA0, oA);                                                               \
+    issue_half(rW, sB0, kA, (buf_ == e_buf ? o_buf : e_buf) + p8::RB0, wave);                       \
+    P8_LGKM0_;                                                                                      \
+    P8_BAR();                                                                                       \
+    p8_mma<0, 0, true>(acc, a, b);                                                                  \
+    P8_BAR();                                                                                       \
+    /* phase 2 */                                                                                   \
+    p8_read_b(b, buf_ + p8::RB1, oB);                                                               \
+    read_ak(buf_);                                                                                  \
+    issue_half(rX, sA0, kB, dst_ + p8::RA0, wave);                                                  \
+    P8_LGKM0_;                                                                                      \
+    P8_BAR();                                                                                       \
+    p8_mma<0, 1, true>(acc, a, b);                                                                  \
+    tmma(0);                                                                                        \
+    P8_BAR();                                                                                       \
+    /* phase 3 */                                                                                   \
+    p8_read_a(a, buf_ + p8::RA1, oA);                                                               \
+    issue_half(rW, sB1, kB, dst_ + p8::RB1, wave);                                                  \
+    issue_ak(kB, dst_);                                                                             \
+    P8_LGKM0_;                                                                                      \
+    P8_BAR();                                                                                       \
+    p8_mma<1, 1, true>(acc, a, b);                                                                  \
+    P8_BAR();                                                                                       \
+    /* phase 4 */                                                                                   \
+    p8_read_b(b, buf_ + p8::RB0, oB);                                                               \
+    issue_half(rX, sA1, kB, dst_ + p8::RA1, wave);                                                  \
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");                                                \
+    P8_LGKM0_;                                                                                      \
+    P8_BAR();                                                                                       \
+    p8_mma<1, 0, true>(acc, a, b);                                                                  \
+    tmma(1);                                                                                        \
+    P8_BAR();
+
+    int t0 = 0;
+    for (; t0 + 1 < nk; t0 += 2) {
+        const int k1 = kb(t0 + 1), k2 = kb(t0 + 2), k3 = kb(t0 + 3);
+        // even buffer: tile t0; phase 1 restages B0 of t0+1 (odd), phases 2-4 tile t0+2 (even)
+        P8F_K(e_buf, e_buf, k1, k2, 0)
+        // odd buffer: tile t0+1; phase 5 restages B0 of t0+2 (even), phases 6-8 tile t0+3 (odd)
+        P8F_K(o_buf, o_buf, k2, k3, 0)
+    }
+    if (t0 < nk) {
+        const int k1 = kb(t0 + 1), k2 = kb(t0 + 2);
+        P8F_K(e_buf, e_buf, k1, k2, 1)
+    }
+#undef P8F_K
+    if (wm == 0) P8_BAR();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // T rows -> LDS: lanes 0-15 hold member a's D rows 0..3, lanes 32-47 member b's D rows 8..11
+    {
+        float* Tl = reinterpret_cast<float*>(smem + p8f::TOFF);
+        const int hq = lane >> 4;
+        if (hq == 0 || hq == 2) {
+            const int mem = hq >> 1;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int rl = wm * 128 + h * 64 + wn * 16 + (lane & 15);
+#pragma unroll
+                for (int qq = 0; qq < R; ++qq) Tl[rl * 4 + mem * 2 + qq] = tacc[h][qq] + tacc[h][R + qq];
+            }
+        }
+    }
+    __syncthreads();
+    lora_mfma_addend<R, true>(acc, lane, m0, n0, wm * 128, wn * 64, bias,
+                              reinterpret_cast<const float*>(smem + p8f::TOFF), theta_pop, ld_theta, offB, scale,
+                              rows_per_member, M, N);
+    store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, M, N, Y, ldy);
+}
+
 static int g_tile_override = 0;
 
+// The fused-projection kernel is opt-in (tile 12): measured at the Sana shapes it is 1-10 % SLOWER
+// than k_lora_project + k_lora_gemm8 (1.205 vs 1.189 ms at 131072x2240x2240, 5.82 vs 5.25 ms at
+// N = 11200) — the extra AK DMA and T-MFMA per K-tile cost more than the 10 % X re-read they save.
+static bool fused_ok(int32_t r, int64_t M, int64_t N, int64_t K, int64_t rows_per_member) {
+    (void)M;
+    (void)N;
+    return g_tile_override == 12 && (r == 1 || r == 2) && rows_per_member >= 256 && K % 64 == 0;
+}
+
+static int launch_gemm8f(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                         const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r, float scale,
+                         int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, void* ws,
+                         hipStream_t st) {
+    const int64_t n_members = (M + rows_per_member - 1) / rows_per_member;
+    EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31) && n_members * 16 * K * 2 < (1ll << 31),
+                  "lora_linear_pop: operand > 2 GiB");
+    unsigned short* AK = reinterpret_cast<unsigned short*>(ws);
+    const int64_t work = n_members * 16 * (K / 8);
+    hipLaunchKernelGGL(k_lora_ak, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, theta_pop, ld_theta, offA,
+                       (int)r, K, (int)n_members, AK);
+    EGG_CHECK_LAUNCH("lora_ak");
+    const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+    if (r == 1)
+        hipLaunchKernelGGL((k_lora_gemm8f<1>), grid, dim3(512), 0, st, (const unsigned short*)X, ldx,
+                           (const unsigned short*)W, ldw, (const unsigned short*)bias, AK, theta_pop, ld_theta, offB,
+                           scale, (int)rows_per_member, (int)n_members, (int)M, (int)N, K, (int)tiles_n,
+                           (unsigned short*)Y, ldy);
+    else
+        hipLaunchKernelGGL((k_lora_gemm8f<2>), grid, dim3(512), 0, st, (const unsigned short*)X, ldx,
+                           (const unsigned short*)W, ldw, (const unsigned short*)bias, AK, theta_pop, ld_theta, offB,
+                           scale, (int)rows_per_member, (int)n_members, (int)M, (int)N, K, (int)tiles_n,
+                           (unsigned short*)Y, ldy);
+    EGG_CHECK_LAUNCH("lora_gemm8f");
+    return EGGROLL_OK;
+}
+
+template <bool MF>
 static int launch_gemm8(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
                         const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
                         int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, hipStream_t st) {
@@ -651,7 +1022,7 @@ static int launch_gemm8(const void* X, int64_t ldx, const void* W, int64_t ldw, 
     EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_gemm: grid too large");
     const dim3 grid((unsigned)(tiles_m * tiles_n));
 #define EGG_GEMM8(RV)                                                                                            \
-    hipLaunchKernelGGL((k_lora_gemm8<RV>), grid, dim3(512), 0, st, (const unsigned short*)X, ldx,                \
+    hipLaunchKernelGGL((k_lora_gemm8<RV, MF && (RV <= 2)>), grid, dim3(512), 0, st, (const unsigned short*)X, ldx,                \
                        (const unsigned short*)W, ldw, (const unsigned short*)bias, T, theta_pop, ld_theta,      \
                        offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy)
     switch (r) {
@@ -739,9 +1110,32 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
     hipStream_t st = as_stream(stream);
     // tile choice: the 8-phase 256x256 kernel when the grid still fills the chip, else 128x128
     const int tsel = g_tile_override ? g_tile_override : ((M / 256) * ((N + 255) / 256) >= 512 ? 8 : 128);
-    if (tsel == 8)
-        return launch_gemm8(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
-                            ldy, st);
+    if (tsel == 10) {  // diagnostic: 8-phase main loop without epilogue (r ignored)
+        const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
+        hipLaunchKernelGGL((k_lora_gemm8<0, false, 1>), dim3((unsigned)(tiles_m * tiles_n)), dim3(512), 0, st,
+                           (const unsigned short*)X, ldx, (const unsigned short*)W, ldw, (const unsigned short*)bias,
+                           T, theta_pop, ld_theta, offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n,
+                           (unsigned short*)Y, ldy);
+        EGG_CHECK_LAUNCH("lora_gemm8_diag");
+        return EGGROLL_OK;
+    }
+    if (tsel == 11) {  // diagnostic: tile 9 with a desynchronised first round
+        const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
+        hipLaunchKernelGGL((k_lora_gemm8<0, false, 2>), dim3((unsigned)(tiles_m * tiles_n)), dim3(512), 0, st,
+                           (const unsigned short*)X, ldx, (const unsigned short*)W, ldw, (const unsigned short*)bias,
+                           T, theta_pop, ld_theta, offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n,
+                           (unsigned short*)Y, ldy);
+        EGG_CHECK_LAUNCH("lora_gemm8_diag");
+        return EGGROLL_OK;
+    }
+    if (tsel == 8 || tsel == 9 || tsel == 12) {
+        EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_gemm: operand > 2 GiB");
+        const bool mf = tsel != 9 && r <= 2 && rows_per_member >= 256;
+        return mf ? launch_gemm8<true>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
+                                              rows_per_member, M, N, K, Y, ldy, st)
+                         : launch_gemm8<false>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
+                                               rows_per_member, M, N, K, Y, ldy, st);
+    }
     return tsel == 256 ? launch_gemm<kT256>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
                                             rows_per_member, M, N, K, Y, ldy, st)
                        : launch_gemm<kT128>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
@@ -749,10 +1143,20 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
 }
 
 extern "C" int eggroll_lora_gemm_tile(int32_t tile) {
-    EGG_CHECK_ARG(tile == 0 || tile == 8 || tile == 128 || tile == 256,
-                  "lora_gemm_tile: tile must be 0 (auto), 8 (8-phase 256x256), 128 or 256");
+    EGG_CHECK_ARG(tile == 0 || tile == 8 || tile == 9 || tile == 10 || tile == 11 || tile == 12 || tile == 128 ||
+                      tile == 256,
+                  "lora_gemm_tile: tile must be 0 (auto), 8 / 9 (8-phase 256x256 with MFMA / VALU LoRA "
+                  "epilogue), 12 (8-phase with the projection fused), 128 or 256");
     g_tile_override = tile;
     return EGGROLL_OK;
+}
+
+int64_t eggroll_lora_workspace_bytes(int64_t M, int64_t K, int32_t r, int64_t rows_per_member) {
+    if (M <= 0 || r <= 0 || rows_per_member <= 0) return 0;
+    const int64_t t_bytes = M * r * 4;
+    const int64_t n_members = (M + rows_per_member - 1) / rows_per_member;
+    const int64_t ak_bytes = n_members * 16 * K * 2;
+    return t_bytes > ak_bytes ? t_bytes : ak_bytes;
 }
 
 int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
@@ -762,6 +1166,13 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
     EGG_CHECK_ARG(K > 0 && K % 64 == 0, "lora_linear_pop: K=%lld must be a multiple of 64", (long long)K);
     EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_linear_pop: r=%d out of range", r);
     if (M == 0) return EGGROLL_OK;
+    if (r > 0 && fused_ok(r, M, N, K, rows_per_member)) {  // projection fused into the 8-phase GEMM
+        EGG_CHECK_ARG(X && W && Y && theta_pop && T_ws, "lora_linear_pop: NULL pointer");
+        EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop: bad strides");
+        EGG_CHECK_ARG(ld_theta % 4 == 0 && offA % 4 == 0, "lora_linear_pop: theta offsets must be 16-byte aligned");
+        return launch_gemm8f(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale, rows_per_member, M, N,
+                             K, Y, ldy, T_ws, as_stream(stream));
+    }
     if (r > 0) {
         EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop: theta_pop / T_ws NULL with r > 0");
         int rc = eggroll_lora_project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T_ws, stream);

@@ -221,8 +221,9 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
         n_members = -(-M // rows_per_member)
         if theta_pop.shape[0] < n_members:
             raise ValueError(f"theta_pop has {theta_pop.shape[0]} members, rows need {n_members}")
-        if T_ws is None or T_ws.numel() < M * r:
-            T_ws = torch.empty(M * r, dtype=torch.float32, device=x.device)
+        need = lora_workspace_numel(M, K, r, rows_per_member)
+        if T_ws is None or T_ws.numel() < need:
+            T_ws = torch.empty(need, dtype=torch.float32, device=x.device)
         ld_t = theta_pop.stride(0)
     else:
         ld_t = 0
@@ -230,6 +231,19 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
               _p(theta_pop) if r > 0 else None, ld_t, offA, offB, r, float(scale), rows_per_member, M, N, K,
               out.data_ptr(), out.stride(0), _p(T_ws) if r > 0 else None, _stream(x.device))
     return out
+
+
+def lora_workspace_numel(M: int, K: int, r: int, rows_per_member: int) -> int:
+    """fp32 elements of the eggroll_lora_linear_pop workspace (T, or the fused path's A_k images)."""
+    nbytes = int(_lib.load().eggroll_lora_workspace_bytes(M, K, r, rows_per_member))
+    return max(1, -(-nbytes // 4))
+
+
+def lora_fused(M: int, N: int, K: int, r: int, rows_per_member: int, tile: int = 0) -> bool:
+    """True when eggroll_lora_linear_pop runs the projection inside the 8-phase GEMM (mirrors
+    fused_ok in eggroll_lora.hip): only with kernel 12 forced — the automatic choice is the
+    two-pass k_lora_project + k_lora_gemm8, which measured faster at every Sana shape."""
+    return tile == 12 and r in (1, 2) and rows_per_member >= 256 and K % 64 == 0
 
 
 def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T: Optional[torch.Tensor],
@@ -250,8 +264,9 @@ def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T:
 
 
 def gemm_tile_for(M: int, N: int) -> int:
-    """Tile libeggroll's automatic choice uses for an M x N LoRA GEMM (mirrors eggroll_lora_gemm)."""
-    return 256 if (M // 256) * ((N + 255) // 256) >= 512 else 128
+    """Kernel libeggroll's automatic choice uses for an M x N LoRA GEMM (mirrors eggroll_lora_gemm):
+    8 = the 8-phase 256x256 kernel, 128 = the 128x128 one-barrier tile."""
+    return 8 if (M // 256) * ((N + 255) // 256) >= 512 else 128
 
 
 def lora_project(x: torch.Tensor, theta_pop: torch.Tensor, offA: int, r: int, rows_per_member: int,

@@ -42,7 +42,7 @@ class PopulationContext:
 
 class GemmTimer:
     """Opt-in live timing of every population LoRA GEMM launch with HIP events recorded on the
-    launching stream (bench.py's roofline leg).  Records (start, end, M, N, K, r)."""
+    launching stream (bench.py's roofline leg).  Records (start, end, M, N, K, r, rows_per_member)."""
 
     active = False
     records: List[tuple] = []
@@ -53,14 +53,19 @@ class GemmTimer:
 
     @classmethod
     def summary(cls) -> Dict[str, Dict[str, float]]:
-        """Per kernel variant (the tile libeggroll picks for each shape, i.e. what rocprof names
-        k_lora_gemm<r, Tile<t,...>>) and "all": launches, total/avg time, algorithmic FLOP."""
+        """Per kernel variant (what rocprof names: k_lora_gemm8<r> (8-phase 256x256) or
+        k_lora_gemm<r,Tile<128>>, each after its k_lora_project<r> pre-pass) and "all": calls,
+        total/avg time of the whole LoRA linear (every launch between the two events), algorithmic
+        FLOP = 2MNK (base) + 2MKr (projection) + 2MNr (rank-r expansion)."""
         torch.cuda.synchronize()
         out: Dict[str, Dict[str, float]] = {}
-        for s, e, M, N, Kd, r in cls.records:
+        for s, e, M, N, Kd, r, rpm in cls.records:
             ms = s.elapsed_time(e)
-            fl = 2.0 * M * N * Kd + 2.0 * M * N * r  # base GEMM + rank-r epilogue
-            for key in (f"k_lora_gemm<{r},Tile<{K.gemm_tile_for(M, N)}>>", "all"):
+            fl = 2.0 * M * N * Kd + 2.0 * M * Kd * r + 2.0 * M * N * r
+            t = K.gemm_tile_for(M, N)
+            name = (f"k_lora_gemm8<{r}>+k_lora_project<{r}>" if t == 8 else
+                    f"k_lora_gemm<{r},Tile<{t}>>+k_lora_project<{r}>")
+            for key in (name, "all"):
                 d = out.setdefault(key, {"launches": 0, "total_ms": 0.0, "flops": 0.0})
                 d["launches"] += 1
                 d["total_ms"] += ms
@@ -121,16 +126,17 @@ class LoRALinear(nn.Module):
             if M % ctx.n_members:
                 raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")
             rpm = M // ctx.n_members
-            T = ctx.workspace(M * self.r, x2.device)[: M * self.r].view(M, self.r)
-            K.lora_project(x2, ctx.theta_pop, self.theta_off_A, self.r, rpm, out=T)
+            ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device)
             if GemmTimer.active:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            y = K.lora_gemm(x2, self.weight, self.bias, T, ctx.theta_pop, self.theta_off_B, self.r, self.scale, rpm)
+            # projection T = X A_k^T + GEMM + LoRA epilogue (one fused kernel when eligible)
+            y = K.lora_linear_pop(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
+                                  self.r, self.scale, rpm, T_ws=ws)
             if GemmTimer.active:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
-                GemmTimer.records.append((e0, e1, M, self.out_features, self.in_features, self.r))
+                GemmTimer.records.append((e0, e1, M, self.out_features, self.in_features, self.r, rpm))
         elif self.r:
             # single member: this module's own (unflattened) lora_A / lora_B
             A = self.lora_A.weight.detach()

@@ -120,7 +120,11 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
  * Ak = theta_pop[k_local*ld_theta + offA] as [r][K]; Bk = theta_pop[... + offB] as [N][r]
  * (PEFT lora_A.weight / lora_B.weight row-major inside theta_k).
  * X, W, Y bf16 row-major (ldx, ldw, ldy in elements); bias bf16 or NULL; theta_pop fp32.
- * T_ws: fp32 workspace [M, r].  Requires K % 64 == 0, r <= 16, ldx/ldw % 8 == 0.      */
+ * T_ws: workspace of >= eggroll_lora_workspace_bytes(M, K, r, rows_per_member) bytes,
+ * 16-byte aligned (fp32 T [M, r] for the two-pass path; bf16 hi/lo A_k images [members][16][K]
+ * when the projection is fused into the GEMM: tile 12 forced, r <= 2, rows_per_member >= 256).
+ * Requires K % 64 == 0, r <= 16, ldx/ldw % 8 == 0.                                        */
+int64_t eggroll_lora_workspace_bytes(int64_t M, int64_t K, int32_t r, int64_t rows_per_member);
 int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw,
                             const void* bias, const float* theta_pop, int64_t ld_theta,
                             int64_t offA, int64_t offB, int32_t r, float scale,
@@ -134,8 +138,12 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
                       const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
                       int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
                       int64_t K, void* Y, int64_t ldy, void* stream);
-/* Tile selection of the LoRA GEMM for A/B measurement: 0 = automatic (256x256 when the grid
- * fills the chip, else 128x128), 128 or 256 force a tile.  Process-global; not thread-safe.   */
+/* Kernel selection of the LoRA GEMM for A/B measurement: 0 = automatic (8-phase 256x256 when the
+ * grid fills the chip, else 128x128); 8 = 8-phase with MFMA epilogue, 9 = 8-phase with VALU
+ * epilogue, 12 = as 8 plus the projection fused into the GEMM in eggroll_lora_linear_pop (opt-in:
+ * slower than the two-pass path at the Sana shapes), 128 / 256 = one-barrier tiles;
+ * 10 / 11 are diagnostics (main loop only; desynchronised first round) that write garbage.
+ * Process-global; not thread-safe.                                                         */
 int eggroll_lora_gemm_tile(int32_t tile);
 int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
                          int64_t offA, int32_t r, int64_t rows_per_member, int64_t M, int64_t K,

@@ -193,7 +193,8 @@ def _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm):
                                  scale, rpm)
 
 
-@pytest.fixture(params=[128, 256, 8], ids=["tile128", "tile256", "tile256x8phase"])
+@pytest.fixture(params=[128, 256, 8, 9, 12],
+                ids=["tile128", "tile256", "tile8phase_mfma", "tile8phase_valu", "tile8phase_fused_proj"])
 def gemm_tile(request):
     from hyperscalees_t2i_amd import _lib
     _lib.call("eggroll_lora_gemm_tile", request.param)
@@ -207,6 +208,7 @@ def gemm_tile(request):
     (1000, 2240, 256, 2, 300),    # Sana cross-attn-like members of 300 rows
     (512, 96, 192, 4, 128),       # r = 4 (VAR-like lora rank)
     (64, 32, 2240, 2, 16),        # proj_out-like N = 32, time-embed rows per member = 16
+    (1536, 320, 512, 1, 700),     # r = 1, tiles straddling two members (MFMA epilogue member blocks)
 ])
 def test_lora_linear_pop_vs_fp64(dev, gemm_tile, M, N, Kd, r, rpm):
     x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm)

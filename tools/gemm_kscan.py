@@ -17,7 +17,7 @@ M, N, rpm = 131072, 2240, 16384
 _lib.call("eggroll_lora_gemm_tile", tile)
 res = {}
 bufs = {}
-for Kd in (1120, 2240, 4480):
+for Kd in (1152, 2240, 4608):
     x = (torch.rand(M, Kd, device=dev) * 2 - 1).bfloat16()
     W = ((torch.rand(N, Kd, device=dev) * 2 - 1) * 0.05).bfloat16()
     b = torch.randn(N, device=dev).bfloat16()
@@ -34,7 +34,7 @@ for (Kd, r), v in res.items():
     out[f"K{Kd}_r{r}_ms"] = round(ms, 4)
     out[f"K{Kd}_r{r}_tf"] = round(2 * M * N * Kd / ms / 1e9, 1)
 for r in (0, 2):
-    slope = (out[f"K4480_r{r}_ms"] - out[f"K1120_r{r}_ms"]) / 3360
+    slope = (out[f"K4608_r{r}_ms"] - out[f"K1152_r{r}_ms"]) / 3456
     out[f"r{r}_fixed_ms"] = round(out[f"K2240_r{r}_ms"] - slope * 2240, 4)
     out[f"r{r}_loop_tf"] = round(2 * M * N / slope / 1e9, 1)
 print(json.dumps(out), flush=True)
