@@ -125,43 +125,6 @@ def build(args, world, rank, device):
     return backend, engine, noiser, theta, pop
 
 
-def aux_kernel_rooflines(engine, noiser, theta, pop, device):
-    """HBM-bound kernels timed with HIP events on the current stream (algorithmic bytes)."""
-    from hyperscalees_t2i_amd import kernels as K
-    lay = noiser.layout
-    nb = noiser.n_base(pop)
-    out = {}
-
-    def t(fn, it=10):
-        fn()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(it):
-            fn()
-        e.record()
-        torch.cuda.synchronize()
-        return s.elapsed_time(e) / it * 1e-3
-
-    fac = noiser.sample_factors(pop, device, seed=0)
-    sec = t(lambda: K.noise_factors(0, nb, lay, device, out=fac))
-    byt = 4.0 * nb * lay.factor_len
-    out["noise_factors"] = {"us": sec * 1e6, "bytes": byt, "GBps": byt / sec / 1e9, "frac": byt / sec / 1e9 / HBM_PEAK_GBPS}
-    nl = engine.hi - engine.lo
-    sec = t(lambda: noiser.perturb(theta, fac, pop, engine.lo, engine.hi, out=engine.theta_pop[:nl]))
-    byt = 4.0 * (nl * lay.D + lay.D + nb * lay.factor_len)
-    out["perturb"] = {"us": sec * 1e6, "bytes": byt, "GBps": byt / sec / 1e9, "frac": byt / sec / 1e9 / HBM_PEAK_GBPS}
-    S = torch.randn(pop, 4, device=device) + 21
-    fit = K.fitness(S, True)
-    sec = t(lambda: K.fitness(S, True))
-    out["fitness"] = {"us": sec * 1e6, "note": "latency-bound single workgroup (64x4 input)"}
-    newt = torch.empty_like(theta)
-    sec = t(lambda: noiser.update_from_factors(theta, fac, fit, pop, 0.0, 40.0, out=newt))
-    byt = 4.0 * (nb * lay.factor_len + 2 * lay.D)
-    out["update"] = {"us": sec * 1e6, "bytes": byt, "GBps": byt / sec / 1e9, "frac": byt / sec / 1e9 / HBM_PEAK_GBPS}
-    return out
-
-
 def marker():
     """One tiny k_philox_words launch: brackets the timed region in rocprofv3 kernel traces."""
     from hyperscalees_t2i_amd import kernels as K
@@ -212,7 +175,8 @@ def main():
     # one extra instrumented epoch for the per-phase breakdown (not part of the timed region)
     theta, _ = engine.step(theta, seed=10_000, guidance_scale=guidance, timing=True)
     phases = dict(engine.timings)
-    aux = aux_kernel_rooflines(engine, noiser, theta, pop, device)
+    from hyperscalees_t2i_amd.measure import aux_kernel_rooflines
+    aux = aux_kernel_rooflines(noiser.layout, pop, engine.lo, engine.hi, device, theta=theta)
 
     value = pop * args.steps / elapsed
     variants = {k: v for k, v in gemm.items() if k != "all"}

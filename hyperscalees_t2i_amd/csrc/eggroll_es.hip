@@ -24,16 +24,19 @@ void set_error(const char* fmt, ...) {
 // ------------------------------------------------------------------------------------
 // (1) noise factors
 // ------------------------------------------------------------------------------------
+// Box-Muller on the CDNA4 transcendental unit: v_log_f32 (log2), v_sqrt_f32 and v_sin_f32 /
+// v_cos_f32 (which take their argument in revolutions: sin(2 pi x)), ~10 VALU ops per pair instead
+// of the ~60 of the correctly-rounded libm expansions — the noise kernel becomes HBM-bound instead
+// of VALU-bound.  Accuracy vs the oracle's correctly-rounded fp32 restatement is pinned by
+// tests/test_gpu_kernels.py (|dz| <= 2e-5).
 __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float& z0, float& z1) {
 #pragma clang fp contract(off)
     // 23-bit uniforms: exact in fp32.  u1 in (0,1), u2 in [0,1).
     const float u1 = ((float)(w0 >> 9) + 0.5f) * 1.1920928955078125e-07f;  // 2^-23
     const float u2 = (float)(w1 >> 9) * 1.1920928955078125e-07f;
-    const float rr = sqrtf(-2.0f * logf(u1));
-    float s, c;
-    sincospif(2.0f * u2, &s, &c);
-    z0 = rr * c;
-    z1 = rr * s;
+    const float rr = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln2 log2(u1)
+    z0 = rr * __builtin_amdgcn_cosf(u2);
+    z1 = rr * __builtin_amdgcn_sinf(u2);
 }
 
 __global__ __launch_bounds__(256) void k_noise(uint32_t k0, uint32_t k1, int64_t base_lo,
@@ -43,7 +46,7 @@ __global__ __launch_bounds__(256) void k_noise(uint32_t k0, uint32_t k1, int64_t
     if (g0 >= factor_len) return;
     const int64_t j = base_lo + blockIdx.y;
     u32x4 c{(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)j, kNoiseTag};
-    const u32x4 w = philox4x32_10(c, k0, k1);
+    const u32x4 w = philox4x32_10_dev(c, k0, k1);
     float4 v;
     box_muller(w.x, w.y, v.x, v.y);
     box_muller(w.z, w.w, v.z, v.w);
@@ -60,7 +63,7 @@ __global__ void k_philox_words(uint32_t k0, uint32_t k1, int64_t j, int64_t n_qu
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n_quads) return;
     u32x4 c{(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)j, kNoiseTag};
-    const u32x4 w = philox4x32_10(c, k0, k1);
+    const u32x4 w = philox4x32_10_dev(c, k0, k1);
     out[4 * q + 0] = w.x;
     out[4 * q + 1] = w.y;
     out[4 * q + 2] = w.z;
@@ -88,62 +91,361 @@ __host__ __device__ __forceinline__ void member_to_base(int64_t k, int32_t pop, 
     }
 }
 
+// Matrix owning work chunk `chunk`: the number of matrices whose chunk_off <= chunk, minus one
+// (chunk_off is a prefix sum).  Every lane tests one matrix per step and a ballot counts — the
+// loads are independent (one memory latency for <= 256 matrices) instead of a binary search's
+// log2(n) dependent ones.  Wave-uniform result.
 __device__ __forceinline__ int find_mat(const eggroll_mat_t* __restrict__ mats, int n_mats, int64_t chunk) {
-    int lo = 0, hi = n_mats - 1;
-    while (lo < hi) {  // last i with chunk_off <= chunk
-        const int mid = (lo + hi + 1) >> 1;
-        if (mats[mid].chunk_off <= chunk) lo = mid; else hi = mid - 1;
+    const int lane = threadIdx.x & 63;
+    int cnt = 0;
+    for (int b = 0; b < n_mats; b += 256) {
+        int64_t co[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {  // four independent loads in flight
+            const int i = b + 64 * t + lane;
+            co[t] = i < n_mats ? mats[i].chunk_off : INT64_MAX;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cnt += __popcll(__ballot(co[t] <= chunk));
     }
-    return lo;
+    return __builtin_amdgcn_readfirstlane(cnt - 1);
 }
 
-// eps value of element e of matrix `mt` for base sample factor row `fj`
-__device__ __forceinline__ float eps_value(const eggroll_mat_t& mt, const float* __restrict__ fj, int64_t e,
-                                           int r, float sqrt_r) {
+// ------------------------------------------------------------------------------------
+// Chunk work decomposition shared by perturb and update.  A chunk is EGGROLL_CHUNK = 1024
+// elements of one matrix (host prefix table); each of the 256 threads owns 4 element slots:
+//   VEC   1-D parameter (eps = the factor itself): e = e0 + tid + 256 u
+//   WIDE  rows in {1,2,4} <= cols (PEFT lora_A [r_l, in]): the chunk is 1024/rows whole columns;
+//         slot (u, row) = column c0 + tid + 256 u of every row — b loads coalesced, a[row]
+//         block-uniform (scalar loads), no integer division
+//   TALL  cols in {1,2,4} < rows (lora_B [out, r_l]): the chunk is 1024/cols whole rows;
+//         slot (u, col) = row r0 + tid + 256 u — a loads coalesced, b[col] block-uniform
+//   GEN   anything else: e = e0 + tid + 256 u, row/col by one 32-bit division per slot
+// Every slot's eps is computed with exactly the same fp32 operation order as the reference
+// restatement (a[0] b[0] + a[1] b[1] + ...) / sqrt(r), so the result does not depend on the kind.
+// ------------------------------------------------------------------------------------
+enum ChunkKind { K_VEC = 0, K_WIDE = 1, K_TALL = 2, K_GEN = 3 };
+
+__device__ __forceinline__ int chunk_kind(const eggroll_mat_t& mt) {
+    if (mt.cols == 0) return K_VEC;
+    if (mt.rows <= mt.cols && (mt.rows == 1 || mt.rows == 2 || mt.rows == 4)) return K_WIDE;
+    if (mt.cols < mt.rows && (mt.cols == 1 || mt.cols == 2 || mt.cols == 4)) return K_TALL;
+    return K_GEN;
+}
+
+struct Slots {  // this thread's element slots inside one chunk
+    int row[4], col[4];
+    bool ok[4];
+};
+
+template <int KIND>
+__device__ __forceinline__ Slots make_slots(const eggroll_mat_t& mt, int64_t cidx, int tid) {
+    Slots sl;
+    const int rows = (int)mt.rows, cols = (int)mt.cols;
+    if constexpr (KIND == K_WIDE) {
+        const int cpc = EGGROLL_CHUNK / rows, c0 = (int)cidx * cpc;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int u = s / rows, rr = s % rows;  // rows is 1, 2 or 4: 4 / rows column groups
+            const int c = c0 + tid + 256 * u;
+            sl.row[s] = rr;
+            sl.col[s] = c;
+            sl.ok[s] = (s < 4) && (u < 4 / rows) && (c < c0 + cpc) && (c < cols);
+        }
+    } else if constexpr (KIND == K_TALL) {
+        const int rpc = EGGROLL_CHUNK / cols, r0 = (int)cidx * rpc;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int u = s / cols, cc = s % cols;
+            const int r = r0 + tid + 256 * u;
+            sl.row[s] = r;
+            sl.col[s] = cc;
+            sl.ok[s] = (u < 4 / cols) && (r < r0 + rpc) && (r < rows);
+        }
+    } else {
+        const int numel = KIND == K_VEC ? rows : rows * cols;
+        const int e0 = (int)cidx * EGGROLL_CHUNK;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int e = e0 + s * 256 + tid;
+            sl.ok[s] = e < numel;
+            if (KIND == K_VEC) {
+                sl.row[s] = e;
+                sl.col[s] = 0;
+            } else {
+                const int r = sl.ok[s] ? e / cols : 0;
+                sl.row[s] = r;
+                sl.col[s] = e - r * cols;
+            }
+        }
+    }
+    return sl;
+}
+
+__device__ __forceinline__ int slot_elem(const eggroll_mat_t& mt, const Slots& sl, int s, int kind) {
+    return kind == K_VEC ? sl.row[s] : sl.row[s] * (int)mt.cols + sl.col[s];
+}
+
+// eps of (row, col) of matrix mt for the base-sample factor row fj (utills.py:59-65 restated)
+// R1: egg rank 1 known at compile time — eps = a[row] b[col] (x / sqrt(1) == x exactly), so the
+// loads of consecutive base samples carry no loop-carried control flow and batch up.
+template <int KIND, bool R1>
+__device__ __forceinline__ float eps_rc(const eggroll_mat_t& mt, const float* __restrict__ fj, int row, int col,
+                                        int r, float sqrt_r) {
 #pragma clang fp contract(off)
-    if (mt.cols == 0) return fj[mt.factor_off + e];
-    const int64_t row = e / mt.cols, col = e - row * mt.cols;
-    const float* a = fj + mt.factor_off + row * r;
-    const float* b = fj + mt.factor_off + mt.rows * r + col * r;
-    float acc = a[0] * b[0];
-    for (int q = 1; q < r; ++q) acc = acc + a[q] * b[q];
-    return acc / sqrt_r;
+    if constexpr (KIND == K_VEC) {
+        return fj[mt.factor_off + row];
+    } else if constexpr (R1) {
+        return fj[mt.factor_off + row] * fj[mt.factor_off + mt.rows + col];
+    } else {
+        const float* a = fj + mt.factor_off + (int64_t)row * r;
+        const float* b = fj + mt.factor_off + mt.rows * r + (int64_t)col * r;
+        float acc = a[0] * b[0];
+        for (int q = 1; q < r; ++q) acc = acc + a[q] * b[q];
+        return acc / sqrt_r;
+    }
 }
 
 // ------------------------------------------------------------------------------------
-// perturb / materialise: out[k] = theta + sigma * s_k * E_j(k)
+// Rank-1 fast paths (egg rank 1, the Sana / BASELINE configuration) for VEC / WIDE / TALL chunks.
+// Each element is x_v * w_q: x is the factor along the chunk's long ("vector") dimension (b for
+// WIDE, a for TALL, the 1-D sample for VEC) — coalesced loads, one per slot column — and w the
+// factor along the short ("uniform") dimension (a[row] for WIDE, b[col] for TALL, 1 for VEC),
+// which is the same for the whole block: lane l of every wave holds the uniform factors of base
+// sample / member l and the inner loops broadcast them with v_readlane (an SGPR operand), so the
+// base loop carries no memory dependency except the x loads.
 // ------------------------------------------------------------------------------------
+template <int KIND, int NU>
+struct R1Map {  // slot s = u * NU + q: vector index vi(u), uniform index q
+    static constexpr int NV = 4 / NU;
+    __device__ static int64_t xoff(const eggroll_mat_t& mt) {  // factor offset of the vector dimension
+        return KIND == K_WIDE ? mt.factor_off + mt.rows : mt.factor_off;
+    }
+    __device__ static int64_t woff(const eggroll_mat_t& mt) {  // factor offset of the uniform dimension
+        return KIND == K_WIDE ? mt.factor_off : mt.factor_off + mt.rows;
+    }
+};
+
+template <int KIND, int NU>
+__device__ __forceinline__ void update_chunk_r1(const float* __restrict__ theta, const float* __restrict__ factors,
+                                                int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
+                                                const eggroll_mat_t& mt, int64_t cidx, float lr,
+                                                float* __restrict__ out, double (&part)[4]) {
+#pragma clang fp contract(off)
+    using MP = R1Map<KIND, NU>;
+    constexpr int NV = MP::NV;
+    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
+    const int lane = threadIdx.x & 63;
+    int vi[NV];
+    bool vok[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        vi[u] = KIND == K_TALL ? sl.row[u * NU] : (KIND == K_WIDE ? sl.col[u * NU] : sl.row[u]);
+        vok[u] = sl.ok[u * NU];
+    }
+    const int64_t xo = MP::xoff(mt), wo = MP::woff(mt);
+    uint32_t vbyte[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) vbyte[u] = (uint32_t)vi[u] * 4u;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (nf > 0) {
+        for (int64_t g = 0; g < n_base; g += 64) {
+            // lane l: w_q = c_{g+l} * (uniform factor q of base g+l)
+            float w[NU];
+            const int64_t jl = g + lane;
+#pragma unroll
+            for (int q = 0; q < NU; ++q) {
+                float c = jl < n_base ? s_c[jl] : 0.0f;
+                if (KIND != K_VEC) c = jl < n_base ? c * factors[jl * ld_f + wo + q] : 0.0f;
+                w[q] = c;
+            }
+            const int n = (int)((n_base - g) < 64 ? (n_base - g) : 64);
+            const float* fg = factors + g * ld_f + xo;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)fg, (short)0, 0x7fffffff, 0x00020000);
+            const int ldb = (int)(ld_f * 4);  // host: 64 * ld_f * 4 < 2^31
+            // groups of 8 base samples with a compile-time trip count (readlane is convergent: a
+            // runtime-count loop around it cannot be unrolled), 8 * NV loads in flight per thread
+            for (int j0 = 0; j0 < n; j0 += 8) {
+                float x[8][NV];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    // buffer load: uniform row offset in soffset (SGPR), lane byte offset in voffset —
+                    // one VGPR per slot column instead of a 64-bit address per (base, slot)
+                    const int sb = (j0 + t) * ldb;
+#pragma unroll
+                    for (int u = 0; u < NV; ++u)
+                        x[t][u] = (j0 + t < n && vok[u])
+                                      ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vbyte[u], sb, 0))
+                                      : 0.0f;
+                }
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    if (j0 + t >= n) break;
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const float ws = __builtin_bit_cast(
+                            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w[s % NU]), j0 + t));
+                        acc[s] = acc[s] + ws * x[t][s / NU];
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        if (!sl.ok[s]) continue;
+        const int64_t e = mt.theta_off + slot_elem(mt, sl, s, KIND);
+        const float th = theta[e];
+        float v = th;
+        if (nf > 0) {
+            const float gq = acc[s] / (float)nf;
+            const float t = lr * gq;
+            v = th + t;
+        }
+        out[e] = v;
+        const double d = (double)v - (double)th;
+        part[0] += d * d;
+        part[1] += (double)v * (double)v;
+        part[2] += (double)th * d;
+        part[3] += (double)th * (double)th;
+    }
+}
+
+template <int KIND, int NU>
+__device__ __forceinline__ void perturb_chunk_r1(const float* __restrict__ theta, const float* __restrict__ factors,
+                                                 int64_t ld_f, const eggroll_mat_t& mt, int64_t cidx, int32_t pop,
+                                                 int32_t antithetic, int64_t member_lo, int n_members, float sigma,
+                                                 float* __restrict__ out, int64_t ld_out) {
+#pragma clang fp contract(off)
+    using MP = R1Map<KIND, NU>;
+    constexpr int NV = MP::NV;
+    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
+    const int lane = threadIdx.x & 63;
+    float th[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+        th[s] = (theta && sl.ok[s]) ? theta[mt.theta_off + slot_elem(mt, sl, s, KIND)] : 0.0f;
+    int vi[NV];
+    bool vok[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        vi[u] = KIND == K_TALL ? sl.row[u * NU] : (KIND == K_WIDE ? sl.col[u * NU] : sl.row[u]);
+        vok[u] = sl.ok[u * NU];
+    }
+    const int64_t xo = MP::xoff(mt), wo = MP::woff(mt);
+    for (int g = 0; g < n_members; g += 64) {
+        // lane l: member g+l's base row offset, sign and uniform factors
+        int64_t jb;
+        float sg;
+        member_to_base(member_lo + g + lane, pop, antithetic, jb, sg);
+        const bool mok = g + lane < n_members;
+        float w[NU];
+#pragma unroll
+        for (int q = 0; q < NU; ++q) w[q] = (KIND == K_VEC || !mok) ? 1.0f : factors[jb * ld_f + wo + q];
+        const int n = (n_members - g) < 64 ? (n_members - g) : 64;
+        for (int i = 0; i < n; ++i) {
+            int64_t j;
+            float sgn;
+            member_to_base(member_lo + g + i, pop, antithetic, j, sgn);
+            const float* fj = factors + j * ld_f + xo;
+            float x[NV];
+#pragma unroll
+            for (int u = 0; u < NV; ++u) x[u] = vok[u] ? fj[vi[u]] : 0.0f;
+            float* dst = out + (int64_t)(g + i) * ld_out + mt.theta_off;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (!sl.ok[s]) continue;
+                const float wq = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w[s % NU]), i));
+                // eps = a[row] * b[col] (/ sqrt(1)); the product order a*b is the reference's
+                const float prod = KIND == K_VEC ? x[s / NU] : (KIND == K_WIDE ? wq * x[s / NU] : x[s / NU] * wq);
+                const float eps = sgn * prod;
+                float v;
+                if (theta) {
+                    const float t = sigma * eps;
+                    v = th[s] + t;
+                } else {
+                    v = sigma * eps;
+                }
+                dst[slot_elem(mt, sl, s, KIND)] = v;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// perturb / materialise: out[k] = theta + sigma * s_k * E_j(k) for the members [lo, lo + n).
+// One block per chunk; theta is read once and every member's row written from registers.
+// ------------------------------------------------------------------------------------
+template <int KIND, bool R1>
+__device__ __forceinline__ void perturb_chunk(const float* __restrict__ theta, const float* __restrict__ factors,
+                                              int64_t ld_f, const eggroll_mat_t& mt, int64_t cidx, int r,
+                                              float sqrt_r, int32_t pop, int32_t antithetic, int64_t member_lo,
+                                              int n_members, float sigma, float* __restrict__ out, int64_t ld_out) {
+#pragma clang fp contract(off)
+    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
+    float th[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+        th[s] = (theta && sl.ok[s]) ? theta[mt.theta_off + slot_elem(mt, sl, s, KIND)] : 0.0f;
+#pragma unroll 4
+    for (int i = 0; i < n_members; ++i) {
+        int64_t j;
+        float sgn;
+        member_to_base(member_lo + i, pop, antithetic, j, sgn);
+        const float* fj = factors + j * ld_f;
+        float* dst = out + (int64_t)i * ld_out + mt.theta_off;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (!sl.ok[s]) continue;
+            const float eps = sgn * eps_rc<KIND, R1>(mt, fj, sl.row[s], sl.col[s], r, sqrt_r);
+            float v;
+            if (theta) {
+                const float t = sigma * eps;
+                v = th[s] + t;
+            } else {
+                v = sigma * eps;
+            }
+            dst[slot_elem(mt, sl, s, KIND)] = v;
+        }
+    }
+}
+
+template <bool RANK1>
 __global__ __launch_bounds__(256) void k_perturb(const float* __restrict__ theta, const float* __restrict__ factors,
                                                  int64_t ld_f, const eggroll_mat_t* __restrict__ mats, int n_mats,
                                                  int r, float sqrt_r, int32_t pop, int32_t antithetic,
-                                                 int64_t member_lo, float sigma, float* __restrict__ out,
-                                                 int64_t ld_out) {
-#pragma clang fp contract(off)
+                                                 int64_t member_lo, int n_members, float sigma,
+                                                 float* __restrict__ out, int64_t ld_out) {
     const int64_t chunk = blockIdx.x;
     const int mi = find_mat(mats, n_mats, chunk);
     const eggroll_mat_t mt = mats[mi];
-    const int64_t numel = mt.cols == 0 ? mt.rows : mt.rows * mt.cols;
-    const int64_t e0 = (chunk - mt.chunk_off) * EGGROLL_CHUNK;
-    const int64_t k = member_lo + blockIdx.y;
-    int64_t j;
-    float sgn;
-    member_to_base(k, pop, antithetic, j, sgn);
-    const float* fj = factors + j * ld_f;
-    float* dst = out + (int64_t)blockIdx.y * ld_out + mt.theta_off;
-#pragma unroll
-    for (int u = 0; u < EGGROLL_CHUNK / 256; ++u) {
-        const int64_t e = e0 + u * 256 + threadIdx.x;
-        if (e >= numel) break;
-        const float eps = sgn * eps_value(mt, fj, e, r, sqrt_r);
-        float v;
-        if (theta) {
-            const float t = sigma * eps;
-            v = theta[mt.theta_off + e] + t;
-        } else {
-            v = sigma * eps;
+    const int64_t cidx = chunk - mt.chunk_off;
+#define EGG_PERTURB(KD, R1_)                                                                                  \
+    perturb_chunk<KD, R1_>(theta, factors, ld_f, mt, cidx, r, sqrt_r, pop, antithetic, member_lo, n_members, sigma, \
+                           out, ld_out)
+    const int kind = chunk_kind(mt);
+#define EGG_PERTURB1(KD, NU_) \
+    perturb_chunk_r1<KD, NU_>(theta, factors, ld_f, mt, cidx, pop, antithetic, member_lo, n_members, sigma, out, ld_out)
+    if constexpr (RANK1) {  // host launches this instantiation only for r == 1
+        const int nu = kind == K_WIDE ? (int)mt.rows : (kind == K_TALL ? (int)mt.cols : 1);
+        if (kind == K_VEC) EGG_PERTURB1(K_VEC, 1);
+        else if (kind == K_WIDE && nu == 1) EGG_PERTURB1(K_WIDE, 1);
+        else if (kind == K_WIDE && nu == 2) EGG_PERTURB1(K_WIDE, 2);
+        else if (kind == K_WIDE) EGG_PERTURB1(K_WIDE, 4);
+        else if (kind == K_TALL && nu == 1) EGG_PERTURB1(K_TALL, 1);
+        else if (kind == K_TALL && nu == 2) EGG_PERTURB1(K_TALL, 2);
+        else if (kind == K_TALL) EGG_PERTURB1(K_TALL, 4);
+        else EGG_PERTURB(K_GEN, true);
+    } else {
+        switch (kind) {
+            case K_VEC: EGG_PERTURB(K_VEC, false); break;
+            case K_WIDE: EGG_PERTURB(K_WIDE, false); break;
+            case K_TALL: EGG_PERTURB(K_TALL, false); break;
+            default: EGG_PERTURB(K_GEN, false); break;
         }
-        dst[e] = v;
     }
+#undef EGG_PERTURB
+#undef EGG_PERTURB1
 }
 
 // ------------------------------------------------------------------------------------
@@ -257,6 +559,48 @@ struct UpdScalars {  // tail of the update workspace
     int32_t step_on, theta_on, nf, pad;
 };
 
+template <int KIND, bool R1>
+__device__ __forceinline__ void update_chunk(const float* __restrict__ theta, const float* __restrict__ factors,
+                                             int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
+                                             const eggroll_mat_t& mt, int64_t cidx, int r, float sqrt_r, float lr,
+                                             float* __restrict__ out, double (&part)[4]) {
+#pragma clang fp contract(off)
+    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (nf > 0) {
+        // sum_j c_j eps_j in base order j = 0, 1, ... (the order is the oracle's)
+#pragma unroll 2
+        for (int64_t j = 0; j < n_base; ++j) {
+            const float* fj = factors + j * ld_f;
+            const float cj = s_c[j];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float ev = eps_rc<KIND, R1>(mt, fj, sl.ok[s] ? sl.row[s] : 0, sl.ok[s] ? sl.col[s] : 0, r, sqrt_r);
+                acc[s] = acc[s] + cj * ev;
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        if (!sl.ok[s]) continue;
+        const int64_t e = mt.theta_off + slot_elem(mt, sl, s, KIND);
+        const float th = theta[e];
+        float v = th;
+        if (nf > 0) {
+            const float g = acc[s] / (float)nf;
+            const float t = lr * g;
+            v = th + t;
+        }
+        out[e] = v;
+        const double d = (double)v - (double)th;
+        part[0] += d * d;
+        part[1] += (double)v * (double)v;
+        part[2] += (double)th * d;
+        part[3] += (double)th * (double)th;
+    }
+}
+
+template <bool RANK1>
 __global__ __launch_bounds__(256) void k_update_delta(const float* __restrict__ theta, const float* __restrict__ factors,
                                                       int64_t ld_f, int64_t n_base, const float* __restrict__ fit,
                                                       const float* __restrict__ stats, int32_t pop, int32_t antithetic,
@@ -282,42 +626,39 @@ __global__ __launch_bounds__(256) void k_update_delta(const float* __restrict__ 
     const int64_t chunk = blockIdx.x;
     const int mi = find_mat(mats, n_mats, chunk);
     const eggroll_mat_t mt = mats[mi];
-    const int64_t numel = mt.cols == 0 ? mt.rows : mt.rows * mt.cols;
-    const int64_t e0 = (chunk - mt.chunk_off) * EGGROLL_CHUNK;
-    double pdd = 0.0, poo = 0.0, ptd = 0.0, ptt = 0.0;
-#pragma unroll
-    for (int u = 0; u < EGGROLL_CHUNK / 256; ++u) {
-        const int64_t e = e0 + u * 256 + tid;
-        if (e >= numel) break;
-        const float th = theta[mt.theta_off + e];
-        float v = th;
-        if (nf > 0) {
-            float acc = 0.0f;
-            for (int64_t j = 0; j < n_base; ++j) {
-                const float ev = eps_value(mt, factors + j * ld_f, e, r, sqrt_r);
-                acc = acc + s_c[j] * ev;
-            }
-            const float g = acc / (float)nf;
-            const float t = lr * g;
-            v = th + t;
+    const int64_t cidx = chunk - mt.chunk_off;
+    double part[4] = {0.0, 0.0, 0.0, 0.0};
+#define EGG_UPDATE(KD, R1_) \
+    update_chunk<KD, R1_>(theta, factors, ld_f, n_base, s_c, nf, mt, cidx, r, sqrt_r, lr, out, part)
+    const int kind = chunk_kind(mt);
+#define EGG_UPDATE1(KD, NU_) \
+    update_chunk_r1<KD, NU_>(theta, factors, ld_f, n_base, s_c, nf, mt, cidx, lr, out, part)
+    if constexpr (RANK1) {  // host launches this instantiation only for r == 1
+        const int nu = kind == K_WIDE ? (int)mt.rows : (kind == K_TALL ? (int)mt.cols : 1);
+        if (kind == K_VEC) EGG_UPDATE1(K_VEC, 1);
+        else if (kind == K_WIDE && nu == 1) EGG_UPDATE1(K_WIDE, 1);
+        else if (kind == K_WIDE && nu == 2) EGG_UPDATE1(K_WIDE, 2);
+        else if (kind == K_WIDE) EGG_UPDATE1(K_WIDE, 4);
+        else if (kind == K_TALL && nu == 1) EGG_UPDATE1(K_TALL, 1);
+        else if (kind == K_TALL && nu == 2) EGG_UPDATE1(K_TALL, 2);
+        else if (kind == K_TALL) EGG_UPDATE1(K_TALL, 4);
+        else EGG_UPDATE(K_GEN, true);
+    } else {
+        switch (kind) {
+            case K_VEC: EGG_UPDATE(K_VEC, false); break;
+            case K_WIDE: EGG_UPDATE(K_WIDE, false); break;
+            case K_TALL: EGG_UPDATE(K_TALL, false); break;
+            default: EGG_UPDATE(K_GEN, false); break;
         }
-        out[mt.theta_off + e] = v;
-        const double d = (double)v - (double)th;
-        pdd += d * d;
-        poo += (double)v * (double)v;
-        ptd += (double)th * d;
-        ptt += (double)th * (double)th;
     }
-    pdd = wave_sum_d(pdd);
-    poo = wave_sum_d(poo);
-    ptd = wave_sum_d(ptd);
-    ptt = wave_sum_d(ptt);
+#undef EGG_UPDATE
+#undef EGG_UPDATE1
+#pragma unroll
+    for (int q = 0; q < 4; ++q) part[q] = wave_sum_d(part[q]);
     const int w = tid >> 6, lane = tid & 63;
     if (lane == 0) {
-        s_red[w][0] = pdd;
-        s_red[w][1] = poo;
-        s_red[w][2] = ptd;
-        s_red[w][3] = ptt;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s_red[w][q] = part[q];
     }
     __syncthreads();
     if (tid < 4) {
@@ -424,12 +765,12 @@ int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int6
     const int64_t need_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
     EGG_CHECK_ARG(n_base >= need_base, "perturb: n_base %lld < %lld needed", (long long)n_base, (long long)need_base);
     EGG_CHECK_ARG(member_hi - member_lo <= 65535, "perturb: at most 65535 members per call");
-    EGG_CHECK_ARG(total_chunks >= 1 && total_chunks < (1ll << 31), "perturb: bad total_chunks");
+    EGG_CHECK_ARG(total_chunks >= 1 && total_chunks <= (1ll << 21), "perturb: bad total_chunks (<= 2^21: 32-bit element indices)");
     if (member_hi == member_lo || D == 0) return EGGROLL_OK;
     const float sqrt_r = (float)sqrt((double)rank);
-    dim3 grid((unsigned)total_chunks, (unsigned)(member_hi - member_lo));
-    hipLaunchKernelGGL(k_perturb, grid, dim3(256), 0, as_stream(stream), theta, factors, ld_f, mats, n_mats, rank,
-                       sqrt_r, pop, antithetic, member_lo, sigma, out, ld_out);
+    hipLaunchKernelGGL(rank == 1 ? k_perturb<true> : k_perturb<false>, dim3((unsigned)total_chunks), dim3(256), 0, as_stream(stream), theta, factors, ld_f,
+                       mats, n_mats, rank, sqrt_r, pop, antithetic, member_lo, (int)(member_hi - member_lo), sigma,
+                       out, ld_out);
     EGG_CHECK_LAUNCH("perturb");
     return EGGROLL_OK;
 }
@@ -458,14 +799,15 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
     const int64_t need_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
     EGG_CHECK_ARG(n_base == need_base, "update: n_base %lld != %lld", (long long)n_base, (long long)need_base);
     EGG_CHECK_ARG(n_base <= 16384, "update: n_base > 16384 unsupported");
-    EGG_CHECK_ARG(total_chunks >= 1 && total_chunks < (1ll << 31), "update: bad total_chunks");
+    EGG_CHECK_ARG(total_chunks >= 1 && total_chunks <= (1ll << 21), "update: bad total_chunks (<= 2^21: 32-bit element indices)");
     EGG_CHECK_ARG(((uintptr_t)workspace & 15) == 0, "update: workspace must be 16-byte aligned");
     if (D == 0) return EGGROLL_OK;
     const float sqrt_r = (float)sqrt((double)rank);
     double* partials = reinterpret_cast<double*>(workspace);
     UpdScalars* sc = reinterpret_cast<UpdScalars*>(partials + total_chunks * 4);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_update_delta, dim3((unsigned)total_chunks), dim3(256), (size_t)n_base * sizeof(float), st,
+    const bool r1 = rank == 1 && ld_f * 4 * 64 < (1ll << 31);  // rank-1 path's 32-bit buffer offsets
+    hipLaunchKernelGGL(r1 ? k_update_delta<true> : k_update_delta<false>, dim3((unsigned)total_chunks), dim3(256), (size_t)n_base * sizeof(float), st,
                        theta, factors, ld_f, n_base, fitness, stats, pop, antithetic, mats, n_mats, rank, sqrt_r, lr,
                        theta_out, partials);
     EGG_CHECK_LAUNCH("update_delta");

@@ -1,0 +1,81 @@
+"""Live roofline measurement of the HBM-bound ES kernels (noise, perturb, fitness, update).
+
+Used by bench.py and tools/aux_probe.py.  Each kernel is timed with HIP events recorded on the
+stream it is launched on (torch's current stream — every libeggroll wrapper launches there) and
+priced against its ALGORITHMIC bytes:
+  noise_factors  4 * n_base * factor_len                       (factors written once)
+  perturb        4 * (n_local * D + D + n_used * factor_len)   (theta_pop written, theta + the
+                                                                local members' factor sets read)
+  update         4 * (n_base * factor_len + 2 * D)             (factors + theta read, theta' written)
+The fitness kernel reads a [pop, m] score matrix: latency-bound, reported in microseconds.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from . import kernels as K
+from .kernels import ThetaLayout, n_base_samples
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def _time(fn, it: int = 20) -> float:
+    """Average seconds per call over `it` back-to-back launches (one warm-up call first)."""
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e-3
+
+
+def _entry(sec: float, byt: float) -> Dict[str, float]:
+    gbps = byt / sec / 1e9
+    return {"us": sec * 1e6, "bytes": byt, "GBps": gbps, "frac": gbps / HBM_PEAK_GBPS}
+
+
+def used_bases(pop: int, antithetic: bool, member_lo: int, member_hi: int) -> int:
+    """Distinct base samples the members [lo, hi) read (reference antithetic layout utills.py:88-105)."""
+    h = pop // 2
+    js = set()
+    for k in range(member_lo, member_hi):
+        if not antithetic:
+            js.add(k)
+        else:
+            js.add(k if k < h else (k - h if k < 2 * h else h))
+    return len(js)
+
+
+def aux_kernel_rooflines(layout: ThetaLayout, pop: int, member_lo: int, member_hi: int, device,
+                         sigma: float = 1e-2, lr: float = 1e-3, theta: Optional[torch.Tensor] = None,
+                         antithetic: bool = True, m: int = 4, it: int = 20) -> Dict[str, Dict[str, float]]:
+    device = torch.device(device)
+    nb = n_base_samples(pop, antithetic)
+    nl = member_hi - member_lo
+    D = layout.D
+    if theta is None:
+        theta = torch.randn(D, device=device) * 0.01
+    out: Dict[str, Dict[str, float]] = {}
+    fac = K.noise_factors(0, nb, layout, device)
+    sec = _time(lambda: K.noise_factors(0, nb, layout, device, out=fac), it)
+    out["noise_factors"] = _entry(sec, 4.0 * nb * layout.factor_len)
+    tp = torch.empty((nl, D), dtype=torch.float32, device=device)
+    sec = _time(lambda: K.perturb(theta, fac, layout, pop, antithetic, member_lo, member_hi, sigma, out=tp), it)
+    nu = used_bases(pop, antithetic, member_lo, member_hi)
+    out["perturb"] = _entry(sec, 4.0 * (nl * D + D + nu * layout.factor_len))
+    S = torch.randn(pop, m, device=device) + 21
+    fit = K.fitness(S, True)
+    sec = _time(lambda: K.fitness(S, True), it)
+    out["fitness"] = {"us": sec * 1e6, "note": f"latency-bound single workgroup ({pop}x{m} input)"}
+    ws = K.UpdateWorkspace(layout, device)
+    newt = torch.empty_like(theta)
+    sec = _time(lambda: K.update(theta, fac, fit, layout, pop, antithetic, lr, 0.0, 40.0, out=newt, workspace=ws), it)
+    out["update"] = _entry(sec, 4.0 * (nb * layout.factor_len + 2 * D))
+    out["sizes"] = {"pop": pop, "members": [member_lo, member_hi], "n_base": nb, "D": D,
+                    "factor_len": layout.factor_len}
+    return out

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -268,3 +268,13 @@ def attach_lora(model: nn.Module, r: int, alpha: float, targets: Sequence[str]) 
             n += 1
     bind_theta_layout(model)
     return n
+
+
+def sana_lora_shapes(a: SanaArch = SANA_SPRINT_1_6B, r: int = 2, alpha: float = 8.0,
+                     targets: Sequence[str] = tuple(SANA_LORA_TARGETS)) -> List[Tuple[int, ...]]:
+    """theta layout (trainable shapes in module.parameters() order, utills.py:141-152) of the
+    LoRA'd transformer, built on the meta device: no weights are allocated."""
+    with torch.device("meta"):
+        model = SanaTransformer2DModel(a)
+        attach_lora(model, r, alpha, targets)
+    return [tuple(p.shape) for p in model.parameters() if p.requires_grad]
