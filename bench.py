@@ -179,7 +179,7 @@ def main():
     aux = aux_kernel_rooflines(noiser.layout, pop, engine.lo, engine.hi, device, theta=theta)
 
     value = pop * args.steps / elapsed
-    variants = {k: v for k, v in gemm.items() if k != "all"}
+    variants = {k: v for k, v in gemm.items() if k != "all" and "tflops" in v}
     dom_name = max(variants, key=lambda k: variants[k]["total_ms"]) if variants else "all"
     dom = gemm.get(dom_name, {"launches": 0, "flops": 0.0, "avg_us": float("nan"), "tflops": float("nan")})
     achieved = dom["tflops"]
@@ -191,6 +191,10 @@ def main():
                 "launches": dom["launches"], "avg_launch_us": dom["avg_us"],
                 "flops_per_launch": dom["flops"] / max(dom["launches"], 1),
                 "all_variants": gemm.get("all")}
+    for k, v in gemm.items():  # the projection pre-pass (HBM-bound) joins the aux kernel table
+        if k.startswith("k_lora_project"):
+            aux["lora_project"] = {"us": v["avg_us"], "bytes": v["bytes"] / v["launches"], "GBps": v["GBps"],
+                                   "frac": v["GBps"] / HBM_PEAK_GBPS, "launches": v["launches"]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline

@@ -65,6 +65,83 @@ __global__ __launch_bounds__(256) void k_lora_project(const unsigned short* __re
     }
 }
 
+// Register-resident-A variant (R <= 2, K <= 512 NI): each wave keeps its member's A_k slice
+// (NI x 8 columns x R per lane) in VGPRs and sweeps PR_ROWS rows, two rows' X loads in flight at a
+// time — the per-row A re-reads of k_lora_project (4 float4 A loads per X load) are gone, so the
+// kernel issues almost only the X stream.  Same lane->column map and summation order as
+// k_lora_project: bit-identical T.
+constexpr int PR_ROWS = 8;  // rows per wave
+
+template <int R, int NI>
+__global__ __launch_bounds__(256) void k_lora_project_ra(const unsigned short* __restrict__ X, int64_t ldx,
+                                                         const float* __restrict__ theta_pop, int64_t ld_theta,
+                                                         int64_t offA, int64_t rows_per_member, int64_t M, int64_t K,
+                                                         float* __restrict__ T) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * PR_ROWS;
+    if (row0 >= M) return;
+    const int64_t row_end = row0 + PR_ROWS < M ? row0 + PR_ROWS : M;
+    int64_t cur = -1;
+    float a[NI][R][8];
+    auto load_a = [&](int64_t kl) {
+        const float* A = theta_pop + kl * ld_theta + offA;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int64_t c = lane * 8 + 512 * i;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+                if (c < K) {
+                    a0 = *reinterpret_cast<const float4*>(A + q * K + c);
+                    a1 = *reinterpret_cast<const float4*>(A + q * K + c + 4);
+                }
+                a[i][q][0] = a0.x; a[i][q][1] = a0.y; a[i][q][2] = a0.z; a[i][q][3] = a0.w;
+                a[i][q][4] = a1.x; a[i][q][5] = a1.y; a[i][q][6] = a1.z; a[i][q][7] = a1.w;
+            }
+        }
+    };
+    for (int64_t row = row0; row < row_end; row += 2) {
+        const bool two = row + 1 < row_end;
+        u16x8 xv[2][NI];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int64_t c = lane * 8 + 512 * i;
+                xv[h][i] = (c < K && (h == 0 || two)) ? *reinterpret_cast<const u16x8*>(X + (row + h) * ldx + c)
+                                                      : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h == 1 && !two) break;
+            const int64_t kl = (row + h) / rows_per_member;
+            if (kl != cur) {  // wave-uniform: only at member boundaries
+                load_a(kl);
+                cur = kl;
+            }
+            float acc[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q) acc[q] = 0.0f;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                if (lane * 8 + 512 * i >= K) break;
+                float xf[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) xf[t] = bf16_to_f32(xv[h][i][t]);
+#pragma unroll
+                for (int q = 0; q < R; ++q)
+                    acc[q] += xf[0] * a[i][q][0] + xf[1] * a[i][q][1] + xf[2] * a[i][q][2] + xf[3] * a[i][q][3] +
+                              xf[4] * a[i][q][4] + xf[5] * a[i][q][5] + xf[6] * a[i][q][6] + xf[7] * a[i][q][7];
+            }
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const float v = wave_sum(acc[q]);
+                if (lane == 0) T[(row + h) * R + q] = v;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // Base GEMM + fused LoRA epilogue, templated on the tile:
 //   Tile<BM, BN, WM, WN>: BM x BN output tile, BK = 64, WM x WN waves (wave tile (BM/WM) x (BN/WN)),
@@ -750,9 +827,30 @@ __global__ __launch_bounds__(256) void k_lora_expand(const float* __restrict__ T
     }
 }
 
+template <int R, int NI>
+static void launch_project_ra(const void* X, int64_t ldx, const float* tp, int64_t ldt, int64_t offA, int64_t rpm,
+                              int64_t M, int64_t K, float* T, hipStream_t st) {
+    const int64_t rows_per_block = 4 * PR_ROWS;
+    hipLaunchKernelGGL((k_lora_project_ra<R, NI>), dim3((unsigned)((M + rows_per_block - 1) / rows_per_block)),
+                       dim3(256), 0, st, (const unsigned short*)X, ldx, tp, ldt, offA, rpm, M, K, T);
+}
+
 template <int R>
 static void launch_project(const void* X, int64_t ldx, const float* tp, int64_t ldt, int64_t offA, int64_t rpm,
                            int64_t M, int64_t K, float* T, hipStream_t st) {
+    if constexpr (R <= 2) {  // register-resident A for K <= 4096
+        const int64_t ni = (K + 511) / 512;
+        switch (ni) {
+            case 1: return launch_project_ra<R, 1>(X, ldx, tp, ldt, offA, rpm, M, K, T, st);
+            case 2: return launch_project_ra<R, 2>(X, ldx, tp, ldt, offA, rpm, M, K, T, st);
+            case 3: return launch_project_ra<R, 3>(X, ldx, tp, ldt, offA, rpm, M, K, T, st);
+            case 4: return launch_project_ra<R, 4>(X, ldx, tp, ldt, offA, rpm, M, K, T, st);
+            case 5: return launch_project_ra<R, 5>(X, ldx, tp, ldt, offA, rpm, M, K, T, st);
+            case 6: return launch_project_ra<R, 6>(X, ldx, tp, ldt, offA, rpm, M, K, T, st);
+            case 8: return launch_project_ra<R, 8>(X, ldx, tp, ldt, offA, rpm, M, K, T, st);
+            default: break;
+        }
+    }
     hipLaunchKernelGGL(k_lora_project<R>, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st,
                        (const unsigned short*)X, ldx, tp, ldt, offA, rpm, M, K, T);
 }

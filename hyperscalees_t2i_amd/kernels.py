@@ -172,7 +172,7 @@ def fitness(S: torch.Tensor, promptnorm: bool) -> Dict[str, torch.Tensor]:
 class UpdateWorkspace:
     def __init__(self, layout: ThetaLayout, device):
         nbytes = int(_lib.load().eggroll_update_workspace_bytes(layout.total_chunks))
-        self.buf = torch.empty(-(-nbytes // 16) * 16, dtype=torch.uint8, device=device)
+        self.buf = torch.zeros(-(-nbytes // 16) * 16, dtype=torch.uint8, device=device)  # done counter starts at 0
 
 
 def update(theta: torch.Tensor, factors: torch.Tensor, fit: Dict[str, torch.Tensor], layout: ThetaLayout, pop: int,

@@ -41,8 +41,11 @@ class PopulationContext:
 
 
 class GemmTimer:
-    """Opt-in live timing of every population LoRA GEMM launch with HIP events recorded on the
-    launching stream (bench.py's roofline leg).  Records (start, end, M, N, K, r, rows_per_member)."""
+    """Opt-in live timing of every population LoRA linear with HIP events recorded on the launching
+    stream (bench.py's roofline leg).  While active, each linear runs as its two kernels with an
+    event between them — k_lora_project (T = X A_k^T, HBM-bound) and the GEMM + fused LoRA epilogue
+    (MFMA-bound) — so each kernel's duration is its own (the figure rocprof reports per kernel).
+    Records (e0, e1, e2, M, N, K, r, rows_per_member)."""
 
     active = False
     records: List[tuple] = []
@@ -53,26 +56,32 @@ class GemmTimer:
 
     @classmethod
     def summary(cls) -> Dict[str, Dict[str, float]]:
-        """Per kernel variant (what rocprof names: k_lora_gemm8<r> (8-phase 256x256) or
-        k_lora_gemm<r,Tile<128>>, each after its k_lora_project<r> pre-pass) and "all": calls,
-        total/avg time of the whole LoRA linear (every launch between the two events), algorithmic
-        FLOP = 2MNK (base) + 2MKr (projection) + 2MNr (rank-r expansion)."""
+        """Per GEMM kernel variant (what rocprof names: k_lora_gemm8<r> = the 8-phase 256x256 tile,
+        k_lora_gemm<r,Tile<128>>) and "all": launches, total/avg kernel time, algorithmic FLOP =
+        2MNK (base) + 2MNr (rank-r LoRA expansion in the epilogue).  "k_lora_project<r>": the
+        projection pre-pass, algorithmic bytes = X (2MK) + T (4Mr) + the members' A rows (4 n_k r K)."""
         torch.cuda.synchronize()
         out: Dict[str, Dict[str, float]] = {}
-        for s, e, M, N, Kd, r, rpm in cls.records:
-            ms = s.elapsed_time(e)
-            fl = 2.0 * M * N * Kd + 2.0 * M * Kd * r + 2.0 * M * N * r
+        for e0, e1, e2, M, N, Kd, r, rpm in cls.records:
             t = K.gemm_tile_for(M, N)
-            name = (f"k_lora_gemm8<{r}>+k_lora_project<{r}>" if t == 8 else
-                    f"k_lora_gemm<{r},Tile<{t}>>+k_lora_project<{r}>")
+            name = f"k_lora_gemm8<{r}>" if t == 8 else f"k_lora_gemm<{r},Tile<{t}>>"
+            ms = e1.elapsed_time(e2)
+            fl = 2.0 * M * N * Kd + 2.0 * M * N * r
             for key in (name, "all"):
                 d = out.setdefault(key, {"launches": 0, "total_ms": 0.0, "flops": 0.0})
                 d["launches"] += 1
                 d["total_ms"] += ms
                 d["flops"] += fl
+            d = out.setdefault(f"k_lora_project<{r}>", {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["total_ms"] += e0.elapsed_time(e1)
+            d["bytes"] += 2.0 * M * Kd + 4.0 * M * r + 4.0 * (-(-M // rpm)) * r * Kd
         for d in out.values():
             d["avg_us"] = 1e3 * d["total_ms"] / d["launches"]
-            d["tflops"] = d["flops"] / (d["total_ms"] * 1e9) if d["total_ms"] > 0 else float("nan")
+            if "flops" in d:
+                d["tflops"] = d["flops"] / (d["total_ms"] * 1e9) if d["total_ms"] > 0 else float("nan")
+            else:
+                d["GBps"] = d["bytes"] / (d["total_ms"] * 1e6) if d["total_ms"] > 0 else float("nan")
         return out
 
 
@@ -127,16 +136,19 @@ class LoRALinear(nn.Module):
                 raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")
             rpm = M // ctx.n_members
             ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device)
-            if GemmTimer.active:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-            # projection T = X A_k^T + GEMM + LoRA epilogue (one fused kernel when eligible)
-            y = K.lora_linear_pop(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
-                                  self.r, self.scale, rpm, T_ws=ws)
-            if GemmTimer.active:
-                e1 = torch.cuda.Event(enable_timing=True)
-                e1.record()
-                GemmTimer.records.append((e0, e1, M, self.out_features, self.in_features, self.r, rpm))
+            if GemmTimer.active:  # the same two kernels as lora_linear_pop's unfused path, timed apart
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                T = ws[: M * self.r].view(M, self.r)
+                ev[0].record()
+                K.lora_project(x2, ctx.theta_pop, self.theta_off_A, self.r, rpm, out=T)
+                ev[1].record()
+                y = K.lora_gemm(x2, self.weight, self.bias, T, ctx.theta_pop, self.theta_off_B, self.r, self.scale,
+                                rpm)
+                ev[2].record()
+                GemmTimer.records.append((*ev, M, self.out_features, self.in_features, self.r, rpm))
+            else:  # projection T = X A_k^T + GEMM + LoRA epilogue (one fused kernel when eligible)
+                y = K.lora_linear_pop(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
+                                      self.r, self.scale, rpm, T_ws=ws)
         elif self.r:
             # single member: this module's own (unflattened) lora_A / lora_B
             A = self.lora_A.weight.detach()

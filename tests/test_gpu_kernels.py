@@ -147,6 +147,25 @@ def test_update_matches_reference_formula(dev, pop, anti, rank, caps):
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
 
 
+def test_update_workspace_reuse_and_many_chunks(dev):
+    """Repeated calls on ONE update workspace (different caps, a ~2000-chunk layout) each match the
+    reference formula: no state leaks from one call's partial sums / scalars into the next."""
+    shapes = [(2, 2240), (2240, 2)] * 200 + [(2, 300), (7,)]
+    pop = 8
+    n = EggRollNoiser(shapes, sigma=0.01, lr_scale=0.1, rank=1, use_antithetic=True)
+    fac = n.sample_factors(pop, dev, seed=3)
+    g = torch.Generator().manual_seed(3)
+    theta = (torch.randn(n.num_params, generator=g) * 0.05).to(dev)
+    S = (torch.randn(pop, 4, generator=g) + 20).to(dev)
+    fit = K.fitness(S, True)
+    eps = n.eps_from_factors(fac, pop).cpu().numpy()
+    for caps in [(0.0, 0.0), (1e-4, 0.0), (0.0, 1.0), (0.0, 0.0), (2e-4, 1.0)]:
+        out = n.update_from_factors(theta, fac, fit, pop, max_step_norm=caps[0], theta_max_norm=caps[1])
+        ref, _ = O.ref_es_tail(S.cpu().numpy(), eps, theta.cpu().numpy(), promptnorm=True, lr_scale=0.1, sigma=0.01,
+                               max_step_norm=caps[0], theta_max_norm=caps[1])
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8, err_msg=str(caps))
+
+
 def test_update_nonfinite_members(dev):
     shapes = [(2, 40), (40, 2)]
     pop = 8
