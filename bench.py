@@ -173,8 +173,12 @@ def main():
     marker()  # timed region ends
     gemm = GemmTimer.summary()
     # one extra instrumented epoch for the per-phase breakdown (not part of the timed region)
+    from hyperscalees_t2i_amd.kernels import OpTimer
+    OpTimer.reset(True)
     theta, _ = engine.step(theta, seed=10_000, guidance_scale=guidance, timing=True)
+    OpTimer.active = False
     phases = dict(engine.timings)
+    model_kernels = OpTimer.summary(HBM_PEAK_GBPS)
     from hyperscalees_t2i_amd.measure import aux_kernel_rooflines
     aux = aux_kernel_rooflines(noiser.layout, pop, engine.lo, engine.hi, device, theta=theta)
 
@@ -218,6 +222,7 @@ def main():
             "cpu_baseline": cpu,
             "phases_ms": phases,
             "aux_kernels": aux,
+            "model_kernels": model_kernels,
         }
         print(json.dumps(line), flush=True)
         if args.aux_out:

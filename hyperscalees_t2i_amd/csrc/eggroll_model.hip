@@ -19,95 +19,149 @@ __device__ __forceinline__ unsigned short f2b(float f) {
     __bf16 b = (__bf16)f;
     return *reinterpret_cast<unsigned short*>(&b);
 }
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with the hardware reciprocal (v_rcp_f32, ~1 ulp) instead of an IEEE division
+// (v_div_scale/fmas/fixup): every caller rounds the result to bf16.
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
-// LDS-tiled depthwise conv.  Block = (image b, band of TH output rows, 32 output channels): the
-// (TH+KS-1) x (W+KS-1) x 32-channel input tile (and the matching gate-channel tile for GLU) is
-// staged into LDS once, SiLU applied once per element (bf16, as torch's silu output), then each
-// thread convolves (pixel, 8-channel) outputs from LDS with ds_read_b128.  HBM traffic: input
-// ~(TH+KS-1)/TH reads, output one write.
-constexpr int DW_CS = 32;          // output channels per block
-constexpr int DW_CH = DW_CS / 8;   // 16-B chunks per pixel per plane
-constexpr int DW_LDS = 72 * 1024;  // max LDS per block
+// LDS-tiled depthwise conv, register sliding window.  Block = (image b, band of DW_TH output rows,
+// tile of DW_TW output columns, DW_CS channels per plane).  The (TH+KS-1) x (TW+KS-1) input tile of
+// each plane (the value plane, and for GLU the gate plane) is staged into LDS once with SiLU applied
+// once per element (bf16, as torch's silu output).  Thread = (4-channel group q, column x): it keeps
+// its 4 channels' KS*KS fp32 weights in registers and walks the band's rows; for KS = 3 the 3x3 input
+// window lives in registers too (one new input row per output row: 3 LDS reads instead of 9).  The
+// previous kernel (8-channel threads, weights and every tap re-read from LDS, bf16->fp32 per use)
+// ran the Sana FFN shape at 1.4 TB/s, VALU-bound on conversions.
+// HBM traffic: input ~(TH+KS-1)/TH (halo rows, mostly L2 hits), output one write.
+constexpr int DW_CS = 32;  // channels per plane per block (64 B per pixel: adjacent blocks share lines)
+constexpr int DW_TW = 32;  // output columns per block
+constexpr int DW_TH = 8;   // output rows per block
+
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4m;
 
 template <int KS, bool PRE_SILU, bool GLU>
-__global__ __launch_bounds__(256, 2) void k_dwconv_nhwc(const unsigned short* __restrict__ in,
+__global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __restrict__ in,
                                                      const unsigned short* __restrict__ wt,   // [KS*KS][Cin]
                                                      const unsigned short* __restrict__ bias, // [Cin] or null
-                                                     int H, int W, int Cin, int TH, int bands, int cslices,
+                                                     int H, int W, int Cin, int xtiles, int bands, int cslices,
                                                      unsigned short* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int PLANES = GLU ? 2 : 1;
     constexpr int HALO = KS / 2;
+    constexpr int TR = DW_TH + KS - 1, TC = DW_TW + KS - 1;
+    constexpr int PIXB = DW_CS * 2;  // bytes per staged pixel per plane
+    __shared__ __attribute__((aligned(16))) char lds[PLANES * TR * TC * PIXB];
     const int Cout = GLU ? Cin / 2 : Cin;
     const int tid = threadIdx.x;
     int bid = blockIdx.x;
     const int cs = bid % cslices;
     bid /= cslices;
+    const int xt = bid % xtiles;
+    bid /= xtiles;
     const int band = bid % bands;
     const int b = bid / bands;
-    const int y0 = band * TH;
-    const int c0 = cs * DW_CS;
-    const int TW = W + KS - 1, TR = TH + KS - 1;
-    const int tile_elems = TR * TW * DW_CH;  // 16-B units per plane
+    const int y0 = band * DW_TH, x0 = xt * DW_TW, c0 = cs * DW_CS;
     const unsigned short* img = in + (int64_t)b * H * W * Cin;
-    for (int u = tid; u < tile_elems * PLANES; u += 256) {
-        const int plane = u / tile_elems;
-        const int rem = u - plane * tile_elems;
-        const int ch = rem % DW_CH;
-        const int pix = rem / DW_CH;
-        const int ty = pix / TW, tx = pix - ty * TW;
-        const int gy = y0 + ty - HALO, gx = tx - HALO;
-        u16x8m v = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-            v = *reinterpret_cast<const u16x8m*>(img + ((int64_t)gy * W + gx) * Cin + plane * Cout + c0 + ch * 8);
+    // stage: 16-byte units [plane][ty][tx][4 chunks]; every load of the thread is issued before the
+    // first is consumed (a rolled load -> SiLU -> ds_write loop pays one memory latency per unit)
+    constexpr int UNITS = PLANES * TR * TC * 4;
+    constexpr int PER = (UNITS + 255) / 256;
+    u16x8m v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = tid + k * 256;
+        const int ch = u & 3;
+        int pix = u >> 2;
+        const int pl = pix / (TR * TC);
+        pix -= pl * (TR * TC);
+        const int ty = pix / TC, tx = pix - ty * TC;
+        const int gy = y0 + ty - HALO, gx = x0 + tx - HALO;
+        v[k] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+        if (u < UNITS && gy >= 0 && gy < H && gx >= 0 && gx < W)
+            v[k] = *reinterpret_cast<const u16x8m*>(img + ((int64_t)gy * W + gx) * Cin + pl * Cout + c0 + ch * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = tid + k * 256;
+        if (u < UNITS) {
             if (PRE_SILU) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] = f2b(silu(b2f(v[i])));
+                for (int i = 0; i < 8; ++i) v[k][i] = f2b(silu(b2f(v[k][i])));
             }
+            *reinterpret_cast<u16x8m*>(lds + (size_t)u * 16) = v[k];
         }
-        *reinterpret_cast<u16x8m*>(lds + (size_t)u * 16) = v;
-    }
-    // weights [plane][tap][32 ch] after the input tile (the launcher sizes LDS for both)
-    char* wlds = lds + (size_t)tile_elems * PLANES * 16;
-    for (int u = tid; u < PLANES * KS * KS * DW_CH; u += 256) {
-        const int ch = u % DW_CH, t = (u / DW_CH) % (KS * KS), pl = u / (DW_CH * KS * KS);
-        *reinterpret_cast<u16x8m*>(wlds + (size_t)u * 16) =
-            *reinterpret_cast<const u16x8m*>(wt + t * Cin + pl * Cout + c0 + ch * 8);
     }
     __syncthreads();
-    const int ch = tid % DW_CH;
-    float bsv[PLANES][8];
+    const int q = tid & 7, xs = tid >> 3;  // 4-channel group, column in the tile
+    const int x = x0 + xs;
+    const int cq = c0 + q * 4;
+    auto rd = [&](int pl, int ty, int tx, float (&f)[4]) {
+        const u16x4m v = *reinterpret_cast<const u16x4m*>(lds + ((pl * TR + ty) * TC + tx) * PIXB + q * 8);
 #pragma unroll
-    for (int pl = 0; pl < PLANES; ++pl)
+        for (int i = 0; i < 4; ++i) f[i] = b2f(v[i]);
+    };
+    float res[DW_TH][4];  // value-plane results, gated by the second plane (GLU)
+#pragma unroll 1
+    for (int pl = 0; pl < PLANES; ++pl) {
+        float w[KS * KS][4], bs[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) bsv[pl][i] = bias ? b2f(bias[pl * Cout + c0 + ch * 8 + i]) : 0.0f;
-    const int npix = TH * W;
-    for (int p = tid / DW_CH; p < npix; p += 256 / DW_CH) {
-        const int py = p / W, px = p - py * W;
-        if (y0 + py >= H) break;
-        float acc[PLANES][8];
+        for (int t = 0; t < KS * KS; ++t) {
+            const u16x4m wv = *reinterpret_cast<const u16x4m*>(wt + (int64_t)t * Cin + pl * Cout + cq);
 #pragma unroll
-        for (int pl = 0; pl < PLANES; ++pl)
+            for (int i = 0; i < 4; ++i) w[t][i] = b2f(wv[i]);
+        }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) acc[pl][i] = bsv[pl][i];
+        for (int i = 0; i < 4; ++i) bs[i] = bias ? b2f(bias[pl * Cout + cq + i]) : 0.0f;
+        float win[3][3][4];  // KS == 3 only
+        if constexpr (KS == 3) {
 #pragma unroll
-        for (int dy = 0; dy < KS; ++dy)
+            for (int r = 0; r < 2; ++r)
 #pragma unroll
-            for (int dx = 0; dx < KS; ++dx) {
-                const int lp = (py + dy) * TW + (px + dx);
+                for (int dx = 0; dx < 3; ++dx) rd(pl, r, xs + dx, win[r][dx]);
+        }
 #pragma unroll
-                for (int pl = 0; pl < PLANES; ++pl) {
-                    const u16x8m v = *reinterpret_cast<const u16x8m*>(lds + ((size_t)pl * tile_elems + lp * DW_CH + ch) * 16);
-                    const u16x8m wv = *reinterpret_cast<const u16x8m*>(wlds + ((size_t)(pl * KS * KS + dy * KS + dx) * DW_CH + ch) * 16);
+        for (int oy = 0; oy < DW_TH; ++oy) {
+            if constexpr (KS == 3) {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) acc[pl][i] += b2f(v[i]) * b2f(wv[i]);
+                for (int dx = 0; dx < 3; ++dx) rd(pl, oy + 2, xs + dx, win[2][dx]);
+            }
+            float acc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = bs[i];
+#pragma unroll
+            for (int dy = 0; dy < KS; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < KS; ++dx) {
+                    float tap[4];
+                    if constexpr (KS == 3) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) tap[i] = win[dy][dx][i];
+                    } else {
+                        rd(pl, oy + dy, xs + dx, tap);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[i] += tap[i] * w[dy * KS + dx][i];
+                }
+            if constexpr (KS == 3) {
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        win[0][dx][i] = win[1][dx][i];
+                        win[1][dx][i] = win[2][dx][i];
+                    }
+            }
+            if (pl == 0 && GLU) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) res[oy][i] = acc[i];
+            } else {
+                const int y = y0 + oy;
+                if (y < H && x < W) {
+                    u16x4m o;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[i] = f2b(GLU ? res[oy][i] * silu(acc[i]) : acc[i]);
+                    *reinterpret_cast<u16x4m*>(out + (((int64_t)b * H + y) * W + x) * Cout + cq) = o;
                 }
             }
-        u16x8m o;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = f2b(GLU ? acc[0][i] * silu(acc[PLANES - 1][i]) : acc[0][i]);
-        *reinterpret_cast<u16x8m*>(out + (((int64_t)b * H + y0 + py) * W + px) * Cout + c0 + ch * 8) = o;
+        }
     }
 }
 
@@ -313,71 +367,114 @@ constexpr int LA_D = 32;
 constexpr int LA_PART = LA_D * LA_D + LA_D;   // kv + ksum floats per partial
 constexpr int LA_T = 256;                     // tokens per chunk
 
+// Pass 1 per (image*head, chunk of LA_T tokens): k (ReLU'd) and v staged into LDS as bf16 with all
+// 8 loads per thread in flight; thread (token group g, i-block a, j-block c) accumulates a 4x4 block
+// kv[4a..4a+3][4c..4c+3] (+ ksum[4c..4c+3]) over its group's 64 tokens from two 8-byte LDS reads per
+// token (8 pk-FMA), then the four token groups are summed in a fixed order through LDS.
+constexpr int LA_RS = LA_D + 8;  // bf16 LDS row stride (80 B: 16-B aligned rows)
+
 __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict__ k, const unsigned short* __restrict__ v,
                                                int64_t ld, int64_t hstride, int heads, int N, int nchunk, int relu,
                                                float* __restrict__ part) {
-    __shared__ float sk[LA_T][LA_D + 1];
-    __shared__ float sv[LA_T][LA_D + 1];
+    __shared__ __attribute__((aligned(16))) unsigned short lds_kv[2 * LA_T * LA_RS];  // sk | sv, then red
+    unsigned short* sk = lds_kv;
+    unsigned short* sv = lds_kv + LA_T * LA_RS;
+    float(*red)[LA_PART] = reinterpret_cast<float(*)[LA_PART]>(lds_kv);  // after the token loop
+    static_assert(4 * LA_PART * 4 <= 2 * LA_T * LA_RS * 2, "reduction buffer fits in the staging LDS");
     const int bh = blockIdx.x / nchunk, c = blockIdx.x - bh * nchunk;
     const int b = bh / heads, h = bh - b * heads;
     const int n0 = c * LA_T;
     const int cnt = (N - n0) < LA_T ? (N - n0) : LA_T;
     const int tid = threadIdx.x;
-    // stage LA_T tokens x 32 dims of k and v (16-B loads: 4 per token row per tensor)
-    for (int u = tid; u < LA_T * 4; u += 256) {
-        const int t = u >> 2, q4 = u & 3;
-        float kf[8], vf[8];
+    u16x8m kr[4], vr[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {  // LA_T tokens x 4 16-B chunks per tensor = 4 units per thread
+        const int u = tid + it * 256, t = u >> 2, q4 = u & 3;
+        kr[it] = vr[it] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
         if (t < cnt) {
             const int64_t off = ((int64_t)b * N + n0 + t) * ld + (int64_t)h * hstride + q4 * 8;
-            const u16x8m kv8 = *reinterpret_cast<const u16x8m*>(k + off);
-            const u16x8m vv8 = *reinterpret_cast<const u16x8m*>(v + off);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                float kk = b2f(kv8[i]);
-                kf[i] = relu ? (kk > 0.f ? kk : 0.f) : kk;
-                vf[i] = b2f(vv8[i]);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) kf[i] = vf[i] = 0.f;
+            kr[it] = *reinterpret_cast<const u16x8m*>(k + off);
+            vr[it] = *reinterpret_cast<const u16x8m*>(v + off);
         }
+    }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            sk[t][q4 * 8 + i] = kf[i];
-            sv[t][q4 * 8 + i] = vf[i];
+    for (int it = 0; it < 4; ++it) {
+        const int u = tid + it * 256, t = u >> 2, q4 = u & 3;
+        if (relu) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kr[it][i] = (kr[it][i] & 0x8000) ? (unsigned short)0 : kr[it][i];  // bf16 ReLU (-0 -> +0)
         }
+        *reinterpret_cast<u16x8m*>(sk + t * LA_RS + q4 * 8) = kr[it];
+        *reinterpret_cast<u16x8m*>(sv + t * LA_RS + q4 * 8) = vr[it];
     }
     __syncthreads();
-    // thread -> row i = tid / 8, columns j0 = (tid % 8) * 4 .. +3 of kv; threads < 32 also do ksum
-    const int i = tid >> 3, j0 = (tid & 7) * 4;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, ks = 0.f;
-    for (int t = 0; t < cnt; ++t) {
-        const float vi = sv[t][i];
-        a0 += vi * sk[t][j0];
-        a1 += vi * sk[t][j0 + 1];
-        a2 += vi * sk[t][j0 + 2];
-        a3 += vi * sk[t][j0 + 3];
-        if (tid < LA_D) ks += sk[t][tid];
+    const int g = tid >> 6, l = tid & 63, ia = l >> 3, jc = l & 7;
+    float acc[4][4], ks[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+        ks[x] = 0.f;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = 0.f;
     }
+    const int t_end = cnt < (g + 1) * 64 ? cnt : (g + 1) * 64;
+    for (int t = g * 64; t < t_end; ++t) {
+        const u16x4m vv = *reinterpret_cast<const u16x4m*>(sv + t * LA_RS + ia * 4);
+        const u16x4m kk = *reinterpret_cast<const u16x4m*>(sk + t * LA_RS + jc * 4);
+        float vf[4], kf[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) { vf[x] = b2f(vv[x]); kf[x] = b2f(kk[x]); }
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            ks[x] += kf[x];
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] += vf[x] * kf[y];
+        }
+    }
+    __syncthreads();  // every wave is done reading sk / sv: reuse the staging LDS for the reduction
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) red[g][(ia * 4 + x) * LA_D + jc * 4 + y] = acc[x][y];
+    if (ia == 0) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) red[g][LA_D * LA_D + jc * 4 + y] = ks[y];
+    }
+    __syncthreads();
     float* dst = part + (int64_t)blockIdx.x * LA_PART;
-    dst[i * LA_D + j0] = a0;
-    dst[i * LA_D + j0 + 1] = a1;
-    dst[i * LA_D + j0 + 2] = a2;
-    dst[i * LA_D + j0 + 3] = a3;
-    if (tid < LA_D) dst[LA_D * LA_D + tid] = ks;
+    for (int e = tid; e < LA_PART; e += 256) dst[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+}
+
+// Fixed-order sum of the nchunk partials of one (image, head) -> kvsum[bh], once per head: the
+// k_la_out blocks then read 4 KiB each instead of every block re-summing all nchunk partials
+// (O(nchunk) instead of O(nchunk^2) partial reads: 64 chunks per head at DC-AE's 128x128 stage).
+__global__ __launch_bounds__(256) void k_la_reduce(const float* __restrict__ part, int nchunk,
+                                                   float* __restrict__ kvsum) {
+    const int64_t bh = blockIdx.x;
+    const float* src = part + bh * nchunk * LA_PART;
+    for (int e = threadIdx.x; e < LA_PART; e += 256) {
+        float s = 0.f;
+        for (int cc = 0; cc < nchunk; ++cc) s += src[(int64_t)cc * LA_PART + e];
+        kvsum[bh * LA_PART + e] = s;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict__ q, int64_t ld, int64_t hstride,
-                                                int heads, int N, int nchunk, int relu, const float* __restrict__ part,
+                                                int heads, int N, int nchunk, int relu, const float* __restrict__ kvsum,
                                                 unsigned short* __restrict__ out, int64_t ldo) {
     __shared__ float skv[LA_PART];
     const int bh = blockIdx.x / nchunk, c = blockIdx.x - bh * nchunk;
     const int b = bh / heads, h = bh - b * heads;
     const int tid = threadIdx.x;
-    for (int e = tid; e < LA_PART; e += 256) {
-        float s = 0.f;
-        for (int cc = 0; cc < nchunk; ++cc) s += part[((int64_t)bh * nchunk + cc) * LA_PART + e];
-        skv[e] = s;
+    float kvr[(LA_PART + 255) / 256];  // all loads in flight before the first LDS write
+#pragma unroll
+    for (int it = 0; it < (LA_PART + 255) / 256; ++it) {
+        const int e = tid + it * 256;
+        kvr[it] = e < LA_PART ? kvsum[(int64_t)bh * LA_PART + e] : 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < (LA_PART + 255) / 256; ++it) {
+        const int e = tid + it * 256;
+        if (e < LA_PART) skv[e] = kvr[it];
     }
     __syncthreads();
     const int n = c * LA_T + tid;
@@ -473,26 +570,18 @@ extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* 
     EGG_CHECK_ARG(H * W * C < (1ll << 31), "dwconv: image too large");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(in && w_t && out, "dwconv: NULL pointer");
-    const int planes = glu ? 2 : 1;
-    auto lds_bytes = [&](int64_t th) { return ((th + ks - 1) * (W + ks - 1) + ks * ks) * DW_CH * 16 * planes; };
-    int64_t TH = 256 / W;
-    if (TH < 1) TH = 1;
-    if (TH > H) TH = H;
-    while (TH > 1 && lds_bytes(TH) > DW_LDS) --TH;
-    EGG_CHECK_ARG(lds_bytes(TH) <= DW_LDS, "dwconv: W=%lld too wide for the LDS tile", (long long)W);
-    const int64_t bands = (H + TH - 1) / TH, cslices = cout / DW_CS;
-    const int64_t nblk = B * bands * cslices;
+    const int64_t bands = (H + DW_TH - 1) / DW_TH, xtiles = (W + DW_TW - 1) / DW_TW, cslices = cout / DW_CS;
+    const int64_t nblk = B * bands * xtiles * cslices;
     EGG_CHECK_ARG(nblk < (1ll << 31), "dwconv: grid too large");
     const dim3 grid((unsigned)nblk);
-    const size_t shm = (size_t)lds_bytes(TH);
     hipStream_t st = as_stream(stream);
     auto* i = (const unsigned short*)in;
     auto* w = (const unsigned short*)w_t;
     auto* bb = (const unsigned short*)bias;
     auto* o = (unsigned short*)out;
 #define EGG_DW(KS_, PS_, GL_)                                                                                 \
-    hipLaunchKernelGGL((k_dwconv_nhwc<KS_, PS_, GL_>), grid, dim3(256), shm, st, i, w, bb, (int)H, (int)W, (int)C, \
-                       (int)TH, (int)bands, (int)cslices, o)
+    hipLaunchKernelGGL((k_dwconv_nhwc<KS_, PS_, GL_>), grid, dim3(256), 0, st, i, w, bb, (int)H, (int)W, (int)C,  \
+                       (int)xtiles, (int)bands, (int)cslices, o)
     if (ks == 3 && pre_silu && glu) EGG_DW(3, true, true);
     else if (ks == 3 && !pre_silu && glu) EGG_DW(3, false, true);
     else if (ks == 3 && pre_silu && !glu) EGG_DW(3, true, false);
@@ -541,7 +630,7 @@ extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, void* ou
 
 extern "C" int64_t eggroll_linear_attention_workspace_bytes(int64_t B, int64_t N, int64_t heads) {
     const int64_t nchunk = (N + LA_T - 1) / LA_T;
-    return B * heads * nchunk * LA_PART * (int64_t)sizeof(float);
+    return B * heads * (nchunk + 1) * LA_PART * (int64_t)sizeof(float);  // partials, then per-head sums
 }
 
 extern "C" int eggroll_linear_attention(const void* q, const void* k, const void* v, int64_t ld, int64_t hstride,
@@ -561,8 +650,12 @@ extern "C" int eggroll_linear_attention(const void* q, const void* k, const void
                        (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
                        (float*)workspace);
     EGG_CHECK_LAUNCH("linear_attention_kv");
+    float* kvsum = (float*)workspace + blocks * LA_PART;
+    hipLaunchKernelGGL(k_la_reduce, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const float*)workspace,
+                       (int)nchunk, kvsum);
+    EGG_CHECK_LAUNCH("linear_attention_reduce");
     hipLaunchKernelGGL(k_la_out, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)q, ld, hstride,
-                       (int)heads, (int)N, (int)nchunk, relu_qk, (const float*)workspace, (unsigned short*)out, ldo);
+                       (int)heads, (int)N, (int)nchunk, relu_qk, (const float*)kvsum, (unsigned short*)out, ldo);
     EGG_CHECK_LAUNCH("linear_attention_out");
     return EGGROLL_OK;
 }

@@ -291,6 +291,58 @@ def lora_expand(T: torch.Tensor, theta_pop: torch.Tensor, offB: int, r: int, sca
     return y
 
 
+class OpTimer:
+    """Opt-in live timing of the model-side libeggroll kernels (bench.py's per-kernel HBM table):
+    HIP events on the launching stream around each call + its ALGORITHMIC bytes (every input read
+    once, every output written once)."""
+
+    active = False
+    records: List[tuple] = []
+
+    @classmethod
+    def reset(cls, active: bool):
+        cls.active, cls.records = active, []
+
+    @classmethod
+    def begin(cls):
+        if not cls.active:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    @classmethod
+    def end(cls, e0, name: str, nbytes: float, shape: str = ""):
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        cls.records.append((name, e0, e1, float(nbytes), shape))
+
+    @classmethod
+    def summary(cls, peak_gbps: float = 8000.0) -> Dict[str, Dict[str, float]]:
+        torch.cuda.synchronize()
+        out: Dict[str, Dict[str, float]] = {}
+        for name, e0, e1, nb, shape in cls.records:
+            ms = e0.elapsed_time(e1)
+            for d in (out.setdefault(name, {"launches": 0, "total_ms": 0.0, "bytes": 0.0, "shapes": {}}),):
+                d["launches"] += 1
+                d["total_ms"] += ms
+                d["bytes"] += nb
+                sd = d["shapes"].setdefault(shape, {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
+                sd["launches"] += 1
+                sd["total_ms"] += ms
+                sd["bytes"] += nb
+        for d in out.values():
+            for x in [d] + list(d["shapes"].values()):
+                x["avg_us"] = 1e3 * x["total_ms"] / x["launches"]
+                x["GBps"] = x["bytes"] / (x["total_ms"] * 1e6) if x["total_ms"] > 0 else float("nan")
+                x["frac"] = x["GBps"] / peak_gbps
+            top = sorted(d["shapes"].items(), key=lambda kv: -kv[1]["total_ms"])[:4]
+            d["shapes"] = {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in top}
+        return out
+
+
 # ---------------------------------------------------------------------------------------
 # model-side fused op: channels-last depthwise conv (+SiLU on load, +GLU gate)
 # ---------------------------------------------------------------------------------------
@@ -309,8 +361,10 @@ def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor]
     co = C // 2 if glu else C
     if out is None:
         out = torch.empty((B, H, W, co), dtype=torch.bfloat16, device=x.device)
+    e0 = OpTimer.begin()
     _lib.call("eggroll_dwconv_nhwc", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu), int(glu),
               out.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, f"dwconv_nhwc<{ks},{int(pre_silu)},{int(glu)}>", 2.0 * B * H * W * (C + co), f"{B}x{H}x{W}x{C}")
     return out
 
 
@@ -345,8 +399,10 @@ def rownorm(x: torch.Tensor, eps: float, layer: bool = False, w: Optional[torch.
     ph, st2 = _row_ptr(mshift, "rownorm(mshift)", C)
     if ps is not None and ph is not None and st1 != st2:
         raise ValueError("mscale / mshift must share a row stride")
+    e0 = OpTimer.begin()
     _lib.call("eggroll_rownorm", x.data_ptr(), rows, C, float(eps), int(bool(layer)), _p(w), _p(b), ps, ph,
               st1 or st2 or C, int(rows_per_group), ACT[act], _p(res), out.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, f"rownorm(C={C})", 2.0 * rows * C * (3 if res is not None else 2), f"rows{rows}")
     return out
 
 
@@ -356,8 +412,10 @@ def gated_residual_(x: torch.Tensor, y: torch.Tensor, gate: torch.Tensor, rows_p
     _dev(y, "gated_residual(y)", torch.bfloat16)
     C = x.shape[-1]
     pg, st = _row_ptr(gate, "gated_residual(gate)", C)
+    e0 = OpTimer.begin()
     _lib.call("eggroll_gated_residual", x.data_ptr(), y.data_ptr(), pg, st, x.numel() // C, C, int(rows_per_group),
               _stream(x.device))
+    OpTimer.end(e0, "gated_residual", 6.0 * x.numel())
     return x
 
 
@@ -369,7 +427,9 @@ def upshortcut_add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     Cout = y.shape[-1]
     if y.shape[:3] != (B, 2 * H, 2 * W):
         raise ValueError(f"upshortcut: y {tuple(y.shape)} vs x {tuple(x.shape)}")
+    e0 = OpTimer.begin()
     _lib.call("eggroll_upshortcut_add", y.data_ptr(), x.data_ptr(), B, H, W, Cin, Cout, _stream(x.device))
+    OpTimer.end(e0, "upshortcut_add", 4.0 * y.numel() + 2.0 * x.numel())
     return y
 
 
@@ -383,8 +443,10 @@ def subpixel_shortcut(y4: torch.Tensor, x: torch.Tensor, out: Optional[torch.Ten
     Cout = y4.shape[3] // 4
     if out is None:
         out = torch.empty((B, 2 * H, 2 * W, Cout), dtype=torch.bfloat16, device=x.device)
+    e0 = OpTimer.begin()
     _lib.call("eggroll_subpixel_shortcut", y4.data_ptr(), x.data_ptr(), out.data_ptr(), B, H, W, Cin, Cout,
               _stream(x.device))
+    OpTimer.end(e0, "subpixel_shortcut", 2.0 * (y4.numel() + x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout}")
     return out
 
 
@@ -408,8 +470,10 @@ def linear_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, 
     ws = _LA_WS.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = _LA_WS[key] = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=q.device)
+    e0 = OpTimer.begin()
     _lib.call("eggroll_linear_attention", q.data_ptr(), k.data_ptr(), v.data_ptr(), ld, hstride, B, N, heads,
               int(bool(relu_qk)), out.data_ptr(), out.stride(0), ws.data_ptr(), _stream(q.device))
+    OpTimer.end(e0, "linear_attention", 2.0 * B * N * heads * 32 * 4, f"B{B} N{N} h{heads}")
     return out
 
 
@@ -420,5 +484,7 @@ def bias_act_(y: torch.Tensor, bias: torch.Tensor, act: Optional[str]) -> torch.
     if not y.is_contiguous() or bias.numel() != y.shape[-1]:
         raise ValueError("bias_act: y must be contiguous with bias over its last dim")
     C = y.shape[-1]
+    e0 = OpTimer.begin()
     _lib.call("eggroll_bias_act", y.data_ptr(), bias.data_ptr(), y.numel() // C, C, ACT[act], _stream(y.device))
+    OpTimer.end(e0, "bias_act", 4.0 * y.numel(), f"{tuple(y.shape)}")
     return y
