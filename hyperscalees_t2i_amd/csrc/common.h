@@ -42,6 +42,18 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// ---- XCD-contiguous block order ------------------------------------------------------
+// The dispatcher deals workgroups round-robin over the 8 XCDs (bid % 8 labels the blocks that share
+// an XCD's private L2).  Bijective remap so the blocks sharing an L2 are CONSECUTIVE logical indices:
+// neighbours in the logical order (the two 64-byte halves of a 128-byte line read by adjacent
+// channel slices, adjacent heads of one token row) then share that L2 instead of each half-line
+// being fetched once per XCD (cdna_hip_programming.md "XCD swizzle must be bijective", T1).
+// Placement only changes speed, never results.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+    const int xcd = bid & 7, q = nblk >> 3, rem = nblk & 7;
+    return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+}
+
 // ---- Philox4x32-10 (Salmon et al., SC'11; Random123 constants) ----------------------
 struct u32x4 { uint32_t x, y, z, w; };
 

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
     __shared__ __attribute__((aligned(16))) char lds[PLANES * TR * TC * PIXB];
     const int Cout = GLU ? Cin / 2 : Cin;
     const int tid = threadIdx.x;
-    int bid = blockIdx.x;
+    int bid = xcd_remap(blockIdx.x, gridDim.x);  // adjacent channel slices share 128-B lines: same L2
     const int cs = bid % cslices;
     bid /= cslices;
     const int xt = bid % xtiles;
@@ -355,6 +355,51 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut(const unsigned short*
     *reinterpret_cast<u16x8m*>(out + (int64_t)pix * Cout + c0) = o;
 }
 
+// Same output, one thread per LOW-resolution pixel (b, h, w) and 8 output channels c0..c0+7, all four
+// phases (i, j): the shortcut source channels (4c + 2i + j) / REP of all phases lie in one
+// 32/REP-channel window of x[b, h, w] starting at 4 c0 / REP, loaded as 16-byte vectors and indexed
+// with compile-time positions (the per-output kernel above gathers them as 8 scalar 2-byte loads
+// per output chunk).  REP = 4 Cout / Cin in {1, 2, 4}.
+template <int REP>
+__global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short* __restrict__ y4,
+                                                            const unsigned short* __restrict__ x,
+                                                            unsigned short* __restrict__ out, int H, int W, int Cin,
+                                                            int Cout, int lowpix_total) {
+    constexpr int XW = 32 / REP;  // source window (channels)
+    const int groups = Cout >> 3;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lp = t / groups;
+    if (lp >= lowpix_total) return;
+    const int c0 = (t - lp * groups) << 3;
+    const int HW = H * W;
+    const int bb = lp / HW;
+    const int r = lp - bb * HW;
+    const int h = r / W, w = r - h * W;
+    const unsigned short* src = x + (int64_t)lp * Cin + 4 * c0 / REP;
+    unsigned short xs[XW];
+#pragma unroll
+    for (int v = 0; v < XW / 8; ++v) {
+        const u16x8m q = *reinterpret_cast<const u16x8m*>(src + 8 * v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xs[8 * v + e] = q[e];
+    }
+    u16x8m yv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = k >> 1, j = k & 1;
+        yv[k] = *reinterpret_cast<const u16x8m*>(
+            y4 + ((int64_t)(bb * (H + 1) + h + i) * (W + 1) + (w + j)) * (4 * Cout) + k * Cout + c0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = k >> 1, j = k & 1;
+        u16x8m o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = f2b(b2f(yv[k][q]) + b2f(xs[(4 * q + k) / REP]));
+        *reinterpret_cast<u16x8m*>(out + ((int64_t)(bb * 2 * H + 2 * h + i) * (2 * W) + 2 * w + j) * Cout + c0) = o;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // ReLU linear attention, head dim 32 (SanaLinearAttnProcessor2_0 / DC-AE multiscale attention):
 //   kv[i][j] = sum_n v[n,i] relu(k[n,j]),  ksum[j] = sum_n relu(k[n,j])     (per image, head)
@@ -381,7 +426,8 @@ __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict_
     unsigned short* sv = lds_kv + LA_T * LA_RS;
     float(*red)[LA_PART] = reinterpret_cast<float(*)[LA_PART]>(lds_kv);  // after the token loop
     static_assert(4 * LA_PART * 4 <= 2 * LA_T * LA_RS * 2, "reduction buffer fits in the staging LDS");
-    const int bh = blockIdx.x / nchunk, c = blockIdx.x - bh * nchunk;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);  // adjacent heads share 128-B lines: same L2
+    const int bh = lb / nchunk, c = lb - bh * nchunk;
     const int b = bh / heads, h = bh - b * heads;
     const int n0 = c * LA_T;
     const int cnt = (N - n0) < LA_T ? (N - n0) : LA_T;
@@ -440,7 +486,7 @@ __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict_
         for (int y = 0; y < 4; ++y) red[g][LA_D * LA_D + jc * 4 + y] = ks[y];
     }
     __syncthreads();
-    float* dst = part + (int64_t)blockIdx.x * LA_PART;
+    float* dst = part + (int64_t)lb * LA_PART;  // slot bh * nchunk + c: k_la_reduce sums chunks in order
     for (int e = tid; e < LA_PART; e += 256) dst[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
 }
 
@@ -453,7 +499,15 @@ __global__ __launch_bounds__(256) void k_la_reduce(const float* __restrict__ par
     const float* src = part + bh * nchunk * LA_PART;
     for (int e = threadIdx.x; e < LA_PART; e += 256) {
         float s = 0.f;
-        for (int cc = 0; cc < nchunk; ++cc) s += src[(int64_t)cc * LA_PART + e];
+        int cc = 0;
+        for (; cc + 8 <= nchunk; cc += 8) {  // 8 loads in flight, summed in chunk order
+            float p[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] = src[(int64_t)(cc + u) * LA_PART + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += p[u];
+        }
+        for (; cc < nchunk; ++cc) s += src[(int64_t)cc * LA_PART + e];
         kvsum[bh * LA_PART + e] = s;
     }
 }
@@ -462,7 +516,8 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
                                                 int heads, int N, int nchunk, int relu, const float* __restrict__ kvsum,
                                                 unsigned short* __restrict__ out, int64_t ldo) {
     __shared__ float skv[LA_PART];
-    const int bh = blockIdx.x / nchunk, c = blockIdx.x - bh * nchunk;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = lb / nchunk, c = lb - bh * nchunk;
     const int b = bh / heads, h = bh - b * heads;
     const int tid = threadIdx.x;
     float kvr[(LA_PART + 255) / 256];  // all loads in flight before the first LDS write
@@ -619,11 +674,26 @@ extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, void* ou
                   "subpixel_shortcut: tensor too large");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(y4 && x && out, "subpixel_shortcut: NULL pointer");
+    const int64_t rep = 4 * Cout / Cin;
+    if ((rep == 1 || rep == 2 || rep == 4) && Cin % 8 == 0) {
+        const int64_t lowpix = B * H * W;
+        const int64_t threads = lowpix * (Cout / 8);
+        const dim3 grid((unsigned)((threads + 255) / 256));
+#define EGG_SP4(RP)                                                                                                  \
+    hipLaunchKernelGGL(k_subpixel_shortcut4<RP>, grid, dim3(256), 0, as_stream(stream), (const unsigned short*)y4, \
+                       (const unsigned short*)x, (unsigned short*)out, (int)H, (int)W, (int)Cin, (int)Cout, (int)lowpix)
+        if (rep == 1) EGG_SP4(1);
+        else if (rep == 2) EGG_SP4(2);
+        else EGG_SP4(4);
+#undef EGG_SP4
+        EGG_CHECK_LAUNCH("subpixel_shortcut");
+        return EGGROLL_OK;
+    }
     const int64_t pix = B * 4 * H * W;
     const int64_t threads = pix * (Cout / 8);
     hipLaunchKernelGGL(k_subpixel_shortcut, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, as_stream(stream),
                        (const unsigned short*)y4, (const unsigned short*)x, (unsigned short*)out, (int)H, (int)W,
-                       (int)Cin, (int)Cout, (int)(4 * Cout / Cin), (int)pix);
+                       (int)Cin, (int)Cout, (int)rep, (int)pix);
     EGG_CHECK_LAUNCH("subpixel_shortcut");
     return EGGROLL_OK;
 }

@@ -355,6 +355,27 @@ def test_gated_residual_and_upshortcut(dev):
         assert (ys.float() - ref).abs().max().item() < 0.05
 
 
+@pytest.mark.parametrize("cin,cout", [(128, 32), (64, 32), (32, 32), (48, 24), (24, 48)])
+def test_subpixel_shortcut_bit_exact(dev, cin, cout):
+    """out[b,2h+i,2w+j,c] = bf16(y4[b,h+i,w+j,(2i+j)*Cout+c] + x[b,h,w,(4c+2i+j)/rep]), rep = 4 Cout / Cin
+    (1, 2, 4 take the vectorised per-low-pixel kernel; 8 the per-output one): exact vs a torch
+    restatement of the interleave."""
+    g = torch.Generator().manual_seed(cin + cout)
+    B, H, W = 2, 5, 7
+    x = torch.randn(B, H, W, cin, generator=g).to(torch.bfloat16).to(dev)
+    y4 = torch.randn(B, H + 1, W + 1, 4 * cout, generator=g).to(torch.bfloat16).to(dev)
+    got = K.subpixel_shortcut(y4, x)
+    rep = 4 * cout // cin
+    ref = torch.empty(B, 2 * H, 2 * W, cout, dtype=torch.bfloat16, device=dev)
+    c = torch.arange(cout, device=dev)
+    for i in range(2):
+        for j in range(2):
+            k = 2 * i + j
+            src = x[:, :, :, (4 * c + k) // rep].float()
+            ref[:, i::2, j::2, :] = (y4[:, i:i + H, j:j + W, k * cout:(k + 1) * cout].float() + src).to(torch.bfloat16)
+    assert torch.equal(got, ref)
+
+
 def test_subpixel_upblock_matches_reference(dev):
     """Sub-pixel phase conv + fused interleave/shortcut == nearest-x2 upsample + 3x3 conv + shortcut."""
     from hyperscalees_t2i_amd.dcae import UpBlock
