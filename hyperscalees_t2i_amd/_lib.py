@@ -38,8 +38,9 @@ SIGNATURES = {
     "eggroll_rownorm": (C.c_int, [vp, i64, i64, f32, i32, vp, vp, vp, vp, i64, i64, i32, vp, vp, vp]),
     "eggroll_gated_residual": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, vp]),
     "eggroll_upshortcut_add": (C.c_int, [vp, vp, i64, i64, i64, i64, i64, vp]),
-    "eggroll_subpixel_shortcut": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, vp]),
+    "eggroll_subpixel_shortcut": (C.c_int, [vp, vp, vp, vp, i64, i64, i64, i64, i64, vp]),
     "eggroll_bias_act": (C.c_int, [vp, vp, i64, i64, i32, vp]),
+    "eggroll_dcae_head": (C.c_int, [vp, i64, i64, i64, i64, f32, vp, vp, vp, vp, vp, vp]),
     "eggroll_linear_attention_workspace_bytes": (i64, [i64, i64, i64]),
     "eggroll_linear_attention": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, vp, i64, vp, vp]),
     "eggroll_lora_expand": (C.c_int, [vp, vp, i64, i64, i32, f32, i64, i64, i64, vp, i64, vp]),

@@ -333,6 +333,7 @@ __global__ __launch_bounds__(256) void k_upshortcut_add(unsigned short* __restri
 // conv3x3(upsample_nearest_x2(x)) + pixel_shuffle(repeat_interleave(x)) (DCUpBlock2d).
 __global__ __launch_bounds__(256) void k_subpixel_shortcut(const unsigned short* __restrict__ y4,
                                                            const unsigned short* __restrict__ x,
+                                                           const unsigned short* __restrict__ bias,
                                                            unsigned short* __restrict__ out, int H, int W, int Cin,
                                                            int Cout, int rep, int pix_total) {
     const int groups = Cout >> 3;
@@ -351,7 +352,8 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut(const unsigned short*
         y4 + ((int64_t)(bb * (H + 1) + h + i) * (W + 1) + (w + j)) * (4 * Cout) + k * Cout + c0);
     u16x8m o;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = f2b(b2f(yv[q]) + b2f(src[(4 * (c0 + q) + k) / rep]));
+    for (int q = 0; q < 8; ++q)
+        o[q] = f2b(b2f(yv[q]) + (bias ? b2f(bias[c0 + q]) : 0.f) + b2f(src[(4 * (c0 + q) + k) / rep]));
     *reinterpret_cast<u16x8m*>(out + (int64_t)pix * Cout + c0) = o;
 }
 
@@ -363,6 +365,7 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut(const unsigned short*
 template <int REP>
 __global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short* __restrict__ y4,
                                                             const unsigned short* __restrict__ x,
+                                                            const unsigned short* __restrict__ bias,
                                                             unsigned short* __restrict__ out, int H, int W, int Cin,
                                                             int Cout, int lowpix_total) {
     constexpr int XW = 32 / REP;  // source window (channels)
@@ -383,6 +386,15 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short
 #pragma unroll
         for (int e = 0; e < 8; ++e) xs[8 * v + e] = q[e];
     }
+    float bv[8];
+    if (bias) {
+        const u16x8m q = *reinterpret_cast<const u16x8m*>(bias + c0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = b2f(q[e]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+    }
     u16x8m yv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -395,7 +407,7 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short
         const int i = k >> 1, j = k & 1;
         u16x8m o;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = f2b(b2f(yv[k][q]) + b2f(xs[(4 * q + k) / REP]));
+        for (int q = 0; q < 8; ++q) o[q] = f2b(b2f(yv[k][q]) + bv[q] + b2f(xs[(4 * q + k) / REP]));
         *reinterpret_cast<u16x8m*>(out + ((int64_t)(bb * 2 * H + 2 * h + i) * (2 * W) + 2 * w + j) * Cout + c0) = o;
     }
 }
@@ -564,6 +576,126 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
     }
 }
 
+// ------------------------------------------------------------------------------------
+// DC-AE decoder head, fused: y[p, o] = cb[o] + sum_{tap, c} a[p + tap, c] * Wc[o, tap, c]  (3x3, pad 1)
+// with a = bf16(relu(rms_norm(x) * w + b)) (norm_out + ReLU + conv_out of the reference decoder).
+// The unfused pair was a rownorm pass over x plus MIOpen's 128 -> 3 channel conv, which ran at 16 TF
+// (3.6 ms per 8-image decode, reading 2 GB at 0.6 TB/s).  Block = 8 x 16 output pixels: the
+// 10 x 18-pixel halo tile of x is loaded with every 16-B load in flight, RMS-normalised per pixel
+// (16-lane shuffle reduction over 128 channels), written to LDS as bf16; then 36 MFMA k-steps
+// (9 taps x 4 x 32 channels) of 16 pixels x 16 outputs (3 real) per output row.  HBM: x read once
+// (+halo L2 hits), y written once — the conv is ~free on MFMA.
+// ------------------------------------------------------------------------------------
+constexpr int HD_C = 128;                // input channels (the decoder's widths[0])
+constexpr int HD_TH = 8, HD_TW = 16;     // output tile
+constexpr int HD_TR = HD_TH + 2, HD_TC = HD_TW + 2;
+constexpr int HD_PSTR = HD_C * 2 + 16;   // LDS bytes per staged pixel (+16: spreads b128 banks)
+
+typedef __attribute__((ext_vector_type(8))) __bf16 hd_bf16x8;
+typedef __attribute__((ext_vector_type(4))) float hd_f32x4;
+
+__global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restrict__ x, int H, int W, float eps,
+                                                   const unsigned short* __restrict__ nw,
+                                                   const unsigned short* __restrict__ nb,
+                                                   const unsigned short* __restrict__ wc,   // [3][3][3][C]
+                                                   const unsigned short* __restrict__ cb,   // [3] or null
+                                                   int xtiles, int bands, unsigned short* __restrict__ y) {
+    __shared__ __attribute__((aligned(16))) char tile[HD_TR * HD_TC * HD_PSTR];
+    __shared__ __attribute__((aligned(16))) unsigned short wl[3 * 9 * HD_C];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int bid = blockIdx.x;
+    const int xt = bid % xtiles;
+    bid /= xtiles;
+    const int band = bid % bands;
+    const int b = bid / bands;
+    const int y0 = band * HD_TH, x0 = xt * HD_TW;
+    const unsigned short* img = x + (int64_t)b * H * W * HD_C;
+    // conv weights -> LDS (6.75 KiB)
+    for (int u = tid; u < 3 * 9 * HD_C / 8; u += 256)
+        *reinterpret_cast<u16x8m*>(wl + u * 8) = *reinterpret_cast<const u16x8m*>(wc + u * 8);
+    // stage the halo tile: unit u = (pixel u / 16, 16-B chunk u % 16); a pixel's 16 chunks are 16
+    // consecutive lanes, so its sum of squares is a 16-lane shuffle reduction
+    constexpr int UNITS = HD_TR * HD_TC * 16;
+    constexpr int PER = (UNITS + 255) / 256;
+    u16x8m v[PER];
+    bool inb[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = tid + k * 256;
+        const int pix = u >> 4, ch = u & 15;
+        const int ty = pix / HD_TC, tx = pix - ty * HD_TC;
+        const int gy = y0 + ty - 1, gx = x0 + tx - 1;
+        inb[k] = u < UNITS && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        v[k] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+        if (inb[k]) v[k] = *reinterpret_cast<const u16x8m*>(img + ((int64_t)gy * W + gx) * HD_C + ch * 8);
+    }
+    float wv[8], bv[8];
+    {
+        const int ch = tid & 15;  // every unit of this thread has the same chunk (256 % 16 == 0)
+        const u16x8m qw = *reinterpret_cast<const u16x8m*>(nw + ch * 8);
+        const u16x8m qb = *reinterpret_cast<const u16x8m*>(nb + ch * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { wv[i] = b2f(qw[i]); bv[i] = b2f(qb[i]); }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int u = tid + k * 256;
+        float f[8], ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { f[i] = b2f(v[k][i]); ss += f[i] * f[i]; }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);  // within the pixel's 16 lanes
+        const float rstd = rsqrtf(ss / HD_C + eps);
+        u16x8m o8 = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (inb[k]) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                float t = f[i] * rstd;
+                t *= wv[i];
+                t += bv[i];
+                o8[i] = f2b(t > 0.f ? t : 0.f);
+            }
+        }
+        if (u < UNITS) *reinterpret_cast<u16x8m*>(tile + (u >> 4) * HD_PSTR + (u & 15) * 16) = o8;
+    }
+    __syncthreads();
+    // conv: wave w computes output rows 2w, 2w+1 (one 16-pixel M-tile each)
+    const int n = lane & 15, g = lane >> 4;
+    hd_f32x4 acc[2] = {hd_f32x4{0.f, 0.f, 0.f, 0.f}, hd_f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 4
+    for (int s = 0; s < 36; ++s) {
+        const int tap = s >> 2, cq = s & 3, dy = tap / 3, dx = tap - 3 * (tap / 3);
+        hd_bf16x8 bf;
+        if (n < 3) {
+            bf = *reinterpret_cast<const hd_bf16x8*>(wl + (n * 9 + tap) * HD_C + cq * 32 + g * 8);
+        } else {
+            const u16x8m z = {0, 0, 0, 0, 0, 0, 0, 0};
+            bf = __builtin_bit_cast(hd_bf16x8, z);
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int oy = wave * 2 + r;
+            const hd_bf16x8 af = *reinterpret_cast<const hd_bf16x8*>(
+                tile + ((oy + dy) * HD_TC + n + dx) * HD_PSTR + (cq * 32 + g * 8) * 2);
+            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[r], 0, 0, 0);
+        }
+    }
+    // C[m = pixel 4g + e][col = output channel n]
+    if (n < 3) {
+        const float bias = cb ? b2f(cb[n]) : 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int yy = y0 + wave * 2 + r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int xx = x0 + 4 * g + e;
+                if (yy < H && xx < W) y[(((int64_t)b * H + yy) * W + xx) * 3 + n] = f2b(acc[r][e] + bias);
+            }
+        }
+    }
+}
+
 }  // namespace eggroll
 
 using namespace eggroll;
@@ -666,14 +798,15 @@ extern "C" int eggroll_upshortcut_add(void* y, const void* x, int64_t B, int64_t
     return EGGROLL_OK;
 }
 
-extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, void* out, int64_t B, int64_t H, int64_t W,
-                                         int64_t Cin, int64_t Cout, void* stream) {
+extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, const void* bias, void* out, int64_t B,
+                                         int64_t H, int64_t W, int64_t Cin, int64_t Cout, void* stream) {
     EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && (4 * Cout) % Cin == 0 && Cout % 8 == 0,
                   "subpixel_shortcut: bad sizes");
     EGG_CHECK_ARG(B * 4 * H * W * Cout < (1ll << 31) && B * (H + 1) * (W + 1) * 4 * Cout < (1ll << 31),
                   "subpixel_shortcut: tensor too large");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(y4 && x && out, "subpixel_shortcut: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)bias & 15) == 0, "subpixel_shortcut: bias must be 16-byte aligned");
     const int64_t rep = 4 * Cout / Cin;
     if ((rep == 1 || rep == 2 || rep == 4) && Cin % 8 == 0) {
         const int64_t lowpix = B * H * W;
@@ -681,7 +814,8 @@ extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, void* ou
         const dim3 grid((unsigned)((threads + 255) / 256));
 #define EGG_SP4(RP)                                                                                                  \
     hipLaunchKernelGGL(k_subpixel_shortcut4<RP>, grid, dim3(256), 0, as_stream(stream), (const unsigned short*)y4, \
-                       (const unsigned short*)x, (unsigned short*)out, (int)H, (int)W, (int)Cin, (int)Cout, (int)lowpix)
+                       (const unsigned short*)x, (const unsigned short*)bias, (unsigned short*)out, (int)H, (int)W,  \
+                       (int)Cin, (int)Cout, (int)lowpix)
         if (rep == 1) EGG_SP4(1);
         else if (rep == 2) EGG_SP4(2);
         else EGG_SP4(4);
@@ -692,8 +826,8 @@ extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, void* ou
     const int64_t pix = B * 4 * H * W;
     const int64_t threads = pix * (Cout / 8);
     hipLaunchKernelGGL(k_subpixel_shortcut, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, as_stream(stream),
-                       (const unsigned short*)y4, (const unsigned short*)x, (unsigned short*)out, (int)H, (int)W,
-                       (int)Cin, (int)Cout, (int)rep, (int)pix);
+                       (const unsigned short*)y4, (const unsigned short*)x, (const unsigned short*)bias,
+                       (unsigned short*)out, (int)H, (int)W, (int)Cin, (int)Cout, (int)rep, (int)pix);
     EGG_CHECK_LAUNCH("subpixel_shortcut");
     return EGGROLL_OK;
 }
@@ -739,5 +873,26 @@ extern "C" int eggroll_bias_act(void* y, const void* bias, int64_t rows, int64_t
     hipLaunchKernelGGL(k_bias_act, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
                        (unsigned short*)y, (const unsigned short*)bias, (unsigned)(C / 8), act, (unsigned)total);
     EGG_CHECK_LAUNCH("bias_act");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_dcae_head(const void* x, int64_t B, int64_t H, int64_t W, int64_t C, float eps,
+                                 const void* norm_w, const void* norm_b, const void* conv_w, const void* conv_b,
+                                 void* y, void* stream) {
+    EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0, "dcae_head: bad sizes");
+    EGG_CHECK_ARG(C == HD_C, "dcae_head: C=%lld unsupported (%d)", (long long)C, HD_C);
+    EGG_CHECK_ARG(H * W * C < (1ll << 31), "dcae_head: image too large");
+    if (B == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(x && norm_w && norm_b && conv_w && y, "dcae_head: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)norm_w & 15) == 0 && ((uintptr_t)norm_b & 15) == 0 &&
+                  ((uintptr_t)conv_w & 15) == 0, "dcae_head: pointers must be 16-byte aligned");
+    const int64_t bands = (H + HD_TH - 1) / HD_TH, xtiles = (W + HD_TW - 1) / HD_TW;
+    const int64_t nblk = B * bands * xtiles;
+    EGG_CHECK_ARG(nblk < (1ll << 31), "dcae_head: grid too large");
+    hipLaunchKernelGGL(k_dcae_head, dim3((unsigned)nblk), dim3(256), 0, as_stream(stream), (const unsigned short*)x,
+                       (int)H, (int)W, eps, (const unsigned short*)norm_w, (const unsigned short*)norm_b,
+                       (const unsigned short*)conv_w, (const unsigned short*)conv_b, (int)xtiles, (int)bands,
+                       (unsigned short*)y);
+    EGG_CHECK_LAUNCH("dcae_head");
     return EGGROLL_OK;
 }

@@ -170,14 +170,15 @@ class UpBlock(nn.Module):
     def refresh_phase_weights(self):
         w4 = subpixel_phase_weights(self.conv.weight)
         self.w4 = w4.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        self.b4 = self.conv.bias.repeat(4) if self.conv.bias is not None else None
 
     def forward(self, x):  # NHWC
         if self.w4 is None:
             self.refresh_phase_weights()
         x = x.contiguous()
-        y4 = nhwc(F.conv2d(nchw(x), self.w4, self.b4, padding=1))
-        return K.subpixel_shortcut(y4.contiguous(), x)
+        # bias-free phase conv (MIOpen's bias-fused conv path ran these at 650-850 TF vs ~1 PF without);
+        # the conv bias is added in fp32 by the interleave kernel
+        y4 = nhwc(F.conv2d(nchw(x), self.w4, None, padding=1))
+        return K.subpixel_shortcut(y4.contiguous(), x, bias=self.conv.bias)
 
     def forward_reference(self, x):  # the literal architecture (for tests)
         up = F.interpolate(nchw(x), scale_factor=2, mode="nearest")
@@ -230,5 +231,8 @@ class DCAEDecoder(nn.Module):
         x = self.conv_in(zt) + zt.repeat_interleave(self.in_repeats, dim=-1)
         for st in self.stages:
             x = st(x)
+        if x.shape[-1] == 128 and self.conv_out.weight.shape[0] == 3:  # norm_out + ReLU + conv_out in one pass
+            no = self.norm_out
+            return nchw(K.dcae_head(x, no.eps, no.weight, no.bias, self.conv_out.weight, self.conv_out.bias))
         x = self.norm_out(x, act="relu")
         return nchw(self.conv_out(x))

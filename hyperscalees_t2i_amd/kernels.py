@@ -433,19 +433,25 @@ def upshortcut_add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return y
 
 
-def subpixel_shortcut(y4: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y4 [B,H+1,W+1,4*Cout] (phase conv output), x [B,H,W,Cin] -> out [B,2H,2W,Cout] (NHWC)."""
+def subpixel_shortcut(y4: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                      bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y4 [B,H+1,W+1,4*Cout] (bias-free phase conv output), x [B,H,W,Cin], bias [Cout] or None
+    -> out [B,2H,2W,Cout] (NHWC)."""
     _dev(y4, "subpixel(y4)", torch.bfloat16)
     _dev(x, "subpixel(x)", torch.bfloat16)
     B, H, W, Cin = x.shape
     if y4.shape[:3] != (B, H + 1, W + 1) or y4.shape[3] % 4:
         raise ValueError(f"subpixel: y4 {tuple(y4.shape)} vs x {tuple(x.shape)}")
     Cout = y4.shape[3] // 4
+    if bias is not None:
+        _dev(bias, "subpixel(bias)", torch.bfloat16)
+        if bias.numel() != Cout:
+            raise ValueError(f"subpixel: bias has {bias.numel()} entries, Cout = {Cout}")
     if out is None:
         out = torch.empty((B, 2 * H, 2 * W, Cout), dtype=torch.bfloat16, device=x.device)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_subpixel_shortcut", y4.data_ptr(), x.data_ptr(), out.data_ptr(), B, H, W, Cin, Cout,
-              _stream(x.device))
+    _lib.call("eggroll_subpixel_shortcut", y4.data_ptr(), x.data_ptr(), _p(bias), out.data_ptr(), B, H, W, Cin,
+              Cout, _stream(x.device))
     OpTimer.end(e0, "subpixel_shortcut", 2.0 * (y4.numel() + x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout}")
     return out
 
@@ -475,6 +481,29 @@ def linear_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, 
               int(bool(relu_qk)), out.data_ptr(), out.stride(0), ws.data_ptr(), _stream(q.device))
     OpTimer.end(e0, "linear_attention", 2.0 * B * N * heads * 32 * 4, f"B{B} N{N} h{heads}")
     return out
+
+
+def dcae_head(x: torch.Tensor, eps: float, norm_w: torch.Tensor, norm_b: torch.Tensor, conv_w: torch.Tensor,
+              conv_b: Optional[torch.Tensor]) -> torch.Tensor:
+    """Fused RMSNorm(+w,+b) -> ReLU -> 3x3 conv (C=128 -> 3, pad 1, +bias): x [B,H,W,128] NHWC bf16,
+    conv_w [3,128,3,3] -> y [B,H,W,3] bf16 (NHWC)."""
+    _dev(x, "dcae_head(x)", torch.bfloat16)
+    for t, nm in ((norm_w, "norm_w"), (norm_b, "norm_b")):
+        _dev(t, f"dcae_head({nm})", torch.bfloat16)
+    if conv_b is not None:
+        _dev(conv_b, "dcae_head(conv_b)", torch.bfloat16)
+    x = x.contiguous()
+    B, H, W, C = x.shape
+    if tuple(conv_w.shape) != (3, C, 3, 3):
+        raise ValueError(f"dcae_head: conv_w {tuple(conv_w.shape)} != (3, {C}, 3, 3)")
+    wt = conv_w.permute(0, 2, 3, 1).contiguous()  # [o][ky][kx][c] (a view for channels-last weights)
+    _dev(wt, "dcae_head(conv_w)", torch.bfloat16)
+    y = torch.empty((B, H, W, 3), dtype=torch.bfloat16, device=x.device)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_dcae_head", x.data_ptr(), B, H, W, C, float(eps), norm_w.data_ptr(), norm_b.data_ptr(),
+              wt.data_ptr(), _p(conv_b), y.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, "dcae_head", 2.0 * x.numel() + 2.0 * y.numel(), f"{tuple(x.shape)}")
+    return y
 
 
 def bias_act_(y: torch.Tensor, bias: torch.Tensor, act: Optional[str]) -> torch.Tensor:

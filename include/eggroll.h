@@ -179,11 +179,21 @@ int eggroll_upshortcut_add(void* y, const void* x, int64_t B, int64_t H, int64_t
                            int64_t Cout, void* stream);
 
 /* DC-AE up-block via sub-pixel phases, NHWC: out[b,2h+i,2w+j,c] = y4[b,h+i,w+j,(2i+j)*Cout+c]
- * + x[b,h,w,(4c+2i+j)/(4*Cout/Cin)], where y4 [B,H+1,W+1,4*Cout] = conv2d(x, 2x2 phase kernels,
- * pad 1).  Equals conv3x3(nearest_upsample_x2(x)) + pixel_shuffle(repeat_interleave(x)) at
- * 4/9 of the conv FLOPs and without the upsampled tensor (reference DCUpBlock2d).             */
-int eggroll_subpixel_shortcut(const void* y4, const void* x, void* out, int64_t B, int64_t H,
-                              int64_t W, int64_t Cin, int64_t Cout, void* stream);
+ * (+ bias[c]) + x[b,h,w,(4c+2i+j)/(4*Cout/Cin)], where y4 [B,H+1,W+1,4*Cout] = conv2d(x, 2x2 phase
+ * kernels, pad 1, no bias).  Equals conv3x3(nearest_upsample_x2(x)) + bias +
+ * pixel_shuffle(repeat_interleave(x)) at 4/9 of the conv FLOPs and without the upsampled tensor
+ * (reference DCUpBlock2d).  bias: [Cout] bf16 or NULL (the conv's own bias, added here in fp32 so
+ * the phase conv runs without one).                                                            */
+int eggroll_subpixel_shortcut(const void* y4, const void* x, const void* bias, void* out, int64_t B,
+                              int64_t H, int64_t W, int64_t Cin, int64_t Cout, void* stream);
+
+/* DC-AE decoder head (norm_out + ReLU + conv_out of the reference AutoencoderDC decoder), NHWC:
+ *   a[p, c] = bf16(relu(x[p, c] / sqrt(mean_c x[p, :]^2 + eps) * norm_w[c] + norm_b[c]))
+ *   y[p, o] = bf16(conv_b[o] + sum_{ky,kx,c} a[p + (ky-1, kx-1), c] * conv_w[o, ky, kx, c])  (zero pad)
+ * x [B,H,W,C] bf16 with C = 128; conv_w [3][3][3][C] bf16 (channels-last [Cout, Cin, 3, 3]);
+ * conv_b [3] or NULL; y [B,H,W,3] bf16.                                                        */
+int eggroll_dcae_head(const void* x, int64_t B, int64_t H, int64_t W, int64_t C, float eps, const void* norm_w,
+                      const void* norm_b, const void* conv_w, const void* conv_b, void* y, void* stream);
 
 /* y[row, c] = act(bf16(y[row, c] + bias[c])) in place; y bf16 [rows, C] contiguous, C % 8 == 0,
  * act 0 none / 1 relu / 2 silu.  (Conv bias + activation of the DC-AE ResBlock in one pass.)   */

@@ -356,24 +356,56 @@ def test_gated_residual_and_upshortcut(dev):
 
 
 @pytest.mark.parametrize("cin,cout", [(128, 32), (64, 32), (32, 32), (48, 24), (24, 48)])
-def test_subpixel_shortcut_bit_exact(dev, cin, cout):
-    """out[b,2h+i,2w+j,c] = bf16(y4[b,h+i,w+j,(2i+j)*Cout+c] + x[b,h,w,(4c+2i+j)/rep]), rep = 4 Cout / Cin
-    (1, 2, 4 take the vectorised per-low-pixel kernel; 8 the per-output one): exact vs a torch
-    restatement of the interleave."""
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_subpixel_shortcut_bit_exact(dev, cin, cout, with_bias):
+    """out[b,2h+i,2w+j,c] = bf16((y4[b,h+i,w+j,(2i+j)*Cout+c] + bias[c]) + x[b,h,w,(4c+2i+j)/rep]),
+    rep = 4 Cout / Cin (1, 2, 4 take the vectorised per-low-pixel kernel; 8 the per-output one):
+    exact vs a torch restatement of the interleave."""
     g = torch.Generator().manual_seed(cin + cout)
     B, H, W = 2, 5, 7
     x = torch.randn(B, H, W, cin, generator=g).to(torch.bfloat16).to(dev)
     y4 = torch.randn(B, H + 1, W + 1, 4 * cout, generator=g).to(torch.bfloat16).to(dev)
-    got = K.subpixel_shortcut(y4, x)
+    bias = torch.randn(cout, generator=g).to(torch.bfloat16).to(dev) if with_bias else None
+    got = K.subpixel_shortcut(y4, x, bias=bias)
     rep = 4 * cout // cin
     ref = torch.empty(B, 2 * H, 2 * W, cout, dtype=torch.bfloat16, device=dev)
     c = torch.arange(cout, device=dev)
+    bf = bias.float() if with_bias else torch.zeros(cout, device=dev)
     for i in range(2):
         for j in range(2):
             k = 2 * i + j
             src = x[:, :, :, (4 * c + k) // rep].float()
-            ref[:, i::2, j::2, :] = (y4[:, i:i + H, j:j + W, k * cout:(k + 1) * cout].float() + src).to(torch.bfloat16)
+            yk = y4[:, i:i + H, j:j + W, k * cout:(k + 1) * cout].float() + bf
+            ref[:, i::2, j::2, :] = (yk + src).to(torch.bfloat16)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 37, 21), (1, 64, 64)])
+def test_dcae_head_matches_unfused(dev, B, H, W):
+    """k_dcae_head (RMSNorm*w+b -> ReLU -> 3x3 conv 128->3 +bias, MFMA) vs the unfused rownorm kernel +
+    torch conv2d and vs an fp32 restatement; ragged tiles (37 x 21) exercise the zero halo."""
+    from hyperscalees_t2i_amd.dcae import RMSNormC, nchw, nhwc
+    g = torch.Generator().manual_seed(H * W)
+    x = (torch.randn(B, H, W, 128, generator=g) * 3 + 0.5).to(torch.bfloat16).to(dev)
+    with torch.device(dev):
+        norm = RMSNormC(128)
+    with torch.no_grad():
+        norm.weight.copy_((torch.rand(128, generator=g) + 0.5).to(torch.bfloat16))
+        norm.bias.copy_((torch.randn(128, generator=g) * 0.2).to(torch.bfloat16))
+    w = (torch.randn(3, 128, 3, 3, generator=g) * 0.05).to(torch.bfloat16).to(dev).contiguous(
+        memory_format=torch.channels_last)
+    cb = (torch.randn(3, generator=g) * 0.1).to(torch.bfloat16).to(dev)
+    got = K.dcae_head(x, norm.eps, norm.weight, norm.bias, w, cb).float()
+    a = norm(x, act="relu")                                    # bf16 activations, as the kernel stages them
+    ref = nhwc(torch.nn.functional.conv2d(nchw(a).float(), w.float(), cb.float(), padding=1))
+    err = (got - ref).abs()
+    assert (err <= 1e-2 * ref.abs() + 2e-2).all(), float(err.max())
+    xf = x.float()
+    af = torch.relu(xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + norm.eps) * norm.weight.float()
+                    + norm.bias.float())
+    ref32 = nhwc(torch.nn.functional.conv2d(nchw(af), w.float(), cb.float(), padding=1))
+    rel = ((got - ref32).norm() / ref32.norm()).item()
+    assert rel < 1e-2, rel
 
 
 def test_subpixel_upblock_matches_reference(dev):
