@@ -181,6 +181,11 @@ def main():
     model_kernels = OpTimer.summary(HBM_PEAK_GBPS)
     from hyperscalees_t2i_amd.measure import aux_kernel_rooflines
     aux = aux_kernel_rooflines(noiser.layout, pop, engine.lo, engine.hi, device, theta=theta)
+    # the same kernels at one GPU's share of configs[2] (pop 64 over 8 GPUs: noise and update over
+    # all 32 base samples, perturb of this GPU's 8 members) — the sizes the node-level metric runs
+    aux64 = None
+    if pop != 64 and not args.small:
+        aux64 = aux_kernel_rooflines(noiser.layout, 64, 0, args.pop_per_gpu, device, theta=theta)
 
     value = pop * args.steps / elapsed
     variants = {k: v for k, v in gemm.items() if k != "all" and "tflops" in v}
@@ -222,6 +227,7 @@ def main():
             "cpu_baseline": cpu,
             "phases_ms": phases,
             "aux_kernels": aux,
+            "aux_kernels_pop64_per_gpu": aux64,
             "model_kernels": model_kernels,
         }
         print(json.dumps(line), flush=True)

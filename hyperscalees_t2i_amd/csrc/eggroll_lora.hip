@@ -1164,6 +1164,190 @@ static int launch_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, c
     return EGGROLL_OK;
 }
 
+// ------------------------------------------------------------------------------------
+// Implicit-GEMM 3x3 convolution (stride 1, zero pad 1), NHWC bf16, on the 8-phase 256x256 template.
+// The DC-AE decoder's ResBlock convs (models/SanaSprint.py:157-160 -> diffusers AutoencoderDC):
+//   GEMM rows    = "super-pixels" of PX horizontally adjacent output pixels (M' = B*H*W/PX)
+//   GEMM columns = PX * Cout (the PX pixels' output channels, contiguous in NHWC)
+//   GEMM K       = 3 * (PX+2) taps * Cin: tap (ty, tx) reads input pixel (y+ty-1, x0+tx-1) of the
+//                  super-pixel whose first pixel is x0; K-tile kt = (tap, 64-channel slice)
+// PX = 2 serves Cout = 128 with a full 256-column tile (the packed weight is zero where a tap does
+// not touch a pixel: 25 % of the MACs) — the 256x256 tile would otherwise run half empty.
+// A operand: each lane's DMA rows keep ONE byte offset (its pixel, relative to a per-block buffer
+// base) and a tap-validity bit mask; the tap's shift and channel slice go in the wave-uniform
+// soffset, and a tap outside the image turns the lane's offset out of range (0x80000000 >
+// num_records), which the buffer unit returns as zeros: the zero padding costs one v_cndmask
+// per DMA.  B operand: the packed weight [PX*Cout][3][PX+2][Cin] streams like the GEMM's W.
+// Epilogue: bias through the MFMA addend (one k-step), optional SiLU in fp32, one bf16 rounding.
+// ------------------------------------------------------------------------------------
+struct ConvStage {
+    uint32_t off[2];   // lane byte offset of its pixel's channel chunk, tap (0,0) = pixel - (W+1)
+    uint32_t mask[2];  // bit t set: tap t reads inside the image
+};
+
+template <int PX>
+__device__ __forceinline__ ConvStage make_conv_stage(int m0, int Mp, int H, int W, int Cin, int h, int wave,
+                                                     int lane) {
+    constexpr int TW = PX + 2;
+    const int Ws = W / PX;
+    ConvStage s;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int j = (i * 8 + wave) * 8 + (lane >> 3);  // region row (as make_stage<true>)
+        const int chunk = (lane & 7) ^ (j & 7);
+        const int tr = (j >> 6) * 128 + h * 64 + (j & 63);
+        const int gr = m0 + tr;
+        uint32_t mk = 0;
+        if (gr < Mp) {
+            const int xs = gr % Ws, yrow = gr / Ws, y = yrow % H;
+#pragma unroll
+            for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+                for (int tx = 0; tx < TW; ++tx) {
+                    const int yy = y + ty - 1, xx = xs * PX + tx - 1;
+                    if (yy >= 0 && yy < H && xx >= 0 && xx < W) mk |= 1u << (ty * TW + tx);
+                }
+        }
+        s.mask[i] = mk;
+        s.off[i] = ((uint32_t)(tr * PX) * (uint32_t)Cin + chunk * 8) * 2;  // pixel gr*PX - block base - (W+1)
+    }
+    return s;
+}
+
+__device__ __forceinline__ void issue_conv_half(__amdgpu_buffer_rsrc_t rs, const ConvStage& s, int tap, int kbytes,
+                                                char* region, int wave) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t v = ((s.mask[i] >> tap) & 1u) ? s.off[i] : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(region + (i * 8 + wave) * 1024), 16, v, kbytes, 0, 0);
+    }
+}
+
+// p8_phase with the DMA supplied by the caller (A: masked conv staging, B: weight staging)
+template <int QA, int QB, int RD, bool VM, class Issue>
+__device__ __forceinline__ void p8c_phase(f32x4 (&acc)[8][4], bf16x8 (&a)[4][2], bf16x8 (&b)[2][2], const char* buf,
+                                          const int (&oA)[2], const int (&oB)[2], Issue&& issue) {
+    if (RD != 2) p8_read_b(b, buf + (QB ? p8::RB1 : p8::RB0), oB);
+    if (RD != 1) p8_read_a(a, buf + (QA ? p8::RA1 : p8::RA0), oA);
+    issue();
+    if (VM) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    P8_LGKM0_;
+    P8_BAR();
+    p8_mma<QA, QB, true>(acc, a, b);
+    P8_BAR();
+}
+
+// store_tile_t with an optional fp32 SiLU before the bf16 rounding
+template <int ACT>
+__device__ __forceinline__ void store_tile_t_act(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int m0, int n0,
+                                                 int rbase, int cbase, int M, int N, unsigned short* __restrict__ Y,
+                                                 int64_t ldy) {
+    if constexpr (ACT == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = acc[i][j][e];
+                    acc[i][j][e] = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+                }
+    }
+    store_tile_t(acc, smem, wave, lane, m0, n0, rbase, cbase, M, N, Y, ldy);
+}
+
+template <int PX, int ACT>
+__global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* __restrict__ X,
+                                                          const unsigned short* __restrict__ Wt,
+                                                          const unsigned short* __restrict__ bias, int H, int W,
+                                                          int Cin, int lcpt, int Mp, int N, int tiles_n,
+                                                          unsigned short* __restrict__ Y) {
+    constexpr int TW = PX + 2;
+    __shared__ __attribute__((aligned(16))) char smem[p8::LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+    const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+    const int tiles_m = (Mp + 255) / 256;
+    const int per_group = GROUP_M * tiles_n;
+    const int grp = tile / per_group, first_m = grp * GROUP_M;
+    const int gsize = (tiles_m - first_m) < GROUP_M ? (tiles_m - first_m) : GROUP_M;
+    const int in_grp = tile - grp * per_group;
+    const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int64_t K = (int64_t)3 * TW * Cin;
+    const int nk = (int)(K / BK);
+
+    const ConvStage sA0 = make_conv_stage<PX>(m0, Mp, H, W, Cin, 0, wave, lane);
+    const ConvStage sA1 = make_conv_stage<PX>(m0, Mp, H, W, Cin, 1, wave, lane);
+    const HalfStage sB0 = make_stage<false>(n0, N - 1, K, 0, wave, lane);
+    const HalfStage sB1 = make_stage<false>(n0, N - 1, K, 1, wave, lane);
+    char* const e_buf = smem;
+    char* const o_buf = smem + p8::BUF;
+    // block base = pixel m0*PX - (W+1); tap (ty, tx) adds (ty*W + tx) pixels in soffset: >= 0 always
+    const unsigned short* xb = X + ((int64_t)m0 * PX - W - 1) * Cin;
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a[4][2], b[2][2];
+    int oA[2], oB[2];
+    p8_frag_offsets(oA, wm * 64 + (lane & 15), lane);
+    p8_frag_offsets(oB, wn * 32 + (lane & 15), lane);
+
+    const int cmask = (1 << lcpt) - 1;
+    // K-tile t (clamped to the last one, as the GEMM): tap = t >> lcpt, channel slice t & cmask
+    auto A = [&](const ConvStage& s, int t, char* dst) {
+        t = t < nk ? t : nk - 1;
+        const int tap = t >> lcpt, ty = tap / TW, tx = tap - ty * TW;
+        const int soff = ((ty * W + tx) * Cin + (t & cmask) * BK) * 2;
+        issue_conv_half(rX, s, tap, soff, dst, wave);
+    };
+    auto B = [&](const HalfStage& s, int t, char* dst) {
+        t = t < nk ? t : nk - 1;
+        issue_half(rW, s, t * (BK * 2), dst, wave);
+    };
+    A(sA0, 0, e_buf + p8::RA0);
+    B(sB1, 0, e_buf + p8::RB1);
+    A(sA1, 0, e_buf + p8::RA1);
+    B(sB0, 0, e_buf + p8::RB0);
+    A(sA0, 1, o_buf + p8::RA0);
+    B(sB1, 1, o_buf + p8::RB1);
+    A(sA1, 1, o_buf + p8::RA1);
+    P8_VM6();
+    P8_BAR();
+    if (wm == 1) P8_BAR();
+
+    int t0 = 0;
+    for (; t0 + 1 < nk; t0 += 2) {
+        p8c_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + p8::RB0); });
+        p8c_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + p8::RA0); });
+        p8c_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + p8::RB1); });
+        p8c_phase<1, 0, 1, true>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + p8::RA1); });
+        p8c_phase<0, 0, 0, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB0, t0 + 2, e_buf + p8::RB0); });
+        p8c_phase<0, 1, 1, false>(acc, a, b, o_buf, oA, oB, [&] { A(sA0, t0 + 3, o_buf + p8::RA0); });
+        p8c_phase<1, 1, 2, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB1, t0 + 3, o_buf + p8::RB1); });
+        p8c_phase<1, 0, 1, true>(acc, a, b, o_buf, oA, oB, [&] { A(sA1, t0 + 3, o_buf + p8::RA1); });
+    }
+    if (t0 < nk) {
+        p8c_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + p8::RB0); });
+        p8c_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + p8::RA0); });
+        p8c_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + p8::RB1); });
+        p8c_phase<1, 0, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + p8::RA1); });
+    }
+    if (wm == 0) P8_BAR();
+    P8_VM0();
+    __syncthreads();
+    if (bias)
+        lora_mfma_addend<0>(acc, lane, m0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, Mp, N);
+    store_tile_t_act<ACT>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
+}
+
 }  // namespace eggroll
 
 using namespace eggroll;
@@ -1278,6 +1462,40 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
     }
     return eggroll_lora_gemm(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K,
                              Y, ldy, stream);
+}
+
+/* Implicit-GEMM 3x3 conv (k_conv3x3_gemm8): see include/eggroll.h */
+int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
+                         int64_t Cin, int64_t N, int32_t px, int32_t act, void* y, void* stream) {
+    EGG_CHECK_ARG(px == 1 || px == 2, "conv3x3_nhwc: px must be 1 or 2 (got %d)", px);
+    EGG_CHECK_ARG(act == 0 || act == 2, "conv3x3_nhwc: act must be 0 (none) or 2 (silu) (got %d)", act);
+    EGG_CHECK_ARG(B > 0 && H > 0 && W > 0 && W % px == 0, "conv3x3_nhwc: bad B/H/W (W %% px == 0 required)");
+    EGG_CHECK_ARG(Cin >= 64 && Cin <= 2048 && (Cin & (Cin - 1)) == 0,
+                  "conv3x3_nhwc: Cin=%lld must be a power of two in [64, 2048]", (long long)Cin);
+    EGG_CHECK_ARG(N >= 64 && N % 64 == 0 && N <= 8192, "conv3x3_nhwc: N=%lld must be a multiple of 64 (<= 8192)",
+                  (long long)N);
+    const int64_t Mp = B * H * (W / px);
+    const int64_t K = 3 * (px + 2) * Cin;
+    EGG_CHECK_ARG(Mp < (1ll << 31) && (256 * px + 2 * W + 8) * Cin * 2 < (1ll << 30) && N * K * 2 < (1ll << 31),
+                  "conv3x3_nhwc: sizes exceed the kernel's 32-bit offsets");
+    EGG_CHECK_ARG(x && w_packed && y, "conv3x3_nhwc: NULL pointer");
+    const int64_t tiles_m = (Mp + 255) / 256, tiles_n = (N + 255) / 256;
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "conv3x3_nhwc: grid too large");
+    int lcpt = 0;
+    while ((64ll << lcpt) < Cin) ++lcpt;
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+    hipStream_t st = as_stream(stream);
+#define EGG_CONV(PX_, ACT_)                                                                                    \
+    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, ACT_>), grid, dim3(512), 0, st, (const unsigned short*)x,           \
+                       (const unsigned short*)w_packed, (const unsigned short*)bias, (int)H, (int)W, (int)Cin, lcpt, \
+                       (int)Mp, (int)N, (int)tiles_n, (unsigned short*)y)
+    if (px == 1 && act == 0) EGG_CONV(1, 0);
+    else if (px == 1) EGG_CONV(1, 1);
+    else if (act == 0) EGG_CONV(2, 0);
+    else EGG_CONV(2, 1);
+#undef EGG_CONV
+    EGG_CHECK_LAUNCH("conv3x3_nhwc");
+    return EGGROLL_OK;
 }
 
 }  // extern "C"

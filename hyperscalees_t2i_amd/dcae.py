@@ -9,8 +9,10 @@ pixel-shuffle shortcuts, RMSNorm).  No weights exist offline: parity with diffus
 shapes and FLOPs (~7.5 TFLOP per 1024^2 image) follow the architecture.
 
 Execution (not one of the ES hot-path kernels): activations stay NHWC
-contiguous; dense 3x3 convs go to MIOpen on channels-last views, 1x1 convs to hipBLASLt, and
-depthwise convs (+SiLU / GLU gate) to libeggroll's eggroll_dwconv_nhwc.
+contiguous; the ResBlocks' dense 3x3 convs run as libeggroll's implicit-GEMM MFMA kernel
+(eggroll_conv3x3_nhwc, conv1's bias + SiLU in its epilogue), the remaining dense convs go to MIOpen
+on channels-last views, 1x1 convs to hipBLASLt, and depthwise convs (+SiLU / GLU gate) to
+libeggroll's eggroll_dwconv_nhwc.
 """
 from __future__ import annotations
 
@@ -60,16 +62,43 @@ class Conv3x3(nn.Module):
         return y if y.is_contiguous() else y.contiguous()
 
 
+def conv_gemm_px(c: int) -> int:
+    """Super-pixel width for libeggroll's implicit-GEMM 3x3 conv at c -> c channels (0: not eligible):
+    2 for c = 128 (fills the 256-column tile), 1 for 256..2048, 0 otherwise (MIOpen)."""
+    if c < 128 or c > 2048 or c & (c - 1):
+        return 0
+    return 2 if c == 128 else 1
+
+
 class ResBlock(nn.Module):
+    """conv1 (+bias, SiLU) -> conv2 (no bias) -> RMSNorm + residual.  Both convs run as libeggroll's
+    implicit-GEMM MFMA kernel (bias + SiLU fused into conv1's epilogue) when the width allows,
+    else MIOpen + a bias/SiLU pass."""
+
     def __init__(self, c: int):
         super().__init__()
         self.conv1 = Conv3x3(c, c)
         self.conv2 = Conv3x3(c, c, bias=False)
         self.norm = RMSNormC(c)
+        self.px = conv_gemm_px(c)
+        self.packed = None
+
+    def refresh_packed_weights(self):
+        if self.px:
+            self.packed = (K.pack_conv3x3_weight(self.conv1.weight, self.px),
+                           self.conv1.bias.repeat(self.px).contiguous(),
+                           K.pack_conv3x3_weight(self.conv2.weight, self.px))
 
     def forward(self, x):
+        x = x.contiguous()
+        if self.px and x.shape[2] % self.px == 0:
+            if self.packed is None:
+                self.refresh_packed_weights()
+            w1, b1, w2 = self.packed
+            h = K.conv3x3_nhwc(x, w1, b1, self.px, "silu")
+            return self.norm(K.conv3x3_nhwc(h, w2, None, self.px), res=x)
         c1 = self.conv1
-        h = nhwc(F.conv2d(nchw(x.contiguous()), c1.weight, None, padding=1)).contiguous()
+        h = nhwc(F.conv2d(nchw(x), c1.weight, None, padding=1)).contiguous()
         h = K.bias_act_(h, c1.bias, "silu")                       # bias + SiLU in one pass
         return self.norm(self.conv2(h), res=x)
 
@@ -225,6 +254,8 @@ class DCAEDecoder(nn.Module):
         for m in self.modules():
             if isinstance(m, UpBlock):
                 m.refresh_phase_weights()
+            if isinstance(m, ResBlock):
+                m.refresh_packed_weights()
 
     def forward(self, z):  # z [B, 32, h, w] -> image [B, 3, 32h, 32w] (channels-last) in ~[-1, 1]
         zt = nhwc(z.to(torch.bfloat16)).contiguous()

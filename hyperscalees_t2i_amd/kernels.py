@@ -312,32 +312,39 @@ class OpTimer:
         return e
 
     @classmethod
-    def end(cls, e0, name: str, nbytes: float, shape: str = ""):
+    def end(cls, e0, name: str, nbytes: float, shape: str = "", flops: float = 0.0):
         if e0 is None:
             return
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        cls.records.append((name, e0, e1, float(nbytes), shape))
+        cls.records.append((name, e0, e1, float(nbytes), shape, float(flops)))
 
     @classmethod
     def summary(cls, peak_gbps: float = 8000.0) -> Dict[str, Dict[str, float]]:
         torch.cuda.synchronize()
         out: Dict[str, Dict[str, float]] = {}
-        for name, e0, e1, nb, shape in cls.records:
+        for name, e0, e1, nb, shape, fl in cls.records:
             ms = e0.elapsed_time(e1)
-            for d in (out.setdefault(name, {"launches": 0, "total_ms": 0.0, "bytes": 0.0, "shapes": {}}),):
+            for d in (out.setdefault(name, {"launches": 0, "total_ms": 0.0, "bytes": 0.0, "flops": 0.0, "shapes": {}}),):
                 d["launches"] += 1
                 d["total_ms"] += ms
                 d["bytes"] += nb
-                sd = d["shapes"].setdefault(shape, {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
+                d["flops"] += fl
+                sd = d["shapes"].setdefault(shape, {"launches": 0, "total_ms": 0.0, "bytes": 0.0, "flops": 0.0})
                 sd["launches"] += 1
                 sd["total_ms"] += ms
                 sd["bytes"] += nb
+                sd["flops"] += fl
         for d in out.values():
             for x in [d] + list(d["shapes"].values()):
                 x["avg_us"] = 1e3 * x["total_ms"] / x["launches"]
                 x["GBps"] = x["bytes"] / (x["total_ms"] * 1e6) if x["total_ms"] > 0 else float("nan")
                 x["frac"] = x["GBps"] / peak_gbps
+                if x["flops"] > 0:  # MFMA-bound ops: useful FLOP rate against the dense bf16 peak
+                    x["tflops"] = x["flops"] / (x["total_ms"] * 1e9)
+                    x["mfma_frac"] = x["tflops"] / 2500.0
+                else:
+                    x.pop("flops")
             top = sorted(d["shapes"].items(), key=lambda kv: -kv[1]["total_ms"])[:4]
             d["shapes"] = {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in top}
         return out
@@ -504,6 +511,44 @@ def dcae_head(x: torch.Tensor, eps: float, norm_w: torch.Tensor, norm_b: torch.T
               wt.data_ptr(), _p(conv_b), y.data_ptr(), _stream(x.device))
     OpTimer.end(e0, "dcae_head", 2.0 * x.numel() + 2.0 * y.numel(), f"{tuple(x.shape)}")
     return y
+
+
+def pack_conv3x3_weight(w: torch.Tensor, px: int) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] conv weight -> the implicit-GEMM operand [px*Cout, 3*(px+2)*Cin] bf16 of
+    eggroll_conv3x3_nhwc: row p*Cout + o, column (ky*(px+2) + tx)*Cin + c holds w[o, c, ky, tx - p]
+    (zero where tx - p is outside 0..2).  px = 1 is the channels-last weight itself."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    wt = w.permute(0, 2, 3, 1).to(torch.bfloat16)  # [o][ky][kx][c]
+    out = torch.zeros((px, Cout, 3, px + 2, Cin), dtype=torch.bfloat16, device=w.device)
+    for p in range(px):
+        out[p, :, :, p:p + 3, :] = wt
+    return out.reshape(px * Cout, 3 * (px + 2) * Cin).contiguous()
+
+
+def conv3x3_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], px: int,
+                 act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """3x3 conv (stride 1, pad 1) of x [B,H,W,Cin] NHWC bf16 with a pack_conv3x3_weight operand;
+    bias [px*Cout] (the conv bias repeated px times) or None; act None / 'silu'.  -> [B,H,W,Cout]."""
+    _dev(x, "conv3x3(x)", torch.bfloat16)
+    _dev(w_packed, "conv3x3(w)", torch.bfloat16)
+    x = x.contiguous()
+    B, H, W, Cin = x.shape
+    N = w_packed.shape[0]
+    if w_packed.shape[1] != 3 * (px + 2) * Cin or N % px:
+        raise ValueError(f"conv3x3: packed weight {tuple(w_packed.shape)} does not match Cin={Cin}, px={px}")
+    if bias is not None:
+        _dev(bias, "conv3x3(bias)", torch.bfloat16)
+        if bias.numel() != N:
+            raise ValueError(f"conv3x3: bias has {bias.numel()} entries, need {N}")
+    Cout = N // px
+    if out is None:
+        out = torch.empty((B, H, W, Cout), dtype=torch.bfloat16, device=x.device)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_conv3x3_nhwc", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, px,
+              ACT[act], out.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, "conv3x3", 2.0 * (x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout} px{px}",
+                flops=2.0 * B * H * W * Cout * 9 * Cin)
+    return out
 
 
 def bias_act_(y: torch.Tensor, bias: torch.Tensor, act: Optional[str]) -> torch.Tensor:

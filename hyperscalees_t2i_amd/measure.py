@@ -22,10 +22,15 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def _time(fn, it: int = 20) -> float:
-    """Average seconds per call over `it` back-to-back launches (one warm-up call first)."""
+    """Average seconds per call over `it` back-to-back launches (one warm-up call first).
+
+    The launches are queued behind a ~2 ms spin kernel, so the GPU runs them back to back: the
+    average is the kernels' own duration (plus the dispatch gap), which is what rocprof reports —
+    not the host's ctypes/Python launch rate, which exceeds a 5-20 us kernel."""
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(5_000_000)
     s.record()
     for _ in range(it):
         fn()

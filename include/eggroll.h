@@ -199,6 +199,17 @@ int eggroll_dcae_head(const void* x, int64_t B, int64_t H, int64_t W, int64_t C,
  * act 0 none / 1 relu / 2 silu.  (Conv bias + activation of the DC-AE ResBlock in one pass.)   */
 int eggroll_bias_act(void* y, const void* bias, int64_t rows, int64_t C, int32_t act, void* stream);
 
+/* Dense 3x3 conv, stride 1, zero pad 1, NHWC bf16, as an implicit GEMM on MFMA (DC-AE ResBlock
+ * conv1/conv2 of the reference's AutoencoderDC decoder, models/SanaSprint.py:157-160):
+ *   y[b, h, x, o] = act(bias[o] + sum_{ky,kx,c} x[b, h+ky-1, x+kx-1, c] * w[o, c, ky, kx])
+ * computed on super-pixels of px (1 or 2) horizontally adjacent pixels: w_packed is
+ * [N = px*Cout][3][px+2][Cin] bf16 with w_packed[p*Cout + o][ky][tx][c] = w[o, c, ky, tx - p]
+ * (zero where tx - p is outside 0..2); bias [N] bf16 (the conv bias repeated px times) or NULL;
+ * act 0 none / 2 silu (fp32, before the single bf16 rounding).  Cin a power of two in [64, 2048],
+ * N % 64 == 0, W % px == 0.  x [B,H,W,Cin]; y [B,H,W,Cout] contiguous.                          */
+int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
+                         int64_t W, int64_t Cin, int64_t N, int32_t px, int32_t act, void* y, void* stream);
+
 /* ReLU linear attention with head dim 32 (diffusers SanaLinearAttnProcessor2_0 and DC-AE
  * SanaMultiscaleLinearAttention): for every image b and head h over its N tokens,
  *   out[n, h*32+i] = sum_j q'[n,j] kv[i][j] / (sum_j q'[n,j] ksum[j] + 1e-15),

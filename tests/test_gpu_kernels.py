@@ -471,13 +471,54 @@ def test_bias_act_and_resblock(dev):
         ref = fn(y + b).float()
         got = K.bias_act_(y.clone(), b, act).float()
         assert (got - ref).abs().max().item() <= 0.02 * max(1.0, ref.abs().max().item())
-    from hyperscalees_t2i_amd.dcae import ResBlock
+
+
+@pytest.mark.parametrize("c", [64, 128, 256])
+def test_resblock_matches_reference(dev, c):
+    """ResBlock.forward (c = 64: MIOpen + bias/SiLU pass; 128: implicit-GEMM conv with 2-pixel
+    super-pixels; 256: 1-pixel) vs the literal conv -> SiLU -> conv -> RMSNorm + residual."""
+    from hyperscalees_t2i_amd.dcae import ResBlock, conv_gemm_px
     torch.manual_seed(1)
     with torch.device(dev):
-        rb = ResBlock(64)
+        rb = ResBlock(c)
+    assert rb.px == conv_gemm_px(c)
     with torch.no_grad():
         for p in rb.parameters():
-            p.copy_(torch.randn_like(p, dtype=torch.float32) * 0.05)
-    x = torch.randn(2, 9, 6, 64, device=dev).to(torch.bfloat16)
+            p.copy_(torch.randn_like(p, dtype=torch.float32) * (0.05 if p.ndim < 2 else 1.0 / math.sqrt(9 * c)))
+    x = torch.randn(2, 9, 6, c, device=dev).to(torch.bfloat16)
     got, ref = rb(x).float(), rb.forward_reference(x).float()
     assert ((got - ref).norm() / ref.norm()).item() < 1e-2
+
+
+# ---------------------------------------------------------------------------------- implicit-GEMM 3x3 conv
+@pytest.mark.parametrize("B,H,W,Cin,Cout,px,bias,act", [
+    (2, 16, 16, 64, 64, 1, True, None),
+    (2, 16, 32, 128, 128, 2, True, "silu"),
+    (1, 7, 10, 128, 128, 2, False, None),     # odd H, tail super-pixel rows (M' % 256 != 0)
+    (1, 24, 40, 256, 256, 1, True, "silu"),
+    (1, 9, 12, 512, 512, 1, False, None),     # N = 512: two column tiles
+    (3, 5, 6, 64, 256, 1, True, None),        # Cin != Cout, tiny image (every pixel is a border pixel)
+])
+def test_conv3x3_nhwc_vs_torch(dev, B, H, W, Cin, Cout, px, bias, act):
+    """eggroll_conv3x3_nhwc vs a torch fp32 conv2d (+bias, +SiLU) on the same bf16 inputs; the kernel
+    rounds once to bf16 at the end: |d| <= 2^-8 |y| + 1e-3 max|y|."""
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + px)
+    x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)
+    b = (torch.randn(Cout, generator=g) * 0.5).to(dev, torch.bfloat16) if bias else None
+    wp = K.pack_conv3x3_weight(w, px)
+    y = K.conv3x3_nhwc(x, wp, b.repeat(px) if bias else None, px, act)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), b.float() if bias else None, padding=1)
+    if act == "silu":
+        ref = torch.nn.functional.silu(ref)
+    ref = ref.permute(0, 2, 3, 1)
+    err = (y.float() - ref).abs()
+    tol = 2.0 ** -8 * ref.abs() + 1e-3 * ref.abs().max()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.3e} (ref max {ref.abs().max().item():.3e})"
+
+
+def test_conv3x3_nhwc_rejects_bad_shapes(dev):
+    x = torch.zeros(1, 8, 8, 96, device=dev, dtype=torch.bfloat16)   # Cin not a power of two
+    w = K.pack_conv3x3_weight(torch.zeros(64, 96, 3, 3, device=dev, dtype=torch.bfloat16), 1)
+    with pytest.raises(RuntimeError):
+        K.conv3x3_nhwc(x, w, None, 1)
