@@ -1185,11 +1185,17 @@ struct ConvStage {
     uint32_t mask[2];  // bit t set: tap t reads inside the image
 };
 
-template <int PX>
+template <int PX, int KS>
 __device__ __forceinline__ ConvStage make_conv_stage(int m0, int Mp, int H, int W, int Cin, int h, int wave,
                                                      int lane) {
-    constexpr int TW = PX + 2;
-    const int Ws = W / PX;
+    constexpr int TW = PX + KS - 1;
+    const int Ho = H + 3 - KS, Ws = (W + 3 - KS) / PX;  // output grid (pad 1)
+    // input pixel of a super-pixel row's first output pixel (monotone in the row index)
+    auto pin = [&](int gr) -> int64_t {
+        const int xs = gr % Ws, yrow = gr / Ws;
+        return ((int64_t)(yrow / Ho) * H + yrow % Ho) * W + xs * PX;
+    };
+    const int64_t pin0 = pin(m0);
     ConvStage s;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1198,10 +1204,12 @@ __device__ __forceinline__ ConvStage make_conv_stage(int m0, int Mp, int H, int 
         const int tr = (j >> 6) * 128 + h * 64 + (j & 63);
         const int gr = m0 + tr;
         uint32_t mk = 0;
+        int64_t pg = pin0;
         if (gr < Mp) {
-            const int xs = gr % Ws, yrow = gr / Ws, y = yrow % H;
+            const int xs = gr % Ws, yrow = gr / Ws, y = yrow % Ho;
+            pg = pin(gr);
 #pragma unroll
-            for (int ty = 0; ty < 3; ++ty)
+            for (int ty = 0; ty < KS; ++ty)
 #pragma unroll
                 for (int tx = 0; tx < TW; ++tx) {
                     const int yy = y + ty - 1, xx = xs * PX + tx - 1;
@@ -1209,7 +1217,7 @@ __device__ __forceinline__ ConvStage make_conv_stage(int m0, int Mp, int H, int 
                 }
         }
         s.mask[i] = mk;
-        s.off[i] = ((uint32_t)(tr * PX) * (uint32_t)Cin + chunk * 8) * 2;  // pixel gr*PX - block base - (W+1)
+        s.off[i] = ((uint32_t)(pg - pin0) * (uint32_t)Cin + chunk * 8) * 2;  // from the block base pixel + (W+1)
     }
     return s;
 }
@@ -1256,14 +1264,70 @@ __device__ __forceinline__ void store_tile_t_act(f32x4 (&acc)[8][4], char* smem,
     store_tile_t(acc, smem, wave, lane, m0, n0, rbase, cbase, M, N, Y, ldy);
 }
 
-template <int PX, int ACT>
+// ResBlock tail fused into conv2's epilogue (NORM): RMSNorm over each pixel's COUT = 256 / PX
+// channels (a 256-column tile holds whole pixels), * w[c] + b[c] + res[row, col], on the fp32
+// accumulators.  Row sums of squares: 16 values per lane, xor-16/32 shuffles across the wave's 4
+// column lanes, then a [256 rows][4 waves] LDS table for the waves that share a pixel.
+template <int PX>
+__device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float* red, int wave, int lane, int m0,
+                                                      int Mp, float eps, const unsigned short* __restrict__ nw,
+                                                      const unsigned short* __restrict__ nb,
+                                                      const unsigned short* __restrict__ res) {
+    constexpr int COUT = 256 / PX;
+    const int wm = wave >> 2, wn = wave & 3, rl = lane & 15, cg = lane >> 4;
+    float ss[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float sq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sq += acc[i][j][e] * acc[i][j][e];
+        sq += __shfl_xor(sq, 16, 64);
+        sq += __shfl_xor(sq, 32, 64);
+        ss[i] = sq;
+    }
+    if (cg == 0)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[(wm * 128 + 16 * i + rl) * 4 + wn] = ss[i];
+    __syncthreads();
+    float wv[4][4], bv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = (wn * 64 + 16 * j + 4 * cg + e) % COUT;
+            wv[j][e] = bf16_to_f32(nw[c]);
+            bv[j][e] = nb ? bf16_to_f32(nb[c]) : 0.0f;
+        }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int rr = wm * 128 + 16 * i + rl;
+        const float* rp = red + rr * 4;
+        const float tot = PX == 1 ? (rp[0] + rp[1]) + (rp[2] + rp[3]) : rp[(wn >> 1) * 2] + rp[(wn >> 1) * 2 + 1];
+        const float rs = rsqrtf(tot / COUT + eps);
+        int row = m0 + rr;
+        row = row < Mp ? row : Mp - 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u16x4 r4 = *reinterpret_cast<const u16x4*>(res + (int64_t)row * 256 + wn * 64 + 16 * j + 4 * cg);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][e] = acc[i][j][e] * rs * wv[j][e] + bv[j][e] + bf16_to_f32(r4[e]);
+        }
+    }
+}
+
+template <int PX, int ACT, bool NORM = false, int KS = 3>
 __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* __restrict__ X,
                                                           const unsigned short* __restrict__ Wt,
                                                           const unsigned short* __restrict__ bias, int H, int W,
                                                           int Cin, int lcpt, int Mp, int N, int tiles_n,
-                                                          unsigned short* __restrict__ Y) {
-    constexpr int TW = PX + 2;
-    __shared__ __attribute__((aligned(16))) char smem[p8::LDS];
+                                                          unsigned short* __restrict__ Y, float eps = 0.0f,
+                                                          const unsigned short* __restrict__ nw = nullptr,
+                                                          const unsigned short* __restrict__ nb = nullptr,
+                                                          const unsigned short* __restrict__ res = nullptr) {
+    constexpr int TW = PX + KS - 1;
+    __shared__ __attribute__((aligned(16))) char smem[p8::LDS + (NORM ? 256 * 4 * 4 : 0)];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -1276,17 +1340,23 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     const int in_grp = tile - grp * per_group;
     const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
     const int m0 = tm * 256, n0 = tn * 256;
-    const int64_t K = (int64_t)3 * TW * Cin;
+    const int64_t K = (int64_t)KS * TW * Cin;
     const int nk = (int)(K / BK);
 
-    const ConvStage sA0 = make_conv_stage<PX>(m0, Mp, H, W, Cin, 0, wave, lane);
-    const ConvStage sA1 = make_conv_stage<PX>(m0, Mp, H, W, Cin, 1, wave, lane);
+    const ConvStage sA0 = make_conv_stage<PX, KS>(m0, Mp, H, W, Cin, 0, wave, lane);
+    const ConvStage sA1 = make_conv_stage<PX, KS>(m0, Mp, H, W, Cin, 1, wave, lane);
     const HalfStage sB0 = make_stage<false>(n0, N - 1, K, 0, wave, lane);
     const HalfStage sB1 = make_stage<false>(n0, N - 1, K, 1, wave, lane);
     char* const e_buf = smem;
     char* const o_buf = smem + p8::BUF;
-    // block base = pixel m0*PX - (W+1); tap (ty, tx) adds (ty*W + tx) pixels in soffset: >= 0 always
-    const unsigned short* xb = X + ((int64_t)m0 * PX - W - 1) * Cin;
+    // block base = input pixel of output row m0, minus (W+1); tap (ty, tx) adds (ty*W + tx) pixels in
+    // soffset, so every address offset is >= 0
+    int64_t pin0;
+    {
+        const int Ho = H + 3 - KS, Ws = (W + 3 - KS) / PX, xs = m0 % Ws, yrow = m0 / Ws;
+        pin0 = ((int64_t)(yrow / Ho) * H + yrow % Ho) * W + xs * PX;
+    }
+    const unsigned short* xb = X + (pin0 - W - 1) * Cin;
     const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
 
@@ -1345,7 +1415,12 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     __syncthreads();
     if (bias)
         lora_mfma_addend<0>(acc, lane, m0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, Mp, N);
-    store_tile_t_act<ACT>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
+    if constexpr (NORM) {
+        conv_rmsnorm_epilogue<PX>(acc, reinterpret_cast<float*>(smem + p8::LDS), wave, lane, m0, Mp, eps, nw, nb, res);
+        store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
+    } else {
+        store_tile_t_act<ACT>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
+    }
 }
 
 }  // namespace eggroll
@@ -1464,37 +1539,78 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
                              Y, ldy, stream);
 }
 
-/* Implicit-GEMM 3x3 conv (k_conv3x3_gemm8): see include/eggroll.h */
-int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
-                         int64_t Cin, int64_t N, int32_t px, int32_t act, void* y, void* stream) {
-    EGG_CHECK_ARG(px == 1 || px == 2, "conv3x3_nhwc: px must be 1 or 2 (got %d)", px);
-    EGG_CHECK_ARG(act == 0 || act == 2, "conv3x3_nhwc: act must be 0 (none) or 2 (silu) (got %d)", act);
-    EGG_CHECK_ARG(B > 0 && H > 0 && W > 0 && W % px == 0, "conv3x3_nhwc: bad B/H/W (W %% px == 0 required)");
+/* Implicit-GEMM ks x ks conv, pad 1 (k_conv3x3_gemm8): see include/eggroll.h */
+int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
+                      int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, void* stream) {
+    EGG_CHECK_ARG(ks == 2 || ks == 3, "conv_nhwc: ks must be 2 or 3 (got %d)", ks);
+    EGG_CHECK_ARG(px == 1 || px == 2, "conv_nhwc: px must be 1 or 2 (got %d)", px);
+    EGG_CHECK_ARG(ks == 3 || px == 1, "conv_nhwc: px 2 needs ks 3");
+    EGG_CHECK_ARG(act == 0 || act == 2, "conv_nhwc: act must be 0 (none) or 2 (silu) (got %d)", act);
+    const int64_t Ho = H + 3 - ks, Wo = W + 3 - ks;
+    EGG_CHECK_ARG(B > 0 && H > 0 && W > 0 && Wo % px == 0, "conv_nhwc: bad B/H/W (output width %% px == 0 required)");
     EGG_CHECK_ARG(Cin >= 64 && Cin <= 2048 && (Cin & (Cin - 1)) == 0,
-                  "conv3x3_nhwc: Cin=%lld must be a power of two in [64, 2048]", (long long)Cin);
-    EGG_CHECK_ARG(N >= 64 && N % 64 == 0 && N <= 8192, "conv3x3_nhwc: N=%lld must be a multiple of 64 (<= 8192)",
+                  "conv_nhwc: Cin=%lld must be a power of two in [64, 2048]", (long long)Cin);
+    EGG_CHECK_ARG(N >= 64 && N % 64 == 0 && N <= 8192, "conv_nhwc: N=%lld must be a multiple of 64 (<= 8192)",
                   (long long)N);
-    const int64_t Mp = B * H * (W / px);
-    const int64_t K = 3 * (px + 2) * Cin;
-    EGG_CHECK_ARG(Mp < (1ll << 31) && (256 * px + 2 * W + 8) * Cin * 2 < (1ll << 30) && N * K * 2 < (1ll << 31),
-                  "conv3x3_nhwc: sizes exceed the kernel's 32-bit offsets");
-    EGG_CHECK_ARG(x && w_packed && y, "conv3x3_nhwc: NULL pointer");
+    const int64_t Mp = B * Ho * (Wo / px);
+    const int64_t K = ks * (px + ks - 1) * Cin;
+    EGG_CHECK_ARG(Mp < (1ll << 31) && (256 * (px + 1) + 2 * W + 8) * Cin * 2 < (1ll << 30) && N * K * 2 < (1ll << 31),
+                  "conv_nhwc: sizes exceed the kernel's 32-bit offsets");
+    EGG_CHECK_ARG(x && w_packed && y, "conv_nhwc: NULL pointer");
     const int64_t tiles_m = (Mp + 255) / 256, tiles_n = (N + 255) / 256;
-    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "conv3x3_nhwc: grid too large");
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "conv_nhwc: grid too large");
     int lcpt = 0;
     while ((64ll << lcpt) < Cin) ++lcpt;
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     hipStream_t st = as_stream(stream);
-#define EGG_CONV(PX_, ACT_)                                                                                    \
-    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, ACT_>), grid, dim3(512), 0, st, (const unsigned short*)x,           \
+#define EGG_CONV(PX_, ACT_, KS_)                                                                               \
+    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, ACT_, false, KS_>), grid, dim3(512), 0, st, (const unsigned short*)x, \
                        (const unsigned short*)w_packed, (const unsigned short*)bias, (int)H, (int)W, (int)Cin, lcpt, \
-                       (int)Mp, (int)N, (int)tiles_n, (unsigned short*)y)
-    if (px == 1 && act == 0) EGG_CONV(1, 0);
-    else if (px == 1) EGG_CONV(1, 1);
-    else if (act == 0) EGG_CONV(2, 0);
-    else EGG_CONV(2, 1);
+                       (int)Mp, (int)N, (int)tiles_n, (unsigned short*)y, 0.0f, nullptr, nullptr, nullptr)
+    if (ks == 2) {
+        if (act == 0) EGG_CONV(1, 0, 2);
+        else EGG_CONV(1, 1, 2);
+    } else if (px == 1 && act == 0) EGG_CONV(1, 0, 3);
+    else if (px == 1) EGG_CONV(1, 1, 3);
+    else if (act == 0) EGG_CONV(2, 0, 3);
+    else EGG_CONV(2, 1, 3);
 #undef EGG_CONV
-    EGG_CHECK_LAUNCH("conv3x3_nhwc");
+    EGG_CHECK_LAUNCH("conv_nhwc");
+    return EGGROLL_OK;
+}
+
+int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
+                         int64_t Cin, int64_t N, int32_t px, int32_t act, void* y, void* stream) {
+    return eggroll_conv_nhwc(x, w_packed, bias, B, H, W, Cin, N, 3, px, act, y, stream);
+}
+
+/* ResBlock conv2 + RMSNorm + residual in one launch: see include/eggroll.h */
+int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
+                                 int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
+                                 const void* norm_b, const void* res, void* y, void* stream) {
+    EGG_CHECK_ARG(px == 1 || px == 2, "conv3x3_rmsnorm_nhwc: px must be 1 or 2 (got %d)", px);
+    EGG_CHECK_ARG(N == 256, "conv3x3_rmsnorm_nhwc: N = px * Cout must be 256 (got %lld)", (long long)N);
+    EGG_CHECK_ARG(B > 0 && H > 0 && W > 0 && W % px == 0, "conv3x3_rmsnorm_nhwc: bad B/H/W (W %% px == 0 required)");
+    EGG_CHECK_ARG(Cin >= 64 && Cin <= 2048 && (Cin & (Cin - 1)) == 0,
+                  "conv3x3_rmsnorm_nhwc: Cin=%lld must be a power of two in [64, 2048]", (long long)Cin);
+    const int64_t Mp = B * H * (W / px);
+    EGG_CHECK_ARG(Mp < (1ll << 31) && (256 * px + 2 * W + 8) * Cin * 2 < (1ll << 30),
+                  "conv3x3_rmsnorm_nhwc: sizes exceed the kernel's 32-bit offsets");
+    EGG_CHECK_ARG(x && w_packed && y && norm_w && res, "conv3x3_rmsnorm_nhwc: NULL pointer");
+    EGG_CHECK_ARG(res != y && x != y, "conv3x3_rmsnorm_nhwc: y may not alias x or res");
+    int lcpt = 0;
+    while ((64ll << lcpt) < Cin) ++lcpt;
+    const dim3 grid((unsigned)((Mp + 255) / 256));
+    hipStream_t st = as_stream(stream);
+#define EGG_CONVN(PX_)                                                                                          \
+    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, 0, true>), grid, dim3(512), 0, st, (const unsigned short*)x,       \
+                       (const unsigned short*)w_packed, (const unsigned short*)bias, (int)H, (int)W, (int)Cin, lcpt, \
+                       (int)Mp, 256, 1, (unsigned short*)y, eps, (const unsigned short*)norm_w,                 \
+                       (const unsigned short*)norm_b, (const unsigned short*)res)
+    if (px == 1) EGG_CONVN(1);
+    else EGG_CONVN(2);
+#undef EGG_CONVN
+    EGG_CHECK_LAUNCH("conv3x3_rmsnorm_nhwc");
     return EGGROLL_OK;
 }
 

@@ -96,6 +96,9 @@ class ResBlock(nn.Module):
                 self.refresh_packed_weights()
             w1, b1, w2 = self.packed
             h = K.conv3x3_nhwc(x, w1, b1, self.px, "silu")
+            if w2.shape[0] == 256:  # whole pixels per tile: RMSNorm + residual in conv2's epilogue
+                n = self.norm
+                return K.conv3x3_rmsnorm_nhwc(h, w2, None, self.px, n.eps, n.weight, n.bias, x)
             return self.norm(K.conv3x3_nhwc(h, w2, None, self.px), res=x)
         c1 = self.conv1
         h = nhwc(F.conv2d(nchw(x), c1.weight, None, padding=1)).contiguous()
@@ -194,20 +197,26 @@ class UpBlock(nn.Module):
         super().__init__()
         self.conv = Conv3x3(cin, cout)           # the architecture's 3x3 weights (source of truth)
         self.repeats = cout * 4 // cin
-        self.w4 = None
+        self.w4 = self.w4p = None
 
     def refresh_phase_weights(self):
         w4 = subpixel_phase_weights(self.conv.weight)
         self.w4 = w4.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        cin = self.w4.shape[1]
+        # libeggroll's implicit-GEMM conv (ks 2) when the widths fit it, else MIOpen
+        self.w4p = (K.pack_conv3x3_weight(self.w4, 1)
+                    if 64 <= cin <= 2048 and cin & (cin - 1) == 0 and self.w4.shape[0] % 64 == 0 else None)
 
     def forward(self, x):  # NHWC
         if self.w4 is None:
             self.refresh_phase_weights()
         x = x.contiguous()
-        # bias-free phase conv (MIOpen's bias-fused conv path ran these at 650-850 TF vs ~1 PF without);
-        # the conv bias is added in fp32 by the interleave kernel
-        y4 = nhwc(F.conv2d(nchw(x), self.w4, None, padding=1))
-        return K.subpixel_shortcut(y4.contiguous(), x, bias=self.conv.bias)
+        # bias-free phase conv; the conv bias is added in fp32 by the interleave kernel
+        if self.w4p is not None:
+            y4 = K.conv_nhwc(x, self.w4p, None, 2)
+        else:
+            y4 = nhwc(F.conv2d(nchw(x), self.w4, None, padding=1)).contiguous()
+        return K.subpixel_shortcut(y4, x, bias=self.conv.bias)
 
     def forward_reference(self, x):  # the literal architecture (for tests)
         up = F.interpolate(nchw(x), scale_factor=2, mode="nearest")

@@ -514,15 +514,41 @@ def dcae_head(x: torch.Tensor, eps: float, norm_w: torch.Tensor, norm_b: torch.T
 
 
 def pack_conv3x3_weight(w: torch.Tensor, px: int) -> torch.Tensor:
-    """[Cout, Cin, 3, 3] conv weight -> the implicit-GEMM operand [px*Cout, 3*(px+2)*Cin] bf16 of
-    eggroll_conv3x3_nhwc: row p*Cout + o, column (ky*(px+2) + tx)*Cin + c holds w[o, c, ky, tx - p]
-    (zero where tx - p is outside 0..2).  px = 1 is the channels-last weight itself."""
-    Cout, Cin = w.shape[0], w.shape[1]
+    """[Cout, Cin, ks, ks] conv weight -> the implicit-GEMM operand [px*Cout, ks*(px+ks-1)*Cin] bf16 of
+    eggroll_conv_nhwc: row p*Cout + o, column (ky*(px+ks-1) + tx)*Cin + c holds w[o, c, ky, tx - p]
+    (zero where tx - p is outside 0..ks-1).  px = 1 is the channels-last weight itself."""
+    Cout, Cin, ks = w.shape[0], w.shape[1], w.shape[-1]
     wt = w.permute(0, 2, 3, 1).to(torch.bfloat16)  # [o][ky][kx][c]
-    out = torch.zeros((px, Cout, 3, px + 2, Cin), dtype=torch.bfloat16, device=w.device)
+    tw = px + ks - 1
+    out = torch.zeros((px, Cout, ks, tw, Cin), dtype=torch.bfloat16, device=w.device)
     for p in range(px):
-        out[p, :, :, p:p + 3, :] = wt
-    return out.reshape(px * Cout, 3 * (px + 2) * Cin).contiguous()
+        out[p, :, :, p:p + ks, :] = wt
+    return out.reshape(px * Cout, ks * tw * Cin).contiguous()
+
+
+def conv_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], ks: int, px: int = 1,
+              act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ks x ks conv (ks 2 or 3), zero pad 1, of x [B,H,W,Cin] NHWC bf16 -> [B, H+3-ks, W+3-ks, N/px]."""
+    _dev(x, "conv(x)", torch.bfloat16)
+    _dev(w_packed, "conv(w)", torch.bfloat16)
+    x = x.contiguous()
+    B, H, W, Cin = x.shape
+    N = w_packed.shape[0]
+    if w_packed.shape[1] != ks * (px + ks - 1) * Cin or N % px:
+        raise ValueError(f"conv: packed weight {tuple(w_packed.shape)} does not match Cin={Cin}, ks={ks}, px={px}")
+    if bias is not None:
+        _dev(bias, "conv(bias)", torch.bfloat16)
+        if bias.numel() != N:
+            raise ValueError(f"conv: bias has {bias.numel()} entries, need {N}")
+    Ho, Wo, Cout = H + 3 - ks, W + 3 - ks, N // px
+    if out is None:
+        out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_conv_nhwc", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, ks, px, ACT[act],
+              out.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, f"conv{ks}x{ks}", 2.0 * (x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout} px{px}",
+                flops=2.0 * B * Ho * Wo * Cout * ks * ks * Cin)
+    return out
 
 
 def conv3x3_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], px: int,
@@ -548,6 +574,32 @@ def conv3x3_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.T
               ACT[act], out.data_ptr(), _stream(x.device))
     OpTimer.end(e0, "conv3x3", 2.0 * (x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout} px{px}",
                 flops=2.0 * B * H * W * Cout * 9 * Cin)
+    return out
+
+
+def conv3x3_rmsnorm_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], px: int, eps: float,
+                         norm_w: torch.Tensor, norm_b: Optional[torch.Tensor], res: torch.Tensor) -> torch.Tensor:
+    """conv3x3_nhwc followed by RMSNorm over channels (* norm_w + norm_b) + res, in one launch
+    (the DC-AE ResBlock tail); px * Cout must be 256."""
+    _dev(x, "conv3x3_rmsnorm(x)", torch.bfloat16)
+    _dev(w_packed, "conv3x3_rmsnorm(w)", torch.bfloat16)
+    _dev(norm_w, "conv3x3_rmsnorm(norm_w)", torch.bfloat16)
+    _dev(res, "conv3x3_rmsnorm(res)", torch.bfloat16)
+    x, res = x.contiguous(), res.contiguous()
+    B, H, W, Cin = x.shape
+    N = w_packed.shape[0]
+    if N != 256 or w_packed.shape[1] != 3 * (px + 2) * Cin or res.shape != (B, H, W, N // px):
+        raise ValueError(f"conv3x3_rmsnorm: packed weight {tuple(w_packed.shape)} / res {tuple(res.shape)} do not "
+                         f"match x {tuple(x.shape)}, px={px} (px * Cout must be 256)")
+    for t, nm in ((bias, "bias"), (norm_b, "norm_b")):
+        if t is not None:
+            _dev(t, f"conv3x3_rmsnorm({nm})", torch.bfloat16)
+    out = torch.empty_like(res)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_conv3x3_rmsnorm_nhwc", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, px,
+              float(eps), norm_w.data_ptr(), _p(norm_b), res.data_ptr(), out.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, "conv3x3", 2.0 * (x.numel() + 2 * out.numel()), f"{tuple(x.shape)}->{N // px} px{px} +norm",
+                flops=2.0 * B * H * W * (N // px) * 9 * Cin)
     return out
 
 

@@ -209,6 +209,19 @@ int eggroll_bias_act(void* y, const void* bias, int64_t rows, int64_t C, int32_t
  * N % 64 == 0, W % px == 0.  x [B,H,W,Cin]; y [B,H,W,Cout] contiguous.                          */
 int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
                          int64_t W, int64_t Cin, int64_t N, int32_t px, int32_t act, void* y, void* stream);
+/* General form: ks x ks conv (ks 2 or 3), zero pad 1, output [B, H+3-ks, W+3-ks, N/px]:
+ *   y[b, h, x, o] = act(bias[o] + sum_{ky,kx,c} x[b, h+ky-1, x+kx-1, c] * w[o, c, ky, kx])
+ * w_packed [N = px*Cout][ks][px+ks-1][Cin] (px 2 only with ks 3).  ks = 2 is the sub-pixel
+ * phase conv of the DC-AE up-blocks (see eggroll_subpixel_shortcut).                          */
+int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
+                      int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, void* stream);
+/* The same conv with the ResBlock tail fused into its epilogue (conv2 -> RMSNorm -> + residual):
+ *   y[p, c] = bf16(z[p, c] / sqrt(mean_c z[p, :]^2 + eps) * norm_w[c] (+ norm_b[c]) + res[p, c])
+ * with z the fp32 conv output (+ bias); requires N = px * Cout = 256 (whole pixels per tile:
+ * Cout 128 with px 2, Cout 256 with px 1).  res [B,H,W,Cout] bf16 (may not alias y).         */
+int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
+                                 int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
+                                 const void* norm_b, const void* res, void* y, void* stream);
 
 /* ReLU linear attention with head dim 32 (diffusers SanaLinearAttnProcessor2_0 and DC-AE
  * SanaMultiscaleLinearAttention): for every image b and head h over its N tokens,

@@ -522,3 +522,34 @@ def test_conv3x3_nhwc_rejects_bad_shapes(dev):
     w = K.pack_conv3x3_weight(torch.zeros(64, 96, 3, 3, device=dev, dtype=torch.bfloat16), 1)
     with pytest.raises(RuntimeError):
         K.conv3x3_nhwc(x, w, None, 1)
+
+
+@pytest.mark.parametrize("B,H,W,Cin,px", [(2, 16, 32, 128, 2), (1, 7, 10, 128, 2), (1, 9, 12, 256, 1), (2, 5, 6, 64, 1)])
+def test_conv3x3_rmsnorm_nhwc_vs_torch(dev, B, H, W, Cin, px):
+    """conv3x3 -> RMSNorm(* w + b) -> + res in one launch vs torch fp32 on the same bf16 inputs."""
+    Cout = 256 // px
+    g = torch.Generator().manual_seed(7 + H)
+    x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)
+    nw = (1 + 0.2 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
+    nb = (0.2 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
+    res = torch.randn(B, H, W, Cout, generator=g).to(dev, torch.bfloat16)
+    y = K.conv3x3_rmsnorm_nhwc(x, K.pack_conv3x3_weight(w, px), None, px, 1e-5, nw, nb, res).float()
+    z = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), None, padding=1).permute(0, 2, 3, 1)
+    ref = z * torch.rsqrt(z.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float() + nb.float() + res.float()
+    err = (y - ref).abs()
+    tol = 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("B,H,W,Cin,N", [(2, 6, 5, 64, 128), (1, 16, 16, 128, 512), (3, 9, 4, 256, 64)])
+def test_conv2x2_pad1_nhwc_vs_torch(dev, B, H, W, Cin, N):
+    """ks = 2 implicit-GEMM conv (the up-blocks' sub-pixel phase conv, output (H+1) x (W+1)) vs torch."""
+    g = torch.Generator().manual_seed(11 + W)
+    x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, Cin, 2, 2, generator=g) / math.sqrt(4 * Cin)).to(dev, torch.bfloat16)
+    y = K.conv_nhwc(x, K.pack_conv3x3_weight(w, 1), None, 2).float()
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), None, padding=1).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    err = (y - ref).abs()
+    assert bool((err <= 2.0 ** -8 * ref.abs() + 1e-3 * ref.abs().max()).all()), f"max err {err.max().item():.3e}"

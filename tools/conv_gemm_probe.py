@@ -52,5 +52,24 @@ for B, C, hw, pxs in [(8, 128, 1024, (2, 1)), (8, 256, 512, (1, 2)), (8, 512, 25
         row[f"px{px}_tflops"] = round(fl / ms / 1e9, 1)
         row[f"px{px}_bias_silu_ms"] = round(ms_f, 3)
         row[f"px{px}_relerr"] = float(f"{err:.2e}")
+        if wp.shape[0] == 256:  # conv2 + RMSNorm + residual fused
+            nw = torch.ones(C, device=dev, dtype=torch.bfloat16)
+            row[f"px{px}_norm_ms"] = round(t(lambda: K.conv3x3_rmsnorm_nhwc(x, wp, None, px, 1e-5, nw, nw, x)), 3)
+            row["rownorm_ms"] = round(t(lambda: K.rownorm(out, 1e-5, layer=False, w=nw, b=nw, res=x)), 3)
     print(json.dumps(row), flush=True)
     del x, y, out
+
+
+# DC-AE up-block sub-pixel phase convs (2x2, pad 1, 4*Cout outputs) at the bench's 8-image batch
+for B, cin, cout, hw in [(8, 256, 128, 512), (8, 512, 256, 256), (8, 512, 512, 128), (8, 1024, 512, 64)]:
+    x = torch.randn(B, hw, hw, cin, device=dev, dtype=torch.bfloat16)
+    w4 = (torch.randn(4 * cout, cin, 2, 2, device=dev) / (4 * cin) ** 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    fl = 2.0 * B * (hw + 1) ** 2 * 4 * cout * 4 * cin
+    xn = x.permute(0, 3, 1, 2)
+    ms_m = t(lambda: F.conv2d(xn, w4, None, padding=1))
+    wp = K.pack_conv3x3_weight(w4, 1)
+    ms = t(lambda: K.conv_nhwc(x, wp, None, 2))
+    print(json.dumps({"upblock": f"{B}x{hw}x{hw}x{cin}->{4 * cout}", "miopen_ms": round(ms_m, 3),
+                      "miopen_tflops": round(fl / ms_m / 1e9, 1), "ours_ms": round(ms, 3),
+                      "ours_tflops": round(fl / ms / 1e9, 1)}), flush=True)
