@@ -1356,7 +1356,12 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
         const int Ho = H + 3 - KS, Ws = (W + 3 - KS) / PX, xs = m0 % Ws, yrow = m0 / Ws;
         pin0 = ((int64_t)(yrow / Ho) * H + yrow % Ho) * W + xs * PX;
     }
-    const unsigned short* xb = X + (pin0 - W - 1) * Cin;
+    // (readfirstlane: the divisions above run on the VALU; an SGPR resource keeps every DMA a single
+    // instruction instead of a readfirstlane waterfall)
+    const uint64_t xbu = (uint64_t)(X + (pin0 - W - 1) * Cin);
+    const unsigned short* xb = (const unsigned short*)(
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(xbu >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xbu));
     const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
 
@@ -1375,7 +1380,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     auto A = [&](const ConvStage& s, int t, char* dst) {
         t = t < nk ? t : nk - 1;
         const int tap = t >> lcpt, ty = tap / TW, tx = tap - ty * TW;
-        const int soff = ((ty * W + tx) * Cin + (t & cmask) * BK) * 2;
+        const int soff = __builtin_amdgcn_readfirstlane(((ty * W + tx) * Cin + (t & cmask) * BK) * 2);
         issue_conv_half(rX, s, tap, soff, dst, wave);
     };
     auto B = [&](const HalfStage& s, int t, char* dst) {
