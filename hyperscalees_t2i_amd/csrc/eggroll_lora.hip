@@ -1269,12 +1269,12 @@ __device__ __forceinline__ void store_tile_t_act(f32x4 (&acc)[8][4], char* smem,
 // accumulators.  Row sums of squares: 16 values per lane, xor-16/32 shuffles across the wave's 4
 // column lanes, then a [256 rows][4 waves] LDS table for the waves that share a pixel.
 template <int PX>
-__device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float* red, int wave, int lane, int m0,
+__device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float* red, int wm, int wn, int lane, int m0,
                                                       int Mp, float eps, const unsigned short* __restrict__ nw,
                                                       const unsigned short* __restrict__ nb,
                                                       const unsigned short* __restrict__ res) {
     constexpr int COUT = 256 / PX;
-    const int wm = wave >> 2, wn = wave & 3, rl = lane & 15, cg = lane >> 4;
+    const int rl = lane & 15, cg = lane >> 4;
     float ss[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1421,7 +1421,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     if (bias)
         lora_mfma_addend<0>(acc, lane, m0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, Mp, N);
     if constexpr (NORM) {
-        conv_rmsnorm_epilogue<PX>(acc, reinterpret_cast<float*>(smem + p8::LDS), wave, lane, m0, Mp, eps, nw, nb, res);
+        conv_rmsnorm_epilogue<PX>(acc, reinterpret_cast<float*>(smem + p8::LDS), wm, wn, lane, m0, Mp, eps, nw, nb, res);
         store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
     } else {
         store_tile_t_act<ACT>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
