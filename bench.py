@@ -171,6 +171,9 @@ def main():
     log(f"rank {rank}: timed {args.steps} epochs in {elapsed:.3f}s")
     GemmTimer.active = False
     marker()  # timed region ends
+    if world > 1:  # theta' must be bit-identical on every rank (outside the timed region)
+        from hyperscalees_t2i_amd.es_step import verify_theta_replicas
+        verify_theta_replicas(theta, engine.dist)
     gemm = GemmTimer.summary()
     # one extra instrumented epoch for the per-phase breakdown (not part of the timed region)
     from hyperscalees_t2i_amd.kernels import OpTimer

@@ -68,6 +68,30 @@ def all_gather_members(local: torch.Tensor, pop: int, info: DistInfo) -> torch.T
     return torch.cat([outs[r][: hi - lo] for r, (lo, hi) in enumerate(shards)])
 
 
+def theta_checksum(theta: torch.Tensor) -> torch.Tensor:
+    """Order-independent bit checksum of fp32 theta: int64 sums of its words and of the words
+    weighted by (index mod 65521 + 1), so a swap or a one-ulp change on any element shows."""
+    w = theta.detach().contiguous().view(torch.int32).to(torch.int64)
+    idx = torch.arange(w.numel(), device=w.device, dtype=torch.int64) % 65521 + 1
+    return torch.stack([w.sum(), (w * idx).sum()])
+
+
+def verify_theta_replicas(theta: torch.Tensor, info: DistInfo) -> None:
+    """Debug check of SURVEY §8(e) "theta checksum allReduce": every rank runs the same fitness and
+    update kernels on the same gathered S, so theta' must be bit-identical on every rank.  Two
+    all-reduces (MIN, MAX) of the checksum; raises on every rank if any replica diverged."""
+    if info.world == 1:
+        return
+    import torch.distributed as dist
+    c = theta_checksum(theta)
+    lo, hi = c.clone(), c.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=info.group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=info.group)
+    if not torch.equal(lo, hi):
+        raise RuntimeError(f"theta replicas diverged across ranks (checksum min {lo.tolist()} != max {hi.tolist()}, "
+                           f"rank {info.rank} has {c.tolist()})")
+
+
 # ---------------------------------------------------------------------------------------
 # engine
 # ---------------------------------------------------------------------------------------
@@ -84,6 +108,7 @@ class ESConfig:
     theta_max_norm: float = 40.0
     max_step_norm: float = 0.0
     max_log_batches: int = 1
+    verify_replicas: bool = False   # debug: theta checksum all-reduce after every update (N > 1)
 
 
 class ESEngine:
@@ -156,6 +181,8 @@ class ESEngine:
         S, raw = both[:, :m].contiguous(), both[:, m:]
         mark("allgather")
         theta_new, stats = self.finish(theta, S, raw, factors, info, seed, mark=mark)
+        if self.cfg.verify_replicas:
+            verify_theta_replicas(theta_new, self.dist)
         if timing:
             torch.cuda.synchronize()
             self.timings = {ev[i][0]: ev[i - 1][1].elapsed_time(ev[i][1]) for i in range(1, len(ev))}

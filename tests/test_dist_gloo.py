@@ -7,7 +7,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from hyperscalees_t2i_amd.es_step import DistInfo, all_gather_members, member_shard
+from hyperscalees_t2i_amd.es_step import DistInfo, all_gather_members, member_shard, verify_theta_replicas
 from oracle import eggroll_oracle as O
 
 
@@ -58,3 +58,35 @@ def test_member_shard_partition():
             assert spans[0][0] == 0 and spans[-1][1] == pop
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _verify_worker(rank, world, port, diverge, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        theta = torch.randn(1000, generator=torch.Generator().manual_seed(3))
+        if diverge and rank == world - 1:
+            theta[517] = torch.nextafter(theta[517], torch.tensor(1e9))  # one ulp on one rank
+        try:
+            verify_theta_replicas(theta, DistInfo(rank, world))
+            q.put((rank, "ok"))
+        except RuntimeError as e:
+            q.put((rank, "diverged" if "diverged" in str(e) else str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("diverge", [False, True])
+def test_verify_theta_replicas_gloo(diverge):
+    """theta checksum all-reduce (SURVEY §8e debug): silent when replicas agree, raises on EVERY rank
+    when one rank's theta differs by one ulp in one element."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port, world = _free_port(), 2
+    procs = [ctx.Process(target=_verify_worker, args=(r, world, port, diverge, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert set(res.values()) == {"diverged" if diverge else "ok"}
