@@ -151,7 +151,10 @@ __global__ __launch_bounds__(256) void k_lora_project_ra(const unsigned short* _
 //   128 KiB LDS) — half the LDS bytes per FLOP.
 // ------------------------------------------------------------------------------------
 constexpr int BK = 64;
-constexpr int GROUP_M = 8;  // row-tiles per rasterisation group
+#ifndef EGG_GROUP_M
+#define EGG_GROUP_M 8
+#endif
+constexpr int GROUP_M = EGG_GROUP_M;  // row-tiles per rasterisation group
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
