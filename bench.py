@@ -171,9 +171,15 @@ def main():
     log(f"rank {rank}: timed {args.steps} epochs in {elapsed:.3f}s")
     GemmTimer.active = False
     marker()  # timed region ends
+    replicas_identical = None
     if world > 1:  # theta' must be bit-identical on every rank (outside the timed region)
         from hyperscalees_t2i_amd.es_step import verify_theta_replicas
-        verify_theta_replicas(theta, engine.dist)
+        try:
+            verify_theta_replicas(theta, engine.dist)
+            replicas_identical = True
+        except RuntimeError as e:  # reported in the line, not fatal: the throughput was still measured
+            log(f"rank {rank}: {e}")
+            replicas_identical = False
     gemm = GemmTimer.summary()
     # one extra instrumented epoch for the per-phase breakdown (not part of the timed region)
     from hyperscalees_t2i_amd.kernels import OpTimer
@@ -228,6 +234,7 @@ def main():
                        "parallelism": f"member-shard x{world} (S all-gather)"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "theta_replicas_identical": replicas_identical,
             "phases_ms": phases,
             "aux_kernels": aux,
             "aux_kernels_pop64_per_gpu": aux64,
