@@ -140,24 +140,26 @@ class MultiscaleLinearAttention(nn.Module):
         self.w_out = _p(c, inner * (1 + len(scales)))
         self.norm_out = RMSNormC(c)
 
-    def _attend(self, br):  # br [B,H,W,3*inner]: per head group h, channels [q | k | v] of 32 each
+    def _attend(self, br, out):  # br [B,H,W,3*inner]: per head group h, channels [q | k | v] of 32 each
         B, H, W, C3 = br.shape
         flat = br.reshape(B * H * W, C3)
         hs = 3 * self.hd
-        o = K.linear_attention(flat, flat[:, self.hd:], flat[:, 2 * self.hd:], B, H * W, self.heads, hs,
-                               relu_qk=True)
-        return o.view(B, H, W, -1)
+        K.linear_attention(flat, flat[:, self.hd:], flat[:, 2 * self.hd:], B, H * W, self.heads, hs,
+                           relu_qk=True, out=out)
 
     def forward(self, x):  # NHWC
         B, H, W, C = x.shape
         qkv = F.linear(x, self.w_qkv)                             # [B,H,W,3*inner]
-        outs = [self._attend(qkv)]
-        for ks, wdw, wpw in zip(self.scales, self.ms_dw, self.ms_pw):
+        inner = self.heads * self.hd
+        # every branch's attention output lands in its column slice of one buffer (no concat pass)
+        o = torch.empty((B * H * W, inner * (1 + len(self.scales))), dtype=x.dtype, device=x.device)
+        self._attend(qkv, o[:, :inner])
+        for i, (ks, wdw, wpw) in enumerate(zip(self.scales, self.ms_dw, self.ms_pw)):
             d = K.dwconv_nhwc(qkv, wdw, None, ks, pre_silu=False, glu=False)
             g = d.view(B * H * W, 3 * self.heads, self.hd).transpose(0, 1)       # [G, n, 32]
             p = torch.bmm(g, wpw.transpose(1, 2)).transpose(0, 1).reshape(B, H, W, -1)
-            outs.append(self._attend(p))
-        y = F.linear(torch.cat(outs, dim=-1), self.w_out)
+            self._attend(p, o[:, (i + 1) * inner:(i + 2) * inner])
+        y = F.linear(o.view(B, H, W, -1), self.w_out)
         return self.norm_out(y, res=x)
 
 

@@ -463,6 +463,38 @@ def test_linear_attention_interleaved_relu(dev):
     assert rel < 8e-3, rel
 
 
+def test_multiscale_linear_attention_vs_literal(dev):
+    """DC-AE SanaMultiscaleLinearAttention (both branches written into column slices of one buffer)
+    vs the literal fp32 restatement: qkv proj -> [qkv, grouped-1x1(dw5x5(qkv))] -> ReLU linear
+    attention per branch -> concat -> out proj.  The shared RMSNorm+residual tail is applied to both."""
+    from hyperscalees_t2i_amd.dcae import MultiscaleLinearAttention
+    torch.manual_seed(7)
+    c, B, H, W = 128, 2, 9, 13
+    m = MultiscaleLinearAttention(c).to(dev)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_((torch.randn_like(p, dtype=torch.float32) * 0.1).to(p.dtype))
+    x = torch.randn(B, H, W, c, device=dev).to(torch.bfloat16)
+    with torch.no_grad():
+        got = m(x).float()
+        heads, hd = m.heads, m.hd
+        qkv = x.float() @ m.w_qkv.float().t()
+        ks = m.scales[0]
+        wc = m.ms_dw[0].float().t().reshape(-1, 1, ks, ks)
+        d = torch.nn.functional.conv2d(qkv.permute(0, 3, 1, 2), wc, padding=ks // 2,
+                                       groups=wc.shape[0]).permute(0, 2, 3, 1)
+        p = torch.einsum("ngj,gij->ngi", d.reshape(-1, 3 * heads, hd), m.ms_pw[0].float()).reshape(B, H, W, -1)
+        outs = []
+        for br in (qkv, p):
+            b5 = br.reshape(B, H * W, heads, 3, hd)
+            outs.append(_linear_attention_ref(b5[:, :, :, 0], b5[:, :, :, 1], b5[:, :, :, 2], relu=True)
+                        .reshape(B, H, W, -1))
+        y = torch.cat(outs, dim=-1) @ m.w_out.float().t()
+        ref = m.norm_out(y.to(torch.bfloat16), res=x).float()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
+
+
 def test_bias_act_and_resblock(dev):
     g = torch.Generator().manual_seed(5)
     y = torch.randn(3, 5, 7, 64, generator=g).to(torch.bfloat16).to(dev)
