@@ -585,3 +585,38 @@ def test_conv2x2_pad1_nhwc_vs_torch(dev, B, H, W, Cin, N):
     assert y.shape == ref.shape
     err = (y - ref).abs()
     assert bool((err <= 2.0 ** -8 * ref.abs() + 1e-3 * ref.abs().max()).all()), f"max err {err.max().item():.3e}"
+
+
+# ---------------------------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("pop", [64, 128])
+def test_full_size_sana_layout_properties(dev, pop):
+    """BASELINE sizes (Sana-Sprint 1.6B LoRA theta, D = 1,515,456, pop 64 / 128) through size-independent
+    properties: antithetic eps pairs are exact negatives; any member range of perturb equals the
+    same rows of the full perturb; theta + eps rows == perturb rows; identical score rows for every
+    antithetic pair give identical fitness -> every collapsed coefficient is 0 -> theta' == theta
+    bit-exact; and the update matches the oracle's reference formula (rtol 1e-5) on random S."""
+    from hyperscalees_t2i_amd.sana import sana_lora_shapes
+    shapes = sana_lora_shapes()
+    n = EggRollNoiser(shapes, sigma=0.01, lr_scale=0.1, rank=1, use_antithetic=True)
+    assert n.num_params == 1515456
+    fac = n.sample_factors(pop, dev, seed=pop + 1)
+    g = torch.Generator().manual_seed(pop)
+    theta = (torch.randn(n.num_params, generator=g) * 0.02).to(dev)
+    eps = n.eps_from_factors(fac, pop)
+    h = pop // 2
+    assert torch.equal(eps[:h], -eps[h:])
+    lo, hi = pop // 2 - 3, pop // 2 + 5
+    part = n.perturb(theta, fac, pop, lo, hi)
+    assert torch.equal(part, theta + 0.01 * eps[lo:hi])
+    assert torch.equal(part[1:3], n.perturb(theta, fac, pop, lo + 1, lo + 3))
+    # paired identical scores -> zero update, bit-exact, at full size
+    S_half = torch.randn(h, 4, generator=g) + 20
+    fit = K.fitness(torch.cat([S_half, S_half]).to(dev), True)
+    assert torch.equal(n.update_from_factors(theta, fac, fit, pop, 0.0, 0.0), theta)
+    # random scores: reference formula via the oracle
+    S = (torch.randn(pop, 4, generator=g) + 20).to(dev)
+    fit = K.fitness(S, True)
+    out = n.update_from_factors(theta, fac, fit, pop, 0.0, 40.0)
+    ref, _ = O.ref_es_tail(S.cpu().numpy(), eps.cpu().numpy(), theta.cpu().numpy(), promptnorm=True, lr_scale=0.1,
+                           sigma=0.01, max_step_norm=0.0, theta_max_norm=40.0)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
