@@ -226,6 +226,9 @@ struct R1Map {  // slot s = u * NU + q: vector index vi(u), uniform index q
     }
 };
 
+#ifndef EGG_UPD_GROUP
+#define EGG_UPD_GROUP 8  // base samples whose factor loads are in flight together
+#endif
 template <int KIND, int NU>
 __device__ __forceinline__ void update_chunk_r1(const float* __restrict__ theta, const float* __restrict__ factors,
                                                 int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
@@ -265,10 +268,10 @@ __device__ __forceinline__ void update_chunk_r1(const float* __restrict__ theta,
             const int ldb = (int)(ld_f * 4);  // host: 64 * ld_f * 4 < 2^31
             // groups of 8 base samples with a compile-time trip count (readlane is convergent: a
             // runtime-count loop around it cannot be unrolled), 8 * NV loads in flight per thread
-            for (int j0 = 0; j0 < n; j0 += 8) {
-                float x[8][NV];
+            for (int j0 = 0; j0 < n; j0 += EGG_UPD_GROUP) {
+                float x[EGG_UPD_GROUP][NV];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
+                for (int t = 0; t < EGG_UPD_GROUP; ++t) {
                     // buffer load: uniform row offset in soffset (SGPR), lane byte offset in voffset —
                     // one VGPR per slot column instead of a 64-bit address per (base, slot)
                     const int sb = (j0 + t) * ldb;
@@ -279,7 +282,7 @@ __device__ __forceinline__ void update_chunk_r1(const float* __restrict__ theta,
                                       : 0.0f;
                 }
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
+                for (int t = 0; t < EGG_UPD_GROUP; ++t) {
                     if (j0 + t >= n) break;
 #pragma unroll
                     for (int s = 0; s < 4; ++s) {
