@@ -108,3 +108,28 @@ def test_es_step_unified_signature(setup, dev, tmp_path):
     assert theta_after.shape == theta.shape and len(texts) == 4
     assert img_dict["best"] is not None and (tmp_path / "epoch_0000" / "best.png").exists()
     assert "summary/mean_reward" in stats and "prompt_3/mu_over_pop" in stats
+
+
+def test_caption_padding_trim_is_exact(setup, dev):
+    """Dropping caption columns that are padding for every image (SanaTransformer2DModel.forward) gives
+    the same transformer output as attending over all 300 tokens with the -10000 mask bias."""
+    be, _, _, _ = setup
+    tr = be.es_model.transformer
+    flat = be.step_sampling_info(1)["flat_ids"]
+    pe, am = be._gather(flat)
+    am = am.clone()
+    am[:, 200:] = 0                      # every prompt shorter than 200 tokens -> trim applies
+    am[:, 0] = 1
+    g = torch.Generator(device=dev).manual_seed(0)
+    B = pe.shape[0]
+    lat = torch.randn(B, tr.config.in_channels, 4, 4, generator=g, device=dev)
+    t = torch.full((B,), 0.9, device=dev)
+    gs = torch.full((B,), 4.5, device=dev)
+    with torch.no_grad():
+        tr.trim_caption_padding = True
+        a = tr(lat, t, pe, am, gs).float()
+        tr.trim_caption_padding = False
+        b = tr(lat, t, pe, am, gs).float()
+    assert torch.isfinite(a).all()
+    rel = ((a - b).norm() / b.norm()).item()
+    assert rel < 1e-2, rel               # flash tiling over fewer keys; zero-weight keys only
