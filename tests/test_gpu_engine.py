@@ -133,3 +133,24 @@ def test_caption_padding_trim_is_exact(setup, dev):
     assert torch.isfinite(a).all()
     rel = ((a - b).norm() / b.norm()).item()
     assert rel < 1e-2, rel               # flash tiling over fewer keys; zero-weight keys only
+
+
+def test_cross_attention_head_dim_padding_is_exact(dev):
+    """CrossAttention with the SDPA head dim zero-padded 112 -> 128 (scale 1/sqrt(112) explicit) equals
+    the unpadded SDPA: padded dims contribute exact zeros."""
+    from hyperscalees_t2i_amd.sana import CrossAttention
+    torch.manual_seed(0)
+    m = CrossAttention(256, 4, 112).to(dev)   # inner 448: GEMM K multiple of 64
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_((torch.randn_like(p, dtype=torch.float32) * 0.05).to(p.dtype))
+        x = torch.randn(3, 64, 256, device=dev).to(torch.bfloat16)
+        enc = torch.randn(3, 40, 256, device=dev).to(torch.bfloat16)
+        mb = torch.zeros(3, 1, 1, 40, device=dev, dtype=torch.bfloat16)
+        mb[1, ..., 17:] = -10000.0
+        m.pad_head_dim = True
+        a = m(x, enc, mb).float()
+        m.pad_head_dim = False
+        b = m(x, enc, mb).float()
+    assert torch.isfinite(a).all()
+    assert (a - b).abs().max().item() <= 1e-2 * b.abs().max().item()
