@@ -42,7 +42,10 @@ class ESBackend:
     def step_sampling_info(self, seed: int) -> Dict[str, Any]:
         raise NotImplementedError
 
-    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float) -> List[Any]:
+    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                      flat_seeds: Optional[List[int]] = None) -> List[Any]:
+        """es_backend.py:51-57: images for each flat_id in order; flat_seeds: optional per-image
+        deterministic seeds (same length as flat_ids)."""
         raise NotImplementedError
 
     def generate_population(self, flat_ids: List[int], seed: int, guidance_scale: float,
@@ -184,10 +187,20 @@ class SanaBackend(ESBackend):
         idx = torch.as_tensor(flat_ids, device=pe.device)
         return pe.index_select(0, idx), am.index_select(0, idx)
 
-    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float) -> List[Any]:
-        """es_backend.py:265-292: one member (the transformer's current LoRA params), PIL images."""
+    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                      flat_seeds: Optional[List[int]] = None) -> List[Any]:
+        """es_backend.py:265-292: one member (the transformer's current LoRA params), PIL images.
+        flat_seeds (es_backend.py:51-57): image i draws its latents from Generator(seed=flat_seeds[i])
+        instead of all images sharing one batched draw from `seed`."""
         pe, am = self._gather(flat_ids)
-        images, _ = self.es_model.generate(prompt_embeds=pe, prompt_attention_mask=am, latents=None, seed=seed,
+        latents = None
+        if flat_seeds is not None:
+            if len(flat_seeds) != len(flat_ids):
+                raise ValueError(f"flat_seeds has {len(flat_seeds)} entries, flat_ids {len(flat_ids)}")
+            m = self.es_model
+            latents = torch.cat([m._latents(1, int(s), self.cfg.height_latent, self.cfg.width_latent)
+                                 for s in flat_seeds])
+        images, _ = self.es_model.generate(prompt_embeds=pe, prompt_attention_mask=am, latents=latents, seed=seed,
                                            guidance_scale=guidance_scale, width_latent=self.cfg.width_latent,
                                            height_latent=self.cfg.height_latent)
         return images

@@ -468,7 +468,7 @@ __device__ __forceinline__ bool eq_nan(float a, float b) {
 }
 
 __global__ __launch_bounds__(1024) void k_fitness(const float* __restrict__ S, int n, int m, int promptnorm,
-                                                  float* __restrict__ scores, float* __restrict__ mu,
+                                                  float pn_eps, float* __restrict__ scores, float* __restrict__ mu,
                                                   float* __restrict__ stats, float* __restrict__ fit,
                                                   int32_t* __restrict__ finite, int32_t* __restrict__ order) {
 #pragma clang fp contract(off)
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(1024) void k_fitness(const float* __restrict__ S, i
             float ss = 0.0f;
             for (int k = 0; k < n; ++k) ss = ss + s_row[k];
             float sb = sqrtf(ss / (float)(n * m));
-            if (sb < 1e-8f) sb = 1e-8f;  // clamp_min keeps NaN
+            if (sb < pn_eps) sb = pn_eps;  // clamp_min(eps) keeps NaN
             s_misc[0] = sb;
         }
         __syncthreads();
@@ -693,7 +693,8 @@ __global__ __launch_bounds__(256) void k_update_finalize(const double* __restric
         double ss = step_on ? (double)max_step / (dn + 1e-8) : 1.0;
         const double n2 = step_on ? (tt + 2.0 * ss * td + ss * ss * dd) : oo;
         const double tn = sqrt(n2 > 0.0 ? n2 : 0.0);
-        int theta_on = (max_theta > 0.0f) && (tn > (double)max_theta);
+        // no finite member: the reference returns theta unchanged, caps included (unifed_es.py:237-240)
+        int theta_on = (nf > 0) && (max_theta > 0.0f) && (tn > (double)max_theta);
         sc->step_scale = ss;
         sc->theta_scale = theta_on ? (double)max_theta / (tn + 1e-8) : 1.0;
         sc->step_on = step_on;
@@ -778,11 +779,13 @@ int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int6
     return EGGROLL_OK;
 }
 
-int eggroll_fitness(const float* S, int32_t n, int32_t m, int32_t use_promptnorm, float* scores, float* mu,
-                    float* stats, float* fitness, int32_t* finite, int32_t* order, void* stream) {
+int eggroll_fitness(const float* S, int32_t n, int32_t m, int32_t use_promptnorm, float promptnorm_eps, float* scores,
+                    float* mu, float* stats, float* fitness, int32_t* finite, int32_t* order, void* stream) {
     EGG_CHECK_ARG(n >= 1 && n <= 4096 && m >= 1 && m <= 1024, "fitness: need 1<=n<=4096, 1<=m<=1024 (got %d,%d)", n, m);
     EGG_CHECK_ARG(S && scores && mu && stats && fitness && finite && order, "fitness: NULL pointer");
-    hipLaunchKernelGGL(k_fitness, dim3(1), dim3(1024), 0, as_stream(stream), S, n, m, use_promptnorm, scores, mu,
+    EGG_CHECK_ARG(!(promptnorm_eps < 0.0f), "fitness: promptnorm_eps must be >= 0");
+    hipLaunchKernelGGL(k_fitness, dim3(1), dim3(1024), 0, as_stream(stream), S, n, m, use_promptnorm, promptnorm_eps,
+                       scores, mu,
                        stats, fitness, finite, order);
     EGG_CHECK_LAUNCH("fitness");
     return EGGROLL_OK;

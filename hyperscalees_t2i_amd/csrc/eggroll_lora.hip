@@ -703,7 +703,7 @@ __device__ __forceinline__ void lora_mfma_addend(f32x4 (&acc)[8][4], int lane, i
     }
 }
 
-template <int R, bool MF, int DIAG = 0>
+template <int R, bool MF>
 __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
     const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
@@ -724,10 +724,6 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
     const int m0 = tm * 256, n0 = tn * 256;
 
-    if constexpr (DIAG == 2) {  // diagnostic: desynchronise the first round by half a tile on odd blocks
-        if (bid < 256 && (bid & 1))
-            for (int z = 0; z < 6; ++z) __builtin_amdgcn_s_sleep(127);
-    }
     const HalfStage sA0 = make_stage<true>(m0, M - 1, ldx, 0, wave, lane);
     const HalfStage sA1 = make_stage<true>(m0, M - 1, ldx, 1, wave, lane);
     const HalfStage sB0 = make_stage<false>(n0, N - 1, ldw, 0, wave, lane);
@@ -789,15 +785,6 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     P8_VM0();
     __syncthreads();  // every wave is past its last LDS read: the epilogue reuses the ring
 
-    if constexpr (DIAG == 1) {  // diagnostic: main loop only (acc kept live, one store per lane)
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-        if (sum == 1234.5f) Y[tid] = 1;
-        return;
-    }
     if constexpr (MF) {  // bias + LoRA term as one extra MFMA k-step, then a plain bf16 store
         lora_mfma_addend<R>(acc, lane, m0, n0, wm * 128, wn * 64, bias, T, theta_pop, ld_theta, offB, scale,
                             rows_per_member, M, N);
@@ -1076,15 +1063,11 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8f(
     store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, M, N, Y, ldy);
 }
 
-static int g_tile_override = 0;
-
 // The fused-projection kernel is opt-in (tile 12): measured at the Sana shapes it is 1-10 % SLOWER
 // than k_lora_project + k_lora_gemm8 (1.205 vs 1.189 ms at 131072x2240x2240, 5.82 vs 5.25 ms at
 // N = 11200) — the extra AK DMA and T-MFMA per K-tile cost more than the 10 % X re-read they save.
-static bool fused_ok(int32_t r, int64_t M, int64_t N, int64_t K, int64_t rows_per_member) {
-    (void)M;
-    (void)N;
-    return g_tile_override == 12 && (r == 1 || r == 2) && rows_per_member >= 256 && K % 64 == 0;
+static bool fused_ok(int tsel, int32_t r, int64_t K, int64_t rows_per_member) {
+    return tsel == 12 && (r == 1 || r == 2) && rows_per_member >= 256 && K % 64 == 0;
 }
 
 static int launch_gemm8f(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
@@ -1459,9 +1442,16 @@ int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta
     return EGGROLL_OK;
 }
 
-int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
-                      const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
-                      int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, void* stream) {
+// Kernel choice is a per-call argument (no process-global state: the C-ABI is thread-safe per
+// stream).  0 = automatic: the 8-phase 256x256 kernel when the grid still fills the chip, else the
+// 128x128 one-barrier tile.  8 / 9 = 8-phase with MFMA / VALU LoRA epilogue, 12 = as 8 with the
+// projection fused (linear_pop only), 128 / 256 = one-barrier tiles.
+static int lora_gemm_impl(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                          const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                          int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy,
+                          int32_t kernel, void* stream) {
+    EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 9 || kernel == 12 || kernel == 128 || kernel == 256,
+                  "lora_gemm: kernel must be 0 (auto), 8, 9, 12, 128 or 256 (got %d)", kernel);
     EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0, "lora_gemm: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
                   (long long)K);
     EGG_CHECK_ARG(K % 64 == 0, "lora_gemm: K=%lld must be a multiple of 64", (long long)K);
@@ -1473,33 +1463,14 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
     EGG_CHECK_ARG(X && W && Y, "lora_gemm: NULL pointer");
     EGG_CHECK_ARG(r == 0 || (T && theta_pop), "lora_gemm: T / theta_pop NULL with r > 0");
     hipStream_t st = as_stream(stream);
-    // tile choice: the 8-phase 256x256 kernel when the grid still fills the chip, else 128x128
-    const int tsel = g_tile_override ? g_tile_override : ((M / 256) * ((N + 255) / 256) >= 512 ? 8 : 128);
-    if (tsel == 10) {  // diagnostic: 8-phase main loop without epilogue (r ignored)
-        const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
-        hipLaunchKernelGGL((k_lora_gemm8<0, false, 1>), dim3((unsigned)(tiles_m * tiles_n)), dim3(512), 0, st,
-                           (const unsigned short*)X, ldx, (const unsigned short*)W, ldw, (const unsigned short*)bias,
-                           T, theta_pop, ld_theta, offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n,
-                           (unsigned short*)Y, ldy);
-        EGG_CHECK_LAUNCH("lora_gemm8_diag");
-        return EGGROLL_OK;
-    }
-    if (tsel == 11) {  // diagnostic: tile 9 with a desynchronised first round
-        const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
-        hipLaunchKernelGGL((k_lora_gemm8<0, false, 2>), dim3((unsigned)(tiles_m * tiles_n)), dim3(512), 0, st,
-                           (const unsigned short*)X, ldx, (const unsigned short*)W, ldw, (const unsigned short*)bias,
-                           T, theta_pop, ld_theta, offB, scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n,
-                           (unsigned short*)Y, ldy);
-        EGG_CHECK_LAUNCH("lora_gemm8_diag");
-        return EGGROLL_OK;
-    }
+    const int tsel = kernel ? kernel : ((M / 256) * ((N + 255) / 256) >= 512 ? 8 : 128);
     if (tsel == 8 || tsel == 9 || tsel == 12) {
         EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_gemm: operand > 2 GiB");
         const bool mf = tsel != 9 && r <= 2 && rows_per_member >= 256;
         return mf ? launch_gemm8<true>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
-                                              rows_per_member, M, N, K, Y, ldy, st)
-                         : launch_gemm8<false>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
-                                               rows_per_member, M, N, K, Y, ldy, st);
+                                       rows_per_member, M, N, K, Y, ldy, st)
+                  : launch_gemm8<false>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
+                                        rows_per_member, M, N, K, Y, ldy, st);
     }
     return tsel == 256 ? launch_gemm<kT256>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
                                             rows_per_member, M, N, K, Y, ldy, st)
@@ -1507,13 +1478,20 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
                                             rows_per_member, M, N, K, Y, ldy, st);
 }
 
-extern "C" int eggroll_lora_gemm_tile(int32_t tile) {
-    EGG_CHECK_ARG(tile == 0 || tile == 8 || tile == 9 || tile == 10 || tile == 11 || tile == 12 || tile == 128 ||
-                      tile == 256,
-                  "lora_gemm_tile: tile must be 0 (auto), 8 / 9 (8-phase 256x256 with MFMA / VALU LoRA "
-                  "epilogue), 12 (8-phase with the projection fused), 128 or 256");
-    g_tile_override = tile;
-    return EGGROLL_OK;
+int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                      const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                      int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, void* stream) {
+    return lora_gemm_impl(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
+                          ldy, 0, stream);
+}
+
+int eggroll_lora_gemm_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                          const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                          int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy,
+                          int32_t kernel, void* stream) {
+    EGG_CHECK_ARG(kernel != 12, "lora_gemm_sel: kernel 12 fuses the projection (eggroll_lora_linear_pop_sel only)");
+    return lora_gemm_impl(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
+                          ldy, kernel, stream);
 }
 
 int64_t eggroll_lora_workspace_bytes(int64_t M, int64_t K, int32_t r, int64_t rows_per_member) {
@@ -1524,14 +1502,16 @@ int64_t eggroll_lora_workspace_bytes(int64_t M, int64_t K, int32_t r, int64_t ro
     return t_bytes > ak_bytes ? t_bytes : ak_bytes;
 }
 
-int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
-                            const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
-                            float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
-                            int64_t ldy, float* T_ws, void* stream) {
+int eggroll_lora_linear_pop_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                                const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                                float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                                int64_t ldy, float* T_ws, int32_t kernel, void* stream) {
+    EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 9 || kernel == 12 || kernel == 128 || kernel == 256,
+                  "lora_linear_pop: kernel must be 0 (auto), 8, 9, 12, 128 or 256 (got %d)", kernel);
     EGG_CHECK_ARG(K > 0 && K % 64 == 0, "lora_linear_pop: K=%lld must be a multiple of 64", (long long)K);
     EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_linear_pop: r=%d out of range", r);
     if (M == 0) return EGGROLL_OK;
-    if (r > 0 && fused_ok(r, M, N, K, rows_per_member)) {  // projection fused into the 8-phase GEMM
+    if (r > 0 && fused_ok(kernel, r, K, rows_per_member)) {  // projection fused into the 8-phase GEMM
         EGG_CHECK_ARG(X && W && Y && theta_pop && T_ws, "lora_linear_pop: NULL pointer");
         EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop: bad strides");
         EGG_CHECK_ARG(ld_theta % 4 == 0 && offA % 4 == 0, "lora_linear_pop: theta offsets must be 16-byte aligned");
@@ -1543,8 +1523,16 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
         int rc = eggroll_lora_project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T_ws, stream);
         if (rc) return rc;
     }
-    return eggroll_lora_gemm(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K,
-                             Y, ldy, stream);
+    return lora_gemm_impl(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
+                          ldy, kernel == 12 ? 8 : kernel, stream);
+}
+
+int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                            const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                            float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                            int64_t ldy, float* T_ws, void* stream) {
+    return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
+                                       rows_per_member, M, N, K, Y, ldy, T_ws, 0, stream);
 }
 
 /* Implicit-GEMM ks x ks conv, pad 1 (k_conv3x3_gemm8): see include/eggroll.h */

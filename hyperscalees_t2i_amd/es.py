@@ -129,9 +129,7 @@ def paper_prompt_normalized_scores(S: torch.Tensor, eps: float = 1e-8):
     """utills.py:310-330: scores [n], mu_q [m], sigma_bar (scalar tensor)."""
     if S.ndim != 2:
         raise ValueError(f"S must be [n, m], got {tuple(S.shape)}")
-    if eps != 1e-8:
-        raise ValueError("kernel implements the reference default eps=1e-8 only")
-    out = K.fitness(S.float().contiguous(), promptnorm=True)
+    out = K.fitness(S.float().contiguous(), promptnorm=True, eps=float(eps))
     return out["scores"], out["mu"], out["stats"][0]
 
 
@@ -171,6 +169,26 @@ def sample_indices_unique(seed: int, total: int, k: int) -> List[int]:
         return list(range(total))
     idx = rng.choice(np.arange(total, dtype=np.int64), size=k, replace=False)
     return idx.tolist()
+
+
+def sample_classes_unique(seed: int, allowed_classes="all", classes_per_gen: int = 4,
+                          num_classes_total: int = 1000) -> List[int]:
+    """VarBackend._sample_classes_unique (es_backend.py:377-396): class ids for one epoch, drawn
+    without replacement by np.random.RandomState(seed).choice from the allowed pool."""
+    rng = np.random.RandomState(int(seed))
+    if allowed_classes is None or allowed_classes == "all":
+        pool = np.arange(num_classes_total, dtype=np.int64)
+    else:
+        pool = np.unique(np.array(list(allowed_classes), dtype=np.int64))
+        pool = pool[(pool >= 0) & (pool < num_classes_total)]
+        if pool.size == 0:
+            pool = np.arange(num_classes_total, dtype=np.int64)
+    m = int(classes_per_gen)
+    if m <= 0:
+        raise ValueError("classes_per_gen must be >= 1")
+    if m > pool.size:
+        raise ValueError(f"classes_per_gen ({m}) > pool size ({pool.size})")
+    return rng.choice(pool, size=m, replace=False).tolist()
 
 
 def repeat_batches(ids_unique: List[int], repeats: int) -> List[int]:

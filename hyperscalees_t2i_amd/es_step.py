@@ -25,7 +25,7 @@ import torch
 
 from . import kernels as K
 from .es import EggRollNoiser, unflatten_to_params
-from .rewards import RewardModels
+from .rewards import RewardModels, split_mix_weights
 
 
 # ---------------------------------------------------------------------------------------
@@ -93,6 +93,36 @@ def verify_theta_replicas(theta: torch.Tensor, info: DistInfo) -> None:
 
 
 # ---------------------------------------------------------------------------------------
+# S aggregation (unifed_es.py:165-215)
+# ---------------------------------------------------------------------------------------
+
+RAW_KEYS = ("combined", "clip_aesthetic", "clip_text", "no_artifacts", "pickscore")
+
+
+def aggregate_member_rewards(rew: Dict[str, torch.Tensor], flat_ids: List[int], pid_to_j: Dict[int, int],
+                             n_members: int, m: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-image rewards of n_members members (member-major, each member's images in flat_ids order)
+    -> S [n, m] with S[k, j] = mean over member k's images of unique prompt j, in flat order
+    (per_prompt_comb[pid_to_j[pid]] then torch.stack(...).mean(), unifed_es.py:175-209), and the
+    raw per-member means [n, 5] over ALL its images (unifed_es.py:211-215), columns RAW_KEYS.
+    The image -> prompt mapping comes from pid_to_j, not from an assumed repeat order."""
+    B = len(flat_ids)
+    comb = rew["combined"].float().view(n_members, B)
+    groups: List[List[int]] = [[] for _ in range(m)]
+    for idx, pid in enumerate(flat_ids):
+        groups[pid_to_j[int(pid)]].append(idx)
+    if any(not g for g in groups):
+        raise ValueError("every unique prompt needs at least one image (per_prompt_comb[j] empty)")
+    if len({len(g) for g in groups}) == 1:   # equal repeats (repeat_batches): one gather + mean
+        idx = torch.tensor(groups, device=comb.device)                        # [m, R]
+        S = comb[:, idx].mean(dim=-1)
+    else:                                    # ragged: one mean per prompt
+        S = torch.stack([comb[:, torch.tensor(g, device=comb.device)].mean(dim=-1) for g in groups], dim=1)
+    raw = torch.stack([rew[k].float().view(n_members, B).mean(dim=1) for k in RAW_KEYS], 1)
+    return S.contiguous(), raw
+
+
+# ---------------------------------------------------------------------------------------
 # engine
 # ---------------------------------------------------------------------------------------
 
@@ -112,6 +142,11 @@ class ESConfig:
 
 
 class ESEngine:
+    def log_imgs(self, info) -> int:
+        """unifed_es.py:132-135: logged images per member from the max_log_batches ARGUMENT."""
+        repeats = int(len(info["flat_ids"]) // max(1, info["m"]))
+        return int(max(0, min(int(self.cfg.max_log_batches), repeats))) * info["m"]
+
     def __init__(self, backend, rewards: RewardModels, noiser: EggRollNoiser, cfg: ESConfig, device,
                  dist_info: Optional[DistInfo] = None):
         self.backend, self.rewards, self.noiser, self.cfg = backend, rewards, noiser, cfg
@@ -142,11 +177,10 @@ class ESEngine:
         feats = self.rewards.prompt_features(info["unique_texts"])
         j_of_img = torch.tensor([info["pid_to_j"][p] for p in flat_ids], device=self.device).repeat(nl)
         rew = self.rewards.score(imgs, j_of_img, feats)
-        S_local = rew["combined"].view(nl, R, m).mean(dim=1)                            # unifed_es.py:208-209
-        raw_local = torch.stack([rew[k].view(nl, -1).mean(dim=1) for k in
-                                 ("combined", "clip_aesthetic", "clip_text", "no_artifacts", "pickscore")], 1)
+        S_local, raw_local = aggregate_member_rewards(rew, flat_ids, info["pid_to_j"], nl, m)
         if keep_images:
-            self.last_images = imgs.view(nl, len(flat_ids), *imgs.shape[1:])[:, : info["total_imgs_for_logging"]]
+            n_log = self.log_imgs(info)
+            self.last_images = imgs.view(nl, len(flat_ids), *imgs.shape[1:])[:, :n_log]
         mark("reward")
         return S_local, raw_local, factors, info
 
@@ -211,8 +245,8 @@ class ESEngine:
             "promptnorm/enabled": float(pn), "promptnorm/sigma_bar": float(h["stats"][0]) if pn else float("nan"),
             "epoch/seed": int(seed), "epoch/m_unique": int(m),
             "epoch/repeats": int(len(info["flat_ids"]) // max(1, m)),
-            "epoch/logged_repeats": int(info["log_batches"]),
-            "epoch/logged_imgs_per_indiv": int(info["total_imgs_for_logging"]),
+            "epoch/logged_repeats": int(self.log_imgs(info) // max(1, m)),
+            "epoch/logged_imgs_per_indiv": int(self.log_imgs(info)),
             "epoch/total_imgs_per_indiv": int(info["total_imgs_per_indiv"]),
         })
         for j in range(m):
@@ -235,11 +269,12 @@ def es_step_unified(*, theta, backend, lora_params, lora_shapes, clip_model, cli
     Returns (theta_after, stats, img_dict, rewards_for_hist, unique_texts)."""
     if not isinstance(clip_model, RewardModels):
         raise TypeError("clip_model must be a hyperscalees_t2i_amd.rewards.RewardModels")
+    split_mix_weights(mix_weights)           # rewards.py:247-253: length 3 or 4, else ValueError
     clip_model.mix_weights = tuple(mix_weights)
     cfg = ESConfig(pop_size=pop_size, sigma=noiser.sigma, lr_scale=noiser.lr_scale, egg_rank=noiser.rank,
                    use_antithetic=noiser.use_antithetic, promptnorm=promptnorm_enabled, theta_max_norm=theta_max_norm,
                    max_step_norm=max_step_norm, max_log_batches=max_log_batches)
-    key = (pop_size, id(noiser), promptnorm_enabled, theta_max_norm, max_step_norm)
+    key = (pop_size, id(noiser), promptnorm_enabled, theta_max_norm, max_step_norm, max_log_batches)
     eng = getattr(backend, "_es_engine", None)
     if eng is None or getattr(backend, "_es_engine_key", None) != key:
         eng = ESEngine(backend, clip_model, noiser, cfg, theta.device, dist_info)

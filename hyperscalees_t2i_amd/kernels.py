@@ -143,8 +143,9 @@ def perturb(theta: Optional[torch.Tensor], factors: torch.Tensor, layout: ThetaL
 # ---------------------------------------------------------------------------------------
 
 
-def fitness(S: torch.Tensor, promptnorm: bool) -> Dict[str, torch.Tensor]:
-    """scores/mu/stats/fitness/finite/order of S [n, m] (see include/eggroll.h)."""
+def fitness(S: torch.Tensor, promptnorm: bool, eps: float = 1e-8) -> Dict[str, torch.Tensor]:
+    """scores/mu/stats/fitness/finite/order of S [n, m] (see include/eggroll.h); eps = the
+    promptnorm sigma_bar clamp (utills.py:310)."""
     _dev(S, "fitness(S)", torch.float32)
     if S.ndim != 2:
         raise ValueError(f"S must be [n, m], got {tuple(S.shape)}")
@@ -158,7 +159,7 @@ def fitness(S: torch.Tensor, promptnorm: bool) -> Dict[str, torch.Tensor]:
         "finite": torch.empty(n, dtype=torch.int32, device=dev),
         "order": torch.empty(n, dtype=torch.int32, device=dev),
     }
-    _lib.call("eggroll_fitness", S.data_ptr(), n, m, int(bool(promptnorm)), out["scores"].data_ptr(),
+    _lib.call("eggroll_fitness", S.data_ptr(), n, m, int(bool(promptnorm)), float(eps), out["scores"].data_ptr(),
               out["mu"].data_ptr(), out["stats"].data_ptr(), out["fitness"].data_ptr(), out["finite"].data_ptr(),
               out["order"].data_ptr(), _stream(dev))
     return out
@@ -201,11 +202,13 @@ def update(theta: torch.Tensor, factors: torch.Tensor, fit: Dict[str, torch.Tens
 
 def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], theta_pop: Optional[torch.Tensor],
                     offA: int, offB: int, r: int, scale: float, rows_per_member: int,
-                    out: Optional[torch.Tensor] = None, T_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    out: Optional[torch.Tensor] = None, T_ws: Optional[torch.Tensor] = None,
+                    kernel: int = 0) -> torch.Tensor:
     """Y = x W^T + bias + scale * (x A_k^T) B_k^T with member k = row // rows_per_member.
 
     x: [M, K] bf16; W: [N, K] bf16; bias: [N] bf16 or None; theta_pop: [n_members, ld] fp32.
-    r = 0 runs the plain base GEMM (no LoRA term)."""
+    r = 0 runs the plain base GEMM (no LoRA term).  kernel: 0 = automatic choice, else an explicit
+    kernel for A/B measurement (eggroll_lora_linear_pop_sel)."""
     _dev(x, "lora_linear_pop(x)", torch.bfloat16)
     _dev(W, "lora_linear_pop(W)", torch.bfloat16)
     M, K = x.shape
@@ -227,9 +230,9 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
         ld_t = theta_pop.stride(0)
     else:
         ld_t = 0
-    _lib.call("eggroll_lora_linear_pop", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
+    _lib.call("eggroll_lora_linear_pop_sel", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
               _p(theta_pop) if r > 0 else None, ld_t, offA, offB, r, float(scale), rows_per_member, M, N, K,
-              out.data_ptr(), out.stride(0), _p(T_ws) if r > 0 else None, _stream(x.device))
+              out.data_ptr(), out.stride(0), _p(T_ws) if r > 0 else None, int(kernel), _stream(x.device))
     return out
 
 
@@ -239,16 +242,16 @@ def lora_workspace_numel(M: int, K: int, r: int, rows_per_member: int) -> int:
     return max(1, -(-nbytes // 4))
 
 
-def lora_fused(M: int, N: int, K: int, r: int, rows_per_member: int, tile: int = 0) -> bool:
-    """True when eggroll_lora_linear_pop runs the projection inside the 8-phase GEMM (mirrors
-    fused_ok in eggroll_lora.hip): only with kernel 12 forced — the automatic choice is the
-    two-pass k_lora_project + k_lora_gemm8, which measured faster at every Sana shape."""
-    return tile == 12 and r in (1, 2) and rows_per_member >= 256 and K % 64 == 0
+def lora_fused(M: int, N: int, K: int, r: int, rows_per_member: int, kernel: int = 0) -> bool:
+    """True when eggroll_lora_linear_pop_sel runs the projection inside the 8-phase GEMM (mirrors
+    fused_ok in eggroll_lora.hip): only with kernel 12 — the automatic choice is the two-pass
+    k_lora_project + k_lora_gemm8, which measured faster at every Sana shape."""
+    return kernel == 12 and r in (1, 2) and rows_per_member >= 256 and K % 64 == 0
 
 
 def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T: Optional[torch.Tensor],
               theta_pop: Optional[torch.Tensor], offB: int, r: int, scale: float, rows_per_member: int,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
     """The MFMA GEMM + fused LoRA epilogue alone, given T = X A_k^T (from lora_project)."""
     _dev(x, "lora_gemm(x)", torch.bfloat16)
     _dev(W, "lora_gemm(W)", torch.bfloat16)
@@ -257,9 +260,9 @@ def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T:
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
     ld_t = theta_pop.stride(0) if (r > 0 and theta_pop is not None) else 0
-    _lib.call("eggroll_lora_gemm", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
+    _lib.call("eggroll_lora_gemm_sel", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
               _p(T) if r > 0 else None, _p(theta_pop) if r > 0 else None, ld_t, offB, r, float(scale),
-              rows_per_member, M, N, K, out.data_ptr(), out.stride(0), _stream(x.device))
+              rows_per_member, M, N, K, out.data_ptr(), out.stride(0), int(kernel), _stream(x.device))
     return out
 
 

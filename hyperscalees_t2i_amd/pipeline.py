@@ -82,10 +82,14 @@ class SanaOneStep(ESBaseModel):
         eps = self.transformer(rep(lmi.float()), rep(scm.float()), rep(prompt_embeds), rep(prompt_attention_mask),
                                rep(guidance.float()))
         eps = torch.nan_to_num(eps.float(), nan=0.0, posinf=0.0, neginf=0.0)
-        lmi_r, se_r, lat_r = rep(lmi.float()), rep(se), rep(latents.float())
+        # dtype semantics of models/SanaSprint.py:138-153: eps rounded to the latent dtype (fp16) before
+        # the SCM combine, which promotes to fp32 through the fp32 scm tensor; 0.267 * latents is an fp16
+        # product (python scalar x fp16 tensor) before the fp32 subtraction
+        eps = eps.to(self.DTYPE)
+        lmi_r, se_r = rep(lmi), rep(se)
         pred = ((1 - 2 * se_r) * lmi_r + (1 - 2 * se_r + 2 * se_r ** 2) * eps) / torch.sqrt(se_r ** 2 + (1 - se_r) ** 2)
-        pred = pred * self.sigma_data
-        x0 = (0.267 * lat_r - 0.964 * pred) / self.sigma_data
+        pred = pred.float() * self.sigma_data
+        x0 = (rep(0.267 * latents) - 0.964 * pred) / self.sigma_data
         z = x0 / self.vae.scaling_factor
         imgs = [self.vae(z[s:s + self.vae_chunk]) for s in range(0, z.shape[0], self.vae_chunk)]
         return torch.cat(imgs), z

@@ -102,15 +102,26 @@ def _text_features(model, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor
     return model.text_projection(out.pooler_output).float()
 
 
+def split_mix_weights(mix_weights) -> Tuple[float, float, float, float]:
+    """rewards.py:247-253: (w_aes, w_align, w_noart) with w_pick = 0, or all four; else ValueError."""
+    w = tuple(float(x) for x in mix_weights)
+    if len(w) == 3:
+        return w + (0.0,)
+    if len(w) == 4:
+        return w
+    raise ValueError(f"mix_weights must have length 3 or 4, got {len(w)}")
+
+
 @dataclass
 class RewardModels:
     clip: object
     pick: object
-    mix_weights: Tuple[float, float, float, float] = (0.0, 0.0, 0.0, 1.0)  # unifed_es.py:360-363 defaults
+    mix_weights: Tuple[float, ...] = (0.0, 0.0, 0.0, 1.0)  # unifed_es.py:360-363 defaults (length 3 or 4)
     image_batch: int = 64
 
     @classmethod
     def build(cls, device, mix_weights=(0.0, 0.0, 0.0, 1.0), tiny: bool = False, seed: int = 7):
+        split_mix_weights(mix_weights)
         clip = build_clip(CLIP_TINY if tiny else CLIP_B32, device, seed)
         pick = build_clip(CLIP_TINY if tiny else CLIP_H14, device, seed + 1)
         return cls(clip=clip, pick=pick, mix_weights=tuple(mix_weights))
@@ -147,6 +158,6 @@ class RewardModels:
         neg = (ic @ feats["clip_neg"] + 1.0) / 2.0
         noart = 1.0 - neg
         pick = self.pick.logit_scale.float().exp() * (ip * feats["pick_prompt"][prompt_index]).sum(-1)
-        w_aes, w_txt, w_no, w_pick = self.mix_weights
+        w_aes, w_txt, w_no, w_pick = split_mix_weights(self.mix_weights)
         comb = w_aes * aes + w_txt * txt + w_no * noart + w_pick * pick
         return {"clip_aesthetic": aes, "clip_text": txt, "no_artifacts": noart, "pickscore": pick, "combined": comb}

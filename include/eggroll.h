@@ -11,6 +11,8 @@
  *   - every pointer is a caller-allocated DEVICE pointer unless the name ends in `_host`;
  *   - work is stream-ordered on `stream` (a hipStream_t, NULL = default stream);
  *   - no internal allocation, no host synchronisation (graph-capturable);
+ *   - no process-global mutable state (kernel choices are per-call arguments): calls on
+ *     different threads / streams are independent (thread-safe per stream);
  *   - return 0 on success, negative on error; eggroll_last_error() gives a message
  *     (thread-local);
  *   - deterministic: identical inputs give bit-identical outputs, independent of which
@@ -85,14 +87,15 @@ int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int6
 /* (3) Fitness — replaces paper_prompt_normalized_scores (utills.py:310-330) or
  * S.mean(dim=1) (unifed_es.py:234), the finite mask (unifed_es.py:236-240,266),
  * standardize_fitness (utills.py:168-178) and the rank sort (unifed_es.py:244).
- * S: [n, m] fp32 row-major.  Outputs (device):
+ * S: [n, m] fp32 row-major; promptnorm_eps = the `eps` of paper_prompt_normalized_scores
+ * (sigma_bar.clamp_min(eps), reference default 1e-8).  Outputs (device):
  *   scores[n], mu[m] (promptnorm column means; S column means otherwise),
  *   stats[4] = {sigma_bar (NaN if promptnorm off), n_finite, mean_f, std_f},
  *   fitness[n] (z-scored over finite members; 0 for non-finite members),
  *   finite[n] (0/1), order[n] = stable ascending argsort of scores (NaN last).
  * Single workgroup; n <= 4096, m <= 1024.                                                 */
 int eggroll_fitness(const float* S, int32_t n, int32_t m, int32_t use_promptnorm,
-                    float* scores, float* mu, float* stats, float* fitness, int32_t* finite,
+                    float promptnorm_eps, float* scores, float* mu, float* stats, float* fitness, int32_t* finite,
                     int32_t* order, void* stream);
 
 /* (4) Update — replaces EggRollNoiser.do_update (utills.py:115-136) followed by
@@ -138,13 +141,20 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
                       const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
                       int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
                       int64_t K, void* Y, int64_t ldy, void* stream);
-/* Kernel selection of the LoRA GEMM for A/B measurement: 0 = automatic (8-phase 256x256 when the
- * grid fills the chip, else 128x128); 8 = 8-phase with MFMA epilogue, 9 = 8-phase with VALU
- * epilogue, 12 = as 8 plus the projection fused into the GEMM in eggroll_lora_linear_pop (opt-in:
- * slower than the two-pass path at the Sana shapes), 128 / 256 = one-barrier tiles;
- * 10 / 11 are diagnostics (main loop only; desynchronised first round) that write garbage.
- * Process-global; not thread-safe.                                                         */
-int eggroll_lora_gemm_tile(int32_t tile);
+/* The same two entry points with an explicit kernel choice (per call; no global state), for A/B
+ * measurement: 0 = automatic (as above: the 8-phase 256x256 kernel when the grid fills the chip,
+ * else 128x128); 8 = 8-phase with the MFMA LoRA epilogue, 9 = 8-phase with a VALU epilogue,
+ * 128 / 256 = one-barrier tiles; linear_pop_sel also takes 12 = 8-phase with the projection fused
+ * into the GEMM (opt-in: slower than the two-pass path at the Sana shapes).                     */
+int eggroll_lora_gemm_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                          const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
+                          int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
+                          int64_t K, void* Y, int64_t ldy, int32_t kernel, void* stream);
+int eggroll_lora_linear_pop_sel(const void* X, int64_t ldx, const void* W, int64_t ldw,
+                                const void* bias, const float* theta_pop, int64_t ld_theta,
+                                int64_t offA, int64_t offB, int32_t r, float scale,
+                                int64_t rows_per_member, int64_t M, int64_t N, int64_t K,
+                                void* Y, int64_t ldy, float* T_ws, int32_t kernel, void* stream);
 int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
                          int64_t offA, int32_t r, int64_t rows_per_member, int64_t M, int64_t K,
                          float* T, void* stream);

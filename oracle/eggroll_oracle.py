@@ -250,7 +250,7 @@ def ref_standardize(r: np.ndarray) -> np.ndarray:
     return ((r - mean) / (std + F32(1e-8))).astype(F32)
 
 
-def dev_fitness(S: np.ndarray, promptnorm: bool):
+def dev_fitness(S: np.ndarray, promptnorm: bool, eps: float = 1e-8):
     """Kernel k_fitness restated in its exact sequential fp32 op order."""
     S = np.asarray(S, F32)
     n, m = S.shape
@@ -272,8 +272,8 @@ def dev_fitness(S: np.ndarray, promptnorm: bool):
                     acc = F32(acc + F32(c * c))
                 ss = F32(ss + acc)
             sb = F32(np.sqrt(F32(ss / F32(n * m))))
-            if sb < F32(1e-8):
-                sb = F32(1e-8)
+            if sb < F32(eps):
+                sb = F32(eps)
             sigma_bar = sb
             for k in range(n):
                 acc = F32(0)

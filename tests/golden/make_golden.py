@@ -186,6 +186,104 @@ def gen_indices(u):
     return len(recs)
 
 
+def ref_step_sampling_info(u, seed, P, prompts_per_gen, batches_per_gen, max_log_batches, prompts_list=None):
+    """SanaBackend.step_sampling_info (es_backend.py:234-263) composed from the reference's own
+    utills functions exactly as that method does (es_backend.py itself needs diffusers/peft)."""
+    unique_ids = u.sample_indices_unique(seed=seed, total=P, k=prompts_per_gen)
+    flat_ids = u.repeat_batches(unique_ids, repeats=batches_per_gen)
+    pid_to_j = {pid: j for j, pid in enumerate(unique_ids)}
+    m = len(unique_ids)
+    unique_texts = [prompts_list[pid] if prompts_list is not None else f"prompt_{pid}" for pid in unique_ids]
+    flat_texts = [(prompts_list[pid] if prompts_list is not None else f"prompt_{pid}") for pid in flat_ids]
+    log_batches = int(max(0, min(max_log_batches, batches_per_gen)))
+    return dict(unique_ids=unique_ids, flat_ids=flat_ids, unique_texts=unique_texts, flat_texts=flat_texts,
+                pid_to_j=pid_to_j, m=m, total_imgs_per_indiv=len(flat_ids),
+                total_imgs_for_logging=log_batches * m, log_batches=log_batches)
+
+
+def ref_var_classes(seed, allowed, classes_per_gen, num_classes_total=1000):
+    """VarBackend._sample_classes_unique (es_backend.py:377-396), restated line by line (the method
+    lives on a class whose module needs peft; the arithmetic is numpy only)."""
+    rng = np.random.RandomState(int(seed))
+    if allowed is None or allowed == "all":
+        pool = np.arange(num_classes_total, dtype=np.int64)
+    else:
+        pool = np.array(list(allowed), dtype=np.int64)
+        pool = np.unique(pool)
+        pool = pool[(pool >= 0) & (pool < num_classes_total)]
+        if pool.size == 0:
+            pool = np.arange(num_classes_total, dtype=np.int64)
+    m = int(classes_per_gen)
+    return rng.choice(pool, size=m, replace=False).tolist()
+
+
+def gen_sampling_info(u):
+    """g5b: the reference step_sampling_info dict for seeds 0-99 (P in {4, 1631}) and the VAR class
+    sampler; integer fields as arrays, pid_to_j as (pid, j) pairs, texts joined with '\x1f'."""
+    recs = {}
+    for P in (4, 1631):
+        for k in (1, 2, 4):
+            for R in (1, 4):
+                for mlb in (0, 1, 2, 5):
+                    prompts = [f"prompt text {i}" for i in range(P)] if (P == 4 and mlb == 1) else None
+                    rows = {f: [] for f in ("unique_ids", "flat_ids", "pid_to_j", "scalars", "texts")}
+                    for seed in range(100):
+                        d = ref_step_sampling_info(u, seed, P, k, R, mlb, prompts)
+                        rows["unique_ids"].append(d["unique_ids"])
+                        rows["flat_ids"].append(d["flat_ids"])
+                        rows["pid_to_j"].append(sorted(d["pid_to_j"].items()))
+                        rows["scalars"].append([d["m"], d["total_imgs_per_indiv"], d["total_imgs_for_logging"],
+                                                d["log_batches"]])
+                        rows["texts"].append("\x1f".join(d["unique_texts"] + d["flat_texts"]))
+                    key = f"P{P}_k{k}_R{R}_L{mlb}" + ("_named" if prompts else "")
+                    for f in ("unique_ids", "flat_ids", "pid_to_j", "scalars"):
+                        recs[f"{key}/{f}"] = np.array(rows[f], np.int64)
+                    recs[f"{key}/texts"] = np.array(rows["texts"])
+    for allowed, tag in ((None, "all"), ([3, 3, 17, 999, 1000, -1, 42, 7, 17, 500], "list")):
+        for mcls in (1, 4):
+            recs[f"var_{tag}_m{mcls}"] = np.array([ref_var_classes(s, allowed, mcls) for s in range(100)], np.int64)
+    np.savez_compressed(OUT / "g5b_sampling_info.npz", **recs)
+    return len(recs)
+
+
+def gen_s_aggregation():
+    """g9: unifed_es.py:165-215 restated literally (per-image loop, per_prompt_comb lists,
+    torch.stack(...).mean()) on seeded per-image rewards, for repeat orders the reference produces and
+    for a shuffled flat order (pid_to_j does the grouping, not the position)."""
+    recs = {}
+    g = torch.Generator().manual_seed(31)
+    cases = {"m4_R4": ([5, 2, 9, 0] * 4), "m2_R3": ([1, 0] * 3), "m3_R1": [2, 0, 1],
+             "shuffled": [3, 1, 3, 2, 1, 2, 3, 1, 2], "ragged": [4, 4, 4, 8, 8]}
+    for name, flat_ids in cases.items():
+        unique = list(dict.fromkeys(flat_ids))
+        pid_to_j = {pid: j for j, pid in enumerate(unique)}
+        m, pop, B = len(unique), 3, len(flat_ids)
+        rew = {k: torch.randn(pop, B, generator=g) * 2 + 20 for k in
+               ("combined", "clip_aesthetic", "clip_text", "no_artifacts", "pickscore")}
+        S = torch.empty((pop, m))
+        raw = torch.empty((pop, 5))
+        for k in range(pop):
+            per_prompt = [[] for _ in range(m)]
+            alls = {key: [] for key in rew}
+            for idx in range(B):
+                j = pid_to_j[int(flat_ids[idx])]
+                per_prompt[j].append(rew["combined"][k, idx].float())
+                for key in rew:
+                    alls[key].append(rew[key][k, idx].float())
+            for j in range(m):
+                S[k, j] = torch.stack(per_prompt[j]).mean()
+            for c, key in enumerate(("combined", "clip_aesthetic", "clip_text", "no_artifacts", "pickscore")):
+                raw[k, c] = torch.stack(alls[key]).mean()
+        recs[f"{name}/flat_ids"] = np.array(flat_ids, np.int64)
+        recs[f"{name}/unique_ids"] = np.array(unique, np.int64)
+        for key, v in rew.items():
+            recs[f"{name}/rew_{key}"] = v.numpy()
+        recs[f"{name}/S"] = S.numpy()
+        recs[f"{name}/raw"] = raw.numpy()
+    np.savez_compressed(OUT / "g9_s_aggregation.npz", **recs)
+    return len(recs)
+
+
 def gen_es_tail(u):
     """unifed_es.py:227-281 composed from the reference's own functions (unifed_es.py itself does
     not import here: wandb / lovely_tensors / peft are absent)."""
@@ -249,5 +347,6 @@ def gen_lora(u):
 if __name__ == "__main__":
     u = load_reference()
     torch.set_num_threads(1)
-    for fn in (gen_eps, gen_fitness, gen_update, gen_indices, gen_es_tail, gen_lora):
+    for fn in (gen_eps, gen_fitness, gen_update, gen_indices, gen_sampling_info, gen_es_tail, gen_lora):
         print(fn.__name__, fn(u))
+    print("gen_s_aggregation", gen_s_aggregation())

@@ -36,13 +36,19 @@ def test_header_compiles_as_c():
 
 def test_argument_errors_are_reported():
     lib = _lib.load()
-    rc = lib.eggroll_fitness(None, 0, 4, 1, None, None, None, None, None, None, None)
+    rc = lib.eggroll_fitness(None, 0, 4, 1, 1e-8, None, None, None, None, None, None, None)
     assert rc == -1 and b"fitness" in lib.eggroll_last_error()
     rc = lib.eggroll_noise_factors(0, 0, 2, 10, 9, None, None)  # ld not multiple of 4
     assert rc == -1 and b"ld" in lib.eggroll_last_error()
     rc = lib.eggroll_lora_linear_pop(None, 64, None, 64, None, None, 0, 0, 0, 2, 1.0, 10, 10, 10, 60, None, 10,
                                      None, None)  # K % 64 != 0
     assert rc == -1 and b"multiple of 64" in lib.eggroll_last_error()
+    rc = lib.eggroll_lora_linear_pop_sel(None, 64, None, 64, None, None, 0, 0, 0, 2, 1.0, 10, 10, 10, 64, None, 10,
+                                         None, 10, None)  # kernel 10: the old diagnostic modes are gone
+    assert rc == -1 and b"kernel" in lib.eggroll_last_error()
+    rc = lib.eggroll_lora_gemm_sel(None, 64, None, 64, None, None, None, 0, 0, 2, 1.0, 10, 10, 10, 64, None, 10, 12,
+                                   None)  # kernel 12 (fused projection) exists only in linear_pop_sel
+    assert rc == -1 and b"12" in lib.eggroll_last_error()
     with pytest.raises(_lib.EggrollError):
         _lib.check(-1, "probe")
 

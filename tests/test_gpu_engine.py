@@ -153,4 +153,59 @@ def test_cross_attention_head_dim_padding_is_exact(dev):
         m.pad_head_dim = False
         b = m(x, enc, mb).float()
     assert torch.isfinite(a).all()
-    assert (a - b).abs().max().item() <= 1e-2 * b.abs().max().item()
+    # the padded head dims add exact zeros to every q.k dot product and to the zero-padded v columns;
+    # SDPA is free to pick another tiling for head dim 128 than for 112, so the claim pinned here is
+    # bit-identity on this stack (gfx950, torch 2.10 ROCm) — measured, not assumed
+    assert torch.equal(a, b), float((a - b).abs().max())
+
+
+def test_latents_match_reference_expression(setup, dev):
+    """models/SanaSprint.py:83-93: randn(b, 32, H, W, Generator(device).manual_seed(seed), fp16) * 0.5,
+    bitwise, for every seed the epoch loop uses (seed = epoch, unifed_es.py:766)."""
+    be = setup[0]
+    for seed in (0, 1, 17, 349):
+        got = be.es_model._latents(16, seed, 4, 4)
+        g = torch.Generator(device=dev).manual_seed(seed)
+        ref = torch.randn(16, 32, 4, 4, device=dev, dtype=torch.float16, generator=g) * 0.5
+        assert got.dtype == torch.float16 and torch.equal(got, ref), seed
+
+
+def test_members_share_latents_and_prompts(setup, dev):
+    """Common random numbers (unifed_es.py:120-124,163): identical theta_k rows give bit-identical
+    member outputs in one population batch — same latents, same prompts, no cross-member leakage."""
+    be, params, shapes, _ = setup
+    theta0 = flatten_params(params).to(dev)
+    tp = theta0[None].repeat(3, 1).contiguous()
+    flat = be.step_sampling_info(2)["flat_ids"]
+    imgs = be.generate_population(flat, 2, 4.5, tp)
+    B = len(flat)
+    assert torch.equal(imgs[:B], imgs[B:2 * B]) and torch.equal(imgs[:B], imgs[2 * B:])
+
+
+def test_s_aggregation_on_device_matches_reference_loop(dev, golden):
+    """es_step.aggregate_member_rewards on device tensors vs the reference per-image loop
+    (unifed_es.py:175-215) run literally on the same device tensors: bit-exact; and vs the g9 CPU
+    fixture within fp32 rounding of a device reduction."""
+    from hyperscalees_t2i_amd.es_step import RAW_KEYS, aggregate_member_rewards
+    npz = golden("g9_s_aggregation.npz")
+    names = sorted({k.split("/")[0] for k in npz.files})
+    for name in names:
+        d = {k.split("/", 1)[1]: npz[k] for k in npz.files if k.startswith(name + "/")}
+        flat, unique = d["flat_ids"].tolist(), d["unique_ids"].tolist()
+        pid_to_j = {p: j for j, p in enumerate(unique)}
+        pop, m, B = d["S"].shape[0], len(unique), len(flat)
+        rew = {k: torch.from_numpy(d[f"rew_{k}"]).to(dev) for k in RAW_KEYS}
+        S, raw = aggregate_member_rewards({k: v.reshape(-1) for k, v in rew.items()}, flat, pid_to_j, pop, m)
+        S_lit = torch.empty((pop, m), device=dev)
+        raw_lit = torch.empty((pop, 5), device=dev)
+        for k in range(pop):
+            per = [[] for _ in range(m)]
+            for idx in range(B):
+                per[pid_to_j[flat[idx]]].append(rew["combined"][k, idx])
+            for j in range(m):
+                S_lit[k, j] = torch.stack(per[j]).mean()
+            for c, key in enumerate(RAW_KEYS):
+                raw_lit[k, c] = torch.stack([rew[key][k, i] for i in range(B)]).mean()
+        assert torch.equal(S, S_lit), name
+        assert torch.equal(raw, raw_lit), name
+        np.testing.assert_allclose(S.cpu().numpy(), d["S"], rtol=3e-7, err_msg=name)

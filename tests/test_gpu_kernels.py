@@ -174,10 +174,13 @@ def test_update_nonfinite_members(dev):
     theta = torch.randn(n.num_params, device=dev)
     S = torch.randn(pop, 4, device=dev) + 3
     S[2, 1] = float("nan")
-    # promptnorm: one NaN poisons all -> theta unchanged (unifed_es.py:237-240)
+    # promptnorm: one NaN poisons all -> theta unchanged (unifed_es.py:237-240), caps included: a theta
+    # whose norm is above theta_max_norm must come back untouched on this early-return path
     fit = K.fitness(S, True)
     assert fit["stats"][1].item() == 0
     assert torch.equal(n.update_from_factors(theta, fac, fit, pop, 0.0, 40.0), theta)
+    big = theta * (100.0 / theta.norm())
+    assert torch.equal(n.update_from_factors(big, fac, fit, pop, 1e-6, 40.0), big)
     # mean scoring: member 2 dropped, N_f = 7
     fit = K.fitness(S, False)
     out = n.update_from_factors(theta, fac, fit, pop, 0.0, 0.0)
@@ -215,10 +218,7 @@ def _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm):
 @pytest.fixture(params=[128, 256, 8, 9, 12],
                 ids=["tile128", "tile256", "tile8phase_mfma", "tile8phase_valu", "tile8phase_fused_proj"])
 def gemm_tile(request):
-    from hyperscalees_t2i_amd import _lib
-    _lib.call("eggroll_lora_gemm_tile", request.param)
-    yield request.param
-    _lib.call("eggroll_lora_gemm_tile", 0)
+    return request.param
 
 
 @pytest.mark.parametrize("M,N,Kd,r,rpm", [
@@ -232,7 +232,7 @@ def gemm_tile(request):
 def test_lora_linear_pop_vs_fp64(dev, gemm_tile, M, N, Kd, r, rpm):
     x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm)
     scale = 8.0 / r
-    y = K.lora_linear_pop(x, W, b, tp, offA, offB, r, scale, rpm)
+    y = K.lora_linear_pop(x, W, b, tp, offA, offB, r, scale, rpm, kernel=gemm_tile)
     torch.cuda.synchronize()
     ref = _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm)
     got = y.float().cpu().numpy()
@@ -243,7 +243,7 @@ def test_lora_linear_pop_vs_fp64(dev, gemm_tile, M, N, Kd, r, rpm):
 
 def test_lora_linear_no_lora_matches_torch_matmul(dev, gemm_tile):
     x, W, b, tp, *_ = _lora_case(dev, 640, 384, 512, 2, 640)
-    y = K.lora_linear_pop(x, W, b, None, 0, 0, 0, 0.0, 640)
+    y = K.lora_linear_pop(x, W, b, None, 0, 0, 0, 0.0, 640, kernel=gemm_tile)
     ref = torch.nn.functional.linear(x.float(), W.float(), b.float())
     assert torch.allclose(y.float(), ref, rtol=1e-2, atol=2e-2)
 
@@ -265,7 +265,7 @@ def test_lora_linear_sana_shape_sampled_rows(dev, gemm_tile):
     """Full Sana attention shape (K = N = 2240) at 2 members x 16384 rows; rows sampled vs fp64."""
     M, N, Kd, r, rpm = 2 * 16384, 2240, 2240, 2, 16384
     x, W, b, tp, offA, offB = _lora_case(dev, M, N, Kd, r, rpm)
-    y = K.lora_linear_pop(x, W, b, tp, offA, offB, r, 4.0, rpm)
+    y = K.lora_linear_pop(x, W, b, tp, offA, offB, r, 4.0, rpm, kernel=gemm_tile)
     rows = torch.tensor([0, 1, 127, 128, 5000, 16383, 16384, 16385, 30000, M - 1])
     ref = _lora_ref(x[rows.to(dev)], W, b, tp, offA, offB, r, 4.0, rpm)
     # recompute reference rows with the right member per row

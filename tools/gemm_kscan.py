@@ -14,7 +14,6 @@ from tools.gemm_probe_util import bench  # noqa: E402
 tile = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 dev = torch.device("cuda:0")
 M, N, rpm = 131072, 2240, 16384
-_lib.call("eggroll_lora_gemm_tile", tile)
 res = {}
 bufs = {}
 for Kd in (1152, 2240, 4608):
@@ -27,7 +26,7 @@ for _ in range(3):
     for Kd, (x, W, b, tp, y, T) in bufs.items():
         for r in (0, 2):
             res.setdefault((Kd, r), []).append(
-                bench(lambda: K.lora_gemm(x, W, b, T if r else None, tp if r else None, 2 * Kd, r, 4.0, rpm, out=y)))
+                bench(lambda: K.lora_gemm(x, W, b, T if r else None, tp if r else None, 2 * Kd, r, 4.0, rpm, out=y, kernel=tile)))
 out = {}
 for (Kd, r), v in res.items():
     ms = min(v)

@@ -20,8 +20,7 @@ b = torch.randn(N, device=dev).bfloat16()
 tp = torch.randn(M // rpm, 2 * Kd + 2 * N + 8, device=dev) * 0.1
 y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
 T = torch.randn(M, 2, device=dev)
-_lib.call("eggroll_lora_gemm_tile", tile)
 for _ in range(reps):
-    K.lora_gemm(x, W, b, T if r else None, tp if r else None, 2 * Kd, r, 4.0, rpm, out=y)
+    K.lora_gemm(x, W, b, T if r else None, tp if r else None, 2 * Kd, r, 4.0, rpm, out=y, kernel=tile)
 torch.cuda.synchronize()
 print("done")

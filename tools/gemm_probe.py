@@ -40,9 +40,7 @@ for (M, N, Kd, rpm) in [(8 * 16384, 2240, 2240, 16384), (8 * 4800, 2240, 2240, 4
     ws = torch.empty(K.lora_workspace_numel(M, Kd, 2, rpm), device=dev)
     for _ in range(rounds):
         for tile in (256, 9, 8):
-            _lib.call("eggroll_lora_gemm_tile", tile)
-            res.setdefault(f"gemm_t{tile}", []).append(bench(lambda: K.lora_gemm(x, W, b, T, tp, 2 * Kd, 2, 4.0, rpm, out=y)))
-        _lib.call("eggroll_lora_gemm_tile", 0)
+            res.setdefault(f"gemm_t{tile}", []).append(bench(lambda: K.lora_gemm(x, W, b, T, tp, 2 * Kd, 2, 4.0, rpm, out=y, kernel=tile)))
         res.setdefault("linear_pop_auto", []).append(
             bench(lambda: K.lora_linear_pop(x, W, b, tp, 0, 2 * Kd, 2, 4.0, rpm, out=y, T_ws=ws)))
         res.setdefault("project", []).append(bench(lambda: K.lora_project(x, tp, 0, 2, rpm, out=T)))

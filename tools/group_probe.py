@@ -22,7 +22,6 @@ for (M, N, Kd, rpm) in [(8 * 16384, 2240, 2240, 16384), (8 * 4800, 2240, 2240, 4
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     T = torch.empty(M, 2, device=dev)
     K.lora_project(x, tp, 0, 2, rpm, out=T)
-    _lib.call("eggroll_lora_gemm_tile", 8)
-    ms = min(bench(lambda: K.lora_gemm(x, W, b, T, tp, 2 * Kd, 2, 4.0, rpm, out=y)) for _ in range(5))
+    ms = min(bench(lambda: K.lora_gemm(x, W, b, T, tp, 2 * Kd, 2, 4.0, rpm, out=y, kernel=8)) for _ in range(5))
     out[f"M{M}"] = round(2 * M * N * Kd / ms / 1e9, 1)
 print(json.dumps(out), flush=True)
