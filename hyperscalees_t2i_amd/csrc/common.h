@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string>
+#include <type_traits>
 
 #include "../../include/eggroll.h"
 
@@ -110,5 +111,34 @@ __device__ __forceinline__ u32x4 philox4x32_10_dev(u32x4 c, uint32_t k0, uint32_
 }
 
 constexpr uint32_t kNoiseTag = 0xE6606011u;
+
+// ---- factor layout + work tiles of perturb / update (include/eggroll.h) ------------------
+// Per matrix, one base sample's factors are a [rows][r] at factor_off, then b [cols][r] at
+// factor_off + pad4(rows * r): every segment starts 16-byte aligned when factor_off % 4 == 0.
+__host__ __device__ inline int64_t egg_pad4(int64_t x) { return (x + 3) & ~(int64_t)3; }
+__host__ __device__ inline int64_t egg_b_off(const eggroll_mat_t& mt, int r) {
+    return mt.factor_off + egg_pad4(mt.rows * (int64_t)r);
+}
+
+enum EggTileKind { T_VEC4 = 0, T_WIDE = 1, T_TALL = 2, T_VEC = 3, T_GEN = 4 };
+
+__host__ __device__ inline int egg_tile_kind(const eggroll_mat_t& mt, int r) {
+    const bool al = (mt.theta_off & 3) == 0 && (mt.factor_off & 3) == 0;
+    if (mt.cols == 0) return (al && (mt.rows & 3) == 0) ? T_VEC4 : T_VEC;
+    const bool rok = r == 1 || r == 2 || r == 4;
+    if (rok && al && mt.rows <= mt.cols && (mt.rows == 1 || mt.rows == 2 || mt.rows == 4) && (mt.cols & 3) == 0)
+        return T_WIDE;
+    if (rok && al && mt.cols < mt.rows && (mt.cols == 1 || mt.cols == 2 || mt.cols == 4) && (mt.rows & 3) == 0)
+        return T_TALL;
+    return T_GEN;
+}
+
+// workgroups of one matrix: fast kinds 1024 long-dimension positions each, generic 1024 elements
+__host__ __device__ inline int64_t egg_tile_count(const eggroll_mat_t& mt, int r) {
+    const int k = egg_tile_kind(mt, r);
+    const int64_t n = k == T_WIDE ? mt.cols : (k == T_TALL || k == T_VEC4 || k == T_VEC) ? mt.rows
+                                                                                        : mt.rows * mt.cols;
+    return (n + 1023) / 1024;
+}
 
 }  // namespace eggroll

@@ -91,305 +91,238 @@ __host__ __device__ __forceinline__ void member_to_base(int64_t k, int32_t pop, 
     }
 }
 
-// Matrix owning work chunk `chunk`: the number of matrices whose chunk_off <= chunk, minus one
-// (chunk_off is a prefix sum).  Every lane tests one matrix per step and a ballot counts — the
-// loads are independent (one memory latency for <= 256 matrices) instead of a binary search's
-// log2(n) dependent ones.  Wave-uniform result.
-__device__ __forceinline__ int find_mat(const eggroll_mat_t* __restrict__ mats, int n_mats, int64_t chunk) {
-    const int lane = threadIdx.x & 63;
-    int cnt = 0;
-    for (int b = 0; b < n_mats; b += 256) {
-        int64_t co[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {  // four independent loads in flight
-            const int i = b + 64 * t + lane;
-            co[t] = i < n_mats ? mats[i].chunk_off : INT64_MAX;
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) cnt += __popcll(__ballot(co[t] <= chunk));
-    }
-    return __builtin_amdgcn_readfirstlane(cnt - 1);
-}
-
 // ------------------------------------------------------------------------------------
-// Chunk work decomposition shared by perturb and update.  A chunk is EGGROLL_CHUNK = 1024
-// elements of one matrix (host prefix table); each of the 256 threads owns 4 element slots:
-//   VEC   1-D parameter (eps = the factor itself): e = e0 + tid + 256 u
-//   WIDE  rows in {1,2,4} <= cols (PEFT lora_A [r_l, in]): the chunk is 1024/rows whole columns;
-//         slot (u, row) = column c0 + tid + 256 u of every row — b loads coalesced, a[row]
-//         block-uniform (scalar loads), no integer division
-//   TALL  cols in {1,2,4} < rows (lora_B [out, r_l]): the chunk is 1024/cols whole rows;
-//         slot (u, col) = row r0 + tid + 256 u — a loads coalesced, b[col] block-uniform
-//   GEN   anything else: e = e0 + tid + 256 u, row/col by one 32-bit division per slot
-// Every slot's eps is computed with exactly the same fp32 operation order as the reference
-// restatement (a[0] b[0] + a[1] b[1] + ...) / sqrt(r), so the result does not depend on the kind.
+// Work decomposition shared by perturb and update: a host-built tile table (eggroll_tile_table)
+// gives every workgroup its (matrix, tile) with ONE scalar load — no search over the matrix list.
+// Fast tiles (T_VEC4 / T_WIDE / T_TALL, egg rank 1, 2 or 4) cover 1024 positions of the matrix's
+// LONG dimension — 4 consecutive positions per thread, so theta, the long-dimension factor and the
+// outputs move as 16-byte vectors — times all NU <= 4 entries of its SHORT dimension:
+//   T_WIDE  PEFT lora_A [r_l, in]  (rows in {1,2,4} <= cols): long = columns, uniform = a[row]
+//   T_TALL  PEFT lora_B [out, r_l] (cols in {1,2,4} <  rows): long = rows,    uniform = b[col]
+//   T_VEC4  1-D parameter (dense noise, the factor is the eps itself)
+// The short-dimension ("uniform") factors are the same for the whole workgroup: lane l of every wave
+// holds base sample / member l's, broadcast with v_readlane (an SGPR operand).  Anything else
+// (other ranks, unaligned 1-D params, matrices with no short dimension <= 4) runs the generic
+// per-element path on 1024-element chunks (T_VEC / T_GEN).
+// Every eps is computed in the reference's fp32 op order (sum_q a[i,q] b[c,q] sequential) / sqrt(r),
+// so the result does not depend on the tile kind.
 // ------------------------------------------------------------------------------------
-enum ChunkKind { K_VEC = 0, K_WIDE = 1, K_TALL = 2, K_GEN = 3 };
-
-__device__ __forceinline__ int chunk_kind(const eggroll_mat_t& mt) {
-    if (mt.cols == 0) return K_VEC;
-    if (mt.rows <= mt.cols && (mt.rows == 1 || mt.rows == 2 || mt.rows == 4)) return K_WIDE;
-    if (mt.cols < mt.rows && (mt.cols == 1 || mt.cols == 2 || mt.cols == 4)) return K_TALL;
-    return K_GEN;
-}
-
-struct Slots {  // this thread's element slots inside one chunk
+struct Slots {  // generic path: this thread's element slots inside one 1024-element chunk
     int row[4], col[4];
     bool ok[4];
 };
 
-template <int KIND>
+template <bool VEC1D>
 __device__ __forceinline__ Slots make_slots(const eggroll_mat_t& mt, int64_t cidx, int tid) {
     Slots sl;
-    const int rows = (int)mt.rows, cols = (int)mt.cols;
-    if constexpr (KIND == K_WIDE) {
-        const int cpc = EGGROLL_CHUNK / rows, c0 = (int)cidx * cpc;
+    const int cols = (int)mt.cols;
+    const int numel = VEC1D ? (int)mt.rows : (int)mt.rows * cols;
+    const int e0 = (int)cidx * EGGROLL_CHUNK;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int u = s / rows, rr = s % rows;  // rows is 1, 2 or 4: 4 / rows column groups
-            const int c = c0 + tid + 256 * u;
-            sl.row[s] = rr;
-            sl.col[s] = c;
-            sl.ok[s] = (s < 4) && (u < 4 / rows) && (c < c0 + cpc) && (c < cols);
-        }
-    } else if constexpr (KIND == K_TALL) {
-        const int rpc = EGGROLL_CHUNK / cols, r0 = (int)cidx * rpc;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int u = s / cols, cc = s % cols;
-            const int r = r0 + tid + 256 * u;
+    for (int s = 0; s < 4; ++s) {
+        const int e = e0 + s * 256 + tid;
+        sl.ok[s] = e < numel;
+        if (VEC1D) {
+            sl.row[s] = e;
+            sl.col[s] = 0;
+        } else {
+            const int r = sl.ok[s] ? e / cols : 0;
             sl.row[s] = r;
-            sl.col[s] = cc;
-            sl.ok[s] = (u < 4 / cols) && (r < r0 + rpc) && (r < rows);
-        }
-    } else {
-        const int numel = KIND == K_VEC ? rows : rows * cols;
-        const int e0 = (int)cidx * EGGROLL_CHUNK;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int e = e0 + s * 256 + tid;
-            sl.ok[s] = e < numel;
-            if (KIND == K_VEC) {
-                sl.row[s] = e;
-                sl.col[s] = 0;
-            } else {
-                const int r = sl.ok[s] ? e / cols : 0;
-                sl.row[s] = r;
-                sl.col[s] = e - r * cols;
-            }
+            sl.col[s] = e - r * cols;
         }
     }
     return sl;
 }
 
-__device__ __forceinline__ int slot_elem(const eggroll_mat_t& mt, const Slots& sl, int s, int kind) {
-    return kind == K_VEC ? sl.row[s] : sl.row[s] * (int)mt.cols + sl.col[s];
-}
-
 // eps of (row, col) of matrix mt for the base-sample factor row fj (utills.py:59-65 restated)
-// R1: egg rank 1 known at compile time — eps = a[row] b[col] (x / sqrt(1) == x exactly), so the
-// loads of consecutive base samples carry no loop-carried control flow and batch up.
-template <int KIND, bool R1>
+template <bool VEC1D>
 __device__ __forceinline__ float eps_rc(const eggroll_mat_t& mt, const float* __restrict__ fj, int row, int col,
                                         int r, float sqrt_r) {
 #pragma clang fp contract(off)
-    if constexpr (KIND == K_VEC) {
+    if constexpr (VEC1D) {
         return fj[mt.factor_off + row];
-    } else if constexpr (R1) {
-        return fj[mt.factor_off + row] * fj[mt.factor_off + mt.rows + col];
     } else {
         const float* a = fj + mt.factor_off + (int64_t)row * r;
-        const float* b = fj + mt.factor_off + mt.rows * r + (int64_t)col * r;
+        const float* b = fj + egg_b_off(mt, r) + (int64_t)col * r;
         float acc = a[0] * b[0];
         for (int q = 1; q < r; ++q) acc = acc + a[q] * b[q];
-        return acc / sqrt_r;
+        return r == 1 ? acc : acc / sqrt_r;
     }
 }
 
-// ------------------------------------------------------------------------------------
-// Rank-1 fast paths (egg rank 1, the Sana / BASELINE configuration) for VEC / WIDE / TALL chunks.
-// Each element is x_v * w_q: x is the factor along the chunk's long ("vector") dimension (b for
-// WIDE, a for TALL, the 1-D sample for VEC) — coalesced loads, one per slot column — and w the
-// factor along the short ("uniform") dimension (a[row] for WIDE, b[col] for TALL, 1 for VEC),
-// which is the same for the whole block: lane l of every wave holds the uniform factors of base
-// sample / member l and the inner loops broadcast them with v_readlane (an SGPR operand), so the
-// base loop carries no memory dependency except the x loads.
-// ------------------------------------------------------------------------------------
-template <int KIND, int NU>
-struct R1Map {  // slot s = u * NU + q: vector index vi(u), uniform index q
-    static constexpr int NV = 4 / NU;
-    __device__ static int64_t xoff(const eggroll_mat_t& mt) {  // factor offset of the vector dimension
-        return KIND == K_WIDE ? mt.factor_off + mt.rows : mt.factor_off;
+// 16-byte (V4) or scalar (unaligned caller buffers) access to 4 consecutive floats
+template <bool V4>
+__device__ __forceinline__ float4 ld4(const float* __restrict__ p) {
+    if constexpr (V4) {
+        return *reinterpret_cast<const float4*>(p);
+    } else {
+        return float4{p[0], p[1], p[2], p[3]};
     }
-    __device__ static int64_t woff(const eggroll_mat_t& mt) {  // factor offset of the uniform dimension
-        return KIND == K_WIDE ? mt.factor_off : mt.factor_off + mt.rows;
+}
+template <bool V4>
+__device__ __forceinline__ void st4(float* __restrict__ p, float4 v) {
+    if constexpr (V4) {
+        *reinterpret_cast<float4*>(p) = v;
+    } else {
+        p[0] = v.x;
+        p[1] = v.y;
+        p[2] = v.z;
+        p[3] = v.w;
+    }
+}
+__device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+__device__ __forceinline__ void f4set(float4& v, int i, float x) {
+    if (i == 0) v.x = x;
+    else if (i == 1) v.y = x;
+    else if (i == 2) v.z = x;
+    else v.w = x;
+}
+
+__device__ __forceinline__ float bcast(float v, int lane) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+// Fast-tile geometry.  Element (v, u) of a thread: long position p0 + v (v < 4), short index u.
+//   theta index: WIDE  toff + u * cols + p0 + v      TALL  toff + (p0 + v) * NU + u     VEC4 toff + p0 + v
+//   long factor: WIDE  b[(p0+v)][q]                  TALL  a[(p0+v)][q]                 VEC4 x[p0+v]
+// The thread's theta / output entries are NU float4s: TH[i] holds flat entries 4i..4i+3 of its block
+// (WIDE: row u = i; TALL: the 4 * NU contiguous floats of rows p0..p0+3).
+template <int KIND, int NU>
+struct FastGeo {
+    __device__ static int64_t th_off(const eggroll_mat_t& mt, int64_t p0, int i) {
+        return KIND == T_WIDE ? mt.theta_off + (int64_t)i * mt.cols + p0 : mt.theta_off + p0 * NU + 4 * i;
+    }
+    // (v, u) -> (float4 index, component)
+    __device__ static int vi(int v, int u) { return KIND == T_WIDE ? u : (v * NU + u) >> 2; }
+    __device__ static int vc(int v, int u) { return KIND == T_WIDE ? v : (v * NU + u) & 3; }
+    __device__ static int64_t x_off(const eggroll_mat_t& mt, int r) {  // long-dimension factor segment
+        return KIND == T_WIDE ? egg_b_off(mt, r) : mt.factor_off;
+    }
+    __device__ static int64_t u_off(const eggroll_mat_t& mt, int r) {  // short-dimension factor segment
+        return KIND == T_WIDE ? mt.factor_off : egg_b_off(mt, r);
     }
 };
 
-#ifndef EGG_UPD_GROUP
-#define EGG_UPD_GROUP 8  // base samples whose factor loads are in flight together
-#endif
-template <int KIND, int NU>
-__device__ __forceinline__ void update_chunk_r1(const float* __restrict__ theta, const float* __restrict__ factors,
-                                                int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
-                                                const eggroll_mat_t& mt, int64_t cidx, float lr,
-                                                float* __restrict__ out, double (&part)[4]) {
+// eps(v, u) of one base sample from its long factors X (4 positions x R) and the uniform factors
+// broadcast from lane `ln` (W[u * R + q]); reference op order.
+template <int KIND, int R, int NU>
+__device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&W)[NU * R], int v, int u, int ln,
+                                          float sqrt_r) {
 #pragma clang fp contract(off)
-    using MP = R1Map<KIND, NU>;
-    constexpr int NV = MP::NV;
-    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
-    const int lane = threadIdx.x & 63;
-    int vi[NV];
-    bool vok[NV];
+    if constexpr (KIND == T_VEC4) {
+        return f4(X[0], v);
+    } else {
+        float acc = 0.0f;
 #pragma unroll
-    for (int u = 0; u < NV; ++u) {
-        vi[u] = KIND == K_TALL ? sl.row[u * NU] : (KIND == K_WIDE ? sl.col[u * NU] : sl.row[u]);
-        vok[u] = sl.ok[u * NU];
-    }
-    const int64_t xo = MP::xoff(mt), wo = MP::woff(mt);
-    uint32_t vbyte[NV];
-#pragma unroll
-    for (int u = 0; u < NV; ++u) vbyte[u] = (uint32_t)vi[u] * 4u;
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (nf > 0) {
-        for (int64_t g = 0; g < n_base; g += 64) {
-            // lane l: w_q = c_{g+l} * (uniform factor q of base g+l)
-            float w[NU];
-            const int64_t jl = g + lane;
-#pragma unroll
-            for (int q = 0; q < NU; ++q) {
-                float c = jl < n_base ? s_c[jl] : 0.0f;
-                if (KIND != K_VEC) c = jl < n_base ? c * factors[jl * ld_f + wo + q] : 0.0f;
-                w[q] = c;
-            }
-            const int n = (int)((n_base - g) < 64 ? (n_base - g) : 64);
-            const float* fg = factors + g * ld_f + xo;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)fg, (short)0, 0x7fffffff, 0x00020000);
-            const int ldb = (int)(ld_f * 4);  // host: 64 * ld_f * 4 < 2^31
-            // groups of 8 base samples with a compile-time trip count (readlane is convergent: a
-            // runtime-count loop around it cannot be unrolled), 8 * NV loads in flight per thread
-            for (int j0 = 0; j0 < n; j0 += EGG_UPD_GROUP) {
-                float x[EGG_UPD_GROUP][NV];
-#pragma unroll
-                for (int t = 0; t < EGG_UPD_GROUP; ++t) {
-                    // buffer load: uniform row offset in soffset (SGPR), lane byte offset in voffset —
-                    // one VGPR per slot column instead of a 64-bit address per (base, slot)
-                    const int sb = (j0 + t) * ldb;
-#pragma unroll
-                    for (int u = 0; u < NV; ++u)
-                        x[t][u] = (j0 + t < n && vok[u])
-                                      ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vbyte[u], sb, 0))
-                                      : 0.0f;
-                }
-#pragma unroll
-                for (int t = 0; t < EGG_UPD_GROUP; ++t) {
-                    if (j0 + t >= n) break;
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const float ws = __builtin_bit_cast(
-                            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w[s % NU]), j0 + t));
-                        acc[s] = acc[s] + ws * x[t][s / NU];
-                    }
-                }
-            }
+        for (int q = 0; q < R; ++q) {
+            const float x = f4(X[(v * R + q) >> 2], (v * R + q) & 3);
+            const float w = bcast(W[u * R + q], ln);
+            const float pr = KIND == T_WIDE ? w * x : x * w;  // a * b
+            acc = q == 0 ? pr : acc + pr;
         }
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        if (!sl.ok[s]) continue;
-        const int64_t e = mt.theta_off + slot_elem(mt, sl, s, KIND);
-        const float th = theta[e];
-        float v = th;
-        if (nf > 0) {
-            const float gq = acc[s] / (float)nf;
-            const float t = lr * gq;
-            v = th + t;
-        }
-        out[e] = v;
-        const double d = (double)v - (double)th;
-        part[0] += d * d;
-        part[1] += (double)v * (double)v;
-        part[2] += (double)th * d;
-        part[3] += (double)th * (double)th;
+        return R == 1 ? acc : acc / sqrt_r;
     }
 }
 
-template <int KIND, int NU>
-__device__ __forceinline__ void perturb_chunk_r1(const float* __restrict__ theta, const float* __restrict__ factors,
-                                                 int64_t ld_f, const eggroll_mat_t& mt, int64_t cidx, int32_t pop,
-                                                 int32_t antithetic, int64_t member_lo, int n_members, float sigma,
-                                                 float* __restrict__ out, int64_t ld_out) {
-#pragma clang fp contract(off)
-    using MP = R1Map<KIND, NU>;
-    constexpr int NV = MP::NV;
-    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
-    const int lane = threadIdx.x & 63;
-    float th[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-        th[s] = (theta && sl.ok[s]) ? theta[mt.theta_off + slot_elem(mt, sl, s, KIND)] : 0.0f;
-    int vi[NV];
-    bool vok[NV];
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-        vi[u] = KIND == K_TALL ? sl.row[u * NU] : (KIND == K_WIDE ? sl.col[u * NU] : sl.row[u]);
-        vok[u] = sl.ok[u * NU];
-    }
-    const int64_t xo = MP::xoff(mt), wo = MP::woff(mt);
-    for (int g = 0; g < n_members; g += 64) {
-        // lane l: member g+l's base row offset, sign and uniform factors
-        int64_t jb;
-        float sg;
-        member_to_base(member_lo + g + lane, pop, antithetic, jb, sg);
-        const bool mok = g + lane < n_members;
-        float w[NU];
-#pragma unroll
-        for (int q = 0; q < NU; ++q) w[q] = (KIND == K_VEC || !mok) ? 1.0f : factors[jb * ld_f + wo + q];
-        const int n = (n_members - g) < 64 ? (n_members - g) : 64;
-        for (int i = 0; i < n; ++i) {
-            int64_t j;
-            float sgn;
-            member_to_base(member_lo + g + i, pop, antithetic, j, sgn);
-            const float* fj = factors + j * ld_f + xo;
-            float x[NV];
-#pragma unroll
-            for (int u = 0; u < NV; ++u) x[u] = vok[u] ? fj[vi[u]] : 0.0f;
-            float* dst = out + (int64_t)(g + i) * ld_out + mt.theta_off;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                if (!sl.ok[s]) continue;
-                const float wq = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w[s % NU]), i));
-                // eps = a[row] * b[col] (/ sqrt(1)); the product order a*b is the reference's
-                const float prod = KIND == K_VEC ? x[s / NU] : (KIND == K_WIDE ? wq * x[s / NU] : x[s / NU] * wq);
-                const float eps = sgn * prod;
-                float v;
-                if (theta) {
-                    const float t = sigma * eps;
-                    v = th[s] + t;
-                } else {
-                    v = sigma * eps;
-                }
-                dst[slot_elem(mt, sl, s, KIND)] = v;
-            }
-        }
-    }
-}
+// members / base samples whose long-factor loads are in flight together: 8 float4 loads per
+// thread whatever the rank (rank 4 at 8 samples needed 228 VGPRs and halved the occupancy)
+template <int KIND, int R>
+struct PGrp {
+    static constexpr int value = (KIND == T_VEC4 || R == 1) ? 8 : 8 / R;
+};
 
 // ------------------------------------------------------------------------------------
 // perturb / materialise: out[k] = theta + sigma * s_k * E_j(k) for the members [lo, lo + n).
-// One block per chunk; theta is read once and every member's row written from registers.
+// One workgroup per tile; theta is read once and every member's row is written from registers.
 // ------------------------------------------------------------------------------------
-template <int KIND, bool R1>
+template <int KIND, int R, int NU, bool V4>
+__device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, const float* __restrict__ factors,
+                                             int64_t ld_f, const eggroll_mat_t& mt, int64_t tidx, float sqrt_r,
+                                             int32_t pop, int32_t antithetic, int64_t member_lo, int n_members,
+                                             float sigma, float* __restrict__ out, int64_t ld_out) {
+#pragma clang fp contract(off)
+    using G = FastGeo<KIND, NU>;
+    constexpr int NX = KIND == T_VEC4 ? 1 : R;  // float4s of long factor per base sample
+    constexpr int NW = KIND == T_VEC4 ? 1 : NU * R;
+    const int lane = threadIdx.x & 63;
+    const int64_t lng = KIND == T_WIDE ? mt.cols : mt.rows;
+    const int64_t p0 = tidx * 1024 + 4 * (int64_t)threadIdx.x;
+    const bool ok = p0 < lng;
+    float4 TH[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) TH[i] = (theta && ok) ? ld4<V4>(theta + G::th_off(mt, p0, i)) : float4{0, 0, 0, 0};
+    const int64_t xo = G::x_off(mt, R) + p0 * (KIND == T_VEC4 ? 1 : R);
+    const int64_t uo = G::u_off(mt, R);
+    for (int g = 0; g < n_members; g += 64) {
+        // lane l: member g+l's uniform factors
+        float W[NW];
+        {
+            int64_t jb;
+            float sg;
+            member_to_base(member_lo + g + lane, pop, antithetic, jb, sg);
+            const bool mok = g + lane < n_members;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) W[w] = (KIND == T_VEC4 || !mok) ? 1.0f : factors[jb * ld_f + uo + w];
+        }
+        const int n = (n_members - g) < 64 ? (n_members - g) : 64;
+        constexpr int PG = PGrp<KIND, R>::value;
+        for (int i0 = 0; i0 < n; i0 += PG) {
+            float4 X[PG][NX];
+#pragma unroll
+            for (int t = 0; t < PG; ++t) {
+                int64_t j;
+                float sgn;
+                member_to_base(member_lo + g + i0 + t, pop, antithetic, j, sgn);
+                const bool lok = ok && (i0 + t < n);
+#pragma unroll
+                for (int c = 0; c < NX; ++c)
+                    X[t][c] = lok ? ld4<true>(factors + j * ld_f + xo + 4 * c) : float4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int t = 0; t < PG; ++t) {
+                if (i0 + t >= n) break;
+                int64_t j;
+                float sgn;
+                member_to_base(member_lo + g + i0 + t, pop, antithetic, j, sgn);
+                float4 O[NU];
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        const float e = sgn * fast_eps<KIND, R, NU>(X[t], W, v, u, i0 + t, sqrt_r);
+                        const float th = f4(TH[G::vi(v, u)], G::vc(v, u));
+                        float val;
+                        if (theta) {
+                            const float tt = sigma * e;
+                            val = th + tt;
+                        } else {
+                            val = sigma * e;
+                        }
+                        f4set(O[G::vi(v, u)], G::vc(v, u), val);
+                    }
+                if (ok) {
+                    float* dst = out + (int64_t)(g + i0 + t) * ld_out;
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) st4<V4>(dst + G::th_off(mt, p0, i), O[i]);
+                }
+            }
+        }
+    }
+}
+
+template <bool VEC1D>
 __device__ __forceinline__ void perturb_chunk(const float* __restrict__ theta, const float* __restrict__ factors,
                                               int64_t ld_f, const eggroll_mat_t& mt, int64_t cidx, int r,
                                               float sqrt_r, int32_t pop, int32_t antithetic, int64_t member_lo,
                                               int n_members, float sigma, float* __restrict__ out, int64_t ld_out) {
 #pragma clang fp contract(off)
-    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
+    const Slots sl = make_slots<VEC1D>(mt, cidx, threadIdx.x);
     float th[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-        th[s] = (theta && sl.ok[s]) ? theta[mt.theta_off + slot_elem(mt, sl, s, KIND)] : 0.0f;
+    for (int s = 0; s < 4; ++s) {
+        const int e = VEC1D ? sl.row[s] : sl.row[s] * (int)mt.cols + sl.col[s];
+        th[s] = (theta && sl.ok[s]) ? theta[mt.theta_off + e] : 0.0f;
+    }
 #pragma unroll 4
     for (int i = 0; i < n_members; ++i) {
         int64_t j;
@@ -400,7 +333,7 @@ __device__ __forceinline__ void perturb_chunk(const float* __restrict__ theta, c
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (!sl.ok[s]) continue;
-            const float eps = sgn * eps_rc<KIND, R1>(mt, fj, sl.row[s], sl.col[s], r, sqrt_r);
+            const float eps = sgn * eps_rc<VEC1D>(mt, fj, sl.row[s], sl.col[s], r, sqrt_r);
             float v;
             if (theta) {
                 const float t = sigma * eps;
@@ -408,47 +341,50 @@ __device__ __forceinline__ void perturb_chunk(const float* __restrict__ theta, c
             } else {
                 v = sigma * eps;
             }
-            dst[slot_elem(mt, sl, s, KIND)] = v;
+            dst[VEC1D ? sl.row[s] : sl.row[s] * (int)mt.cols + sl.col[s]] = v;
         }
     }
 }
 
-template <bool RANK1>
+// Dispatch of one tile to its kind's instantiation (R = egg rank, a template parameter).
+template <int R, bool V4, class FastFn, class GenFn>
+__device__ __forceinline__ void dispatch_tile(const eggroll_mat_t& mt, int r, FastFn&& fast, GenFn&& gen) {
+    const int kind = egg_tile_kind(mt, r);
+    const int nu = kind == T_WIDE ? (int)mt.rows : (kind == T_TALL ? (int)mt.cols : 1);
+    if (kind == T_VEC4) fast(std::integral_constant<int, T_VEC4>{}, std::integral_constant<int, 1>{});
+    else if (kind == T_WIDE && nu == 1) fast(std::integral_constant<int, T_WIDE>{}, std::integral_constant<int, 1>{});
+    else if (kind == T_WIDE && nu == 2) fast(std::integral_constant<int, T_WIDE>{}, std::integral_constant<int, 2>{});
+    else if (kind == T_WIDE) fast(std::integral_constant<int, T_WIDE>{}, std::integral_constant<int, 4>{});
+    else if (kind == T_TALL && nu == 1) fast(std::integral_constant<int, T_TALL>{}, std::integral_constant<int, 1>{});
+    else if (kind == T_TALL && nu == 2) fast(std::integral_constant<int, T_TALL>{}, std::integral_constant<int, 2>{});
+    else if (kind == T_TALL) fast(std::integral_constant<int, T_TALL>{}, std::integral_constant<int, 4>{});
+    else if (kind == T_VEC) gen(std::true_type{});
+    else gen(std::false_type{});
+}
+
+template <int R, bool V4>
 __global__ __launch_bounds__(256) void k_perturb(const float* __restrict__ theta, const float* __restrict__ factors,
-                                                 int64_t ld_f, const eggroll_mat_t* __restrict__ mats, int n_mats,
-                                                 int r, float sqrt_r, int32_t pop, int32_t antithetic,
-                                                 int64_t member_lo, int n_members, float sigma,
-                                                 float* __restrict__ out, int64_t ld_out) {
-    const int64_t chunk = blockIdx.x;
-    const int mi = find_mat(mats, n_mats, chunk);
-    const eggroll_mat_t mt = mats[mi];
-    const int64_t cidx = chunk - mt.chunk_off;
-#define EGG_PERTURB(KD, R1_)                                                                                  \
-    perturb_chunk<KD, R1_>(theta, factors, ld_f, mt, cidx, r, sqrt_r, pop, antithetic, member_lo, n_members, sigma, \
-                           out, ld_out)
-    const int kind = chunk_kind(mt);
-#define EGG_PERTURB1(KD, NU_) \
-    perturb_chunk_r1<KD, NU_>(theta, factors, ld_f, mt, cidx, pop, antithetic, member_lo, n_members, sigma, out, ld_out)
-    if constexpr (RANK1) {  // host launches this instantiation only for r == 1
-        const int nu = kind == K_WIDE ? (int)mt.rows : (kind == K_TALL ? (int)mt.cols : 1);
-        if (kind == K_VEC) EGG_PERTURB1(K_VEC, 1);
-        else if (kind == K_WIDE && nu == 1) EGG_PERTURB1(K_WIDE, 1);
-        else if (kind == K_WIDE && nu == 2) EGG_PERTURB1(K_WIDE, 2);
-        else if (kind == K_WIDE) EGG_PERTURB1(K_WIDE, 4);
-        else if (kind == K_TALL && nu == 1) EGG_PERTURB1(K_TALL, 1);
-        else if (kind == K_TALL && nu == 2) EGG_PERTURB1(K_TALL, 2);
-        else if (kind == K_TALL) EGG_PERTURB1(K_TALL, 4);
-        else EGG_PERTURB(K_GEN, true);
-    } else {
-        switch (kind) {
-            case K_VEC: EGG_PERTURB(K_VEC, false); break;
-            case K_WIDE: EGG_PERTURB(K_WIDE, false); break;
-            case K_TALL: EGG_PERTURB(K_TALL, false); break;
-            default: EGG_PERTURB(K_GEN, false); break;
-        }
-    }
-#undef EGG_PERTURB
-#undef EGG_PERTURB1
+                                                 int64_t ld_f, const eggroll_mat_t* __restrict__ mats,
+                                                 const eggroll_tile_t* __restrict__ tiles, int r, float sqrt_r,
+                                                 int32_t pop, int32_t antithetic, int64_t member_lo, int n_members,
+                                                 float sigma, float* __restrict__ out, int64_t ld_out) {
+    const eggroll_tile_t tl = tiles[blockIdx.x];
+    const eggroll_mat_t mt = mats[tl.mat];
+    dispatch_tile<R, V4>(
+        mt, r,
+        [&](auto KD, auto NUv) {
+            constexpr int KK = decltype(KD)::value;
+            if constexpr (KK == T_VEC4)
+                perturb_fast<T_VEC4, 1, 1, V4>(theta, factors, ld_f, mt, tl.index, sqrt_r, pop, antithetic, member_lo,
+                                               n_members, sigma, out, ld_out);
+            else if constexpr (R > 0)
+                perturb_fast<KK, R, decltype(NUv)::value, V4>(theta, factors, ld_f, mt, tl.index, sqrt_r, pop,
+                                                              antithetic, member_lo, n_members, sigma, out, ld_out);
+        },
+        [&](auto VD) {
+            perturb_chunk<decltype(VD)::value>(theta, factors, ld_f, mt, tl.index, r, sqrt_r, pop, antithetic,
+                                               member_lo, n_members, sigma, out, ld_out);
+        });
 }
 
 // ------------------------------------------------------------------------------------
@@ -476,10 +412,19 @@ __global__ __launch_bounds__(1024) void k_fitness(const float* __restrict__ S, i
     __shared__ float s_row[4096];
     __shared__ float s_sc[4096];
     __shared__ float s_misc[4];
+    __shared__ float s_S[4096];
     const int tid = threadIdx.x;
+    // S staged in LDS with one coalesced pass when it fits (pop x prompts <= 4096): the sequential
+    // fixed-order loops below then read LDS instead of issuing one dependent global load per step
+    if (n * m <= 4096) {
+        for (int i = tid; i < n * m; i += blockDim.x) s_S[i] = S[i];
+        __syncthreads();
+        S = s_S;
+    }
     // column means (thread j, sequential over k)
     for (int jj = tid; jj < m; jj += blockDim.x) {
         float acc = 0.0f;
+#pragma unroll 16
         for (int k = 0; k < n; ++k) acc = acc + S[(int64_t)k * m + jj];
         const float v = acc / (float)n;
         s_mu[jj] = v;
@@ -498,6 +443,7 @@ __global__ __launch_bounds__(1024) void k_fitness(const float* __restrict__ S, i
         __syncthreads();
         if (tid == 0) {
             float ss = 0.0f;
+#pragma unroll 16
             for (int k = 0; k < n; ++k) ss = ss + s_row[k];
             float sb = sqrtf(ss / (float)(n * m));
             if (sb < pn_eps) sb = pn_eps;  // clamp_min(eps) keeps NaN
@@ -521,10 +467,12 @@ __global__ __launch_bounds__(1024) void k_fitness(const float* __restrict__ S, i
     if (tid == 0) {
         int nf = 0;
         float sum = 0.0f;
+#pragma unroll 16
         for (int k = 0; k < n; ++k)
             if (isfinite(s_sc[k])) { sum = sum + s_sc[k]; ++nf; }
         const float mean = sum / (float)nf;
         float sq = 0.0f;
+#pragma unroll 16
         for (int k = 0; k < n; ++k)
             if (isfinite(s_sc[k])) { const float d = s_sc[k] - mean; sq = sq + d * d; }
         const float std = sqrtf(sq / (float)(nf - 1));  // torch.std unbiased; nf==1 -> NaN
@@ -546,6 +494,7 @@ __global__ __launch_bounds__(1024) void k_fitness(const float* __restrict__ S, i
         finite[k] = fin ? 1 : 0;
         fit[k] = fin ? (degenerate ? 0.0f : (s - mean) / (std + 1e-8f)) : 0.0f;
         int rank = 0;
+#pragma unroll 16
         for (int i = 0; i < n; ++i) {
             const float o = s_sc[i];
             rank += lt_nan_last(o, s) || (i < k && eq_nan(o, s));
@@ -555,30 +504,131 @@ __global__ __launch_bounds__(1024) void k_fitness(const float* __restrict__ S, i
 }
 
 // ------------------------------------------------------------------------------------
-// (4) update
+// (4) update: theta' = theta + lr * (1/N_f) sum_j c_j E_j per tile (c_j = antithetic-collapsed
+// fitness), then the norm caps.  With caps enabled every workgroup also writes its fp64 partial
+// sums {|d|^2, |theta'|^2, theta.d, |theta|^2}; k_update_caps reduces them in a FIXED order
+// (bit-reproducible on every rank) and rescales only if a cap triggers.
 // ------------------------------------------------------------------------------------
 struct UpdScalars {  // tail of the update workspace
     double step_scale, theta_scale;
     int32_t step_on, theta_on, nf, pad;
 };
 
-template <int KIND, bool R1>
+__device__ __forceinline__ void norm_acc(double (&part)[4], float v, float th) {
+    const double d = (double)v - (double)th;
+    part[0] += d * d;
+    part[1] += (double)v * (double)v;
+    part[2] += (double)th * d;
+    part[3] += (double)th * (double)th;
+}
+
+template <int KIND, int R, int NU, bool V4, bool NORMS>
+__device__ __forceinline__ void update_fast(const float* __restrict__ theta, const float* __restrict__ factors,
+                                            int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
+                                            const eggroll_mat_t& mt, int64_t tidx, float sqrt_r, float lr,
+                                            float* __restrict__ out, double (&part)[4]) {
+#pragma clang fp contract(off)
+    using G = FastGeo<KIND, NU>;
+    constexpr int NX = KIND == T_VEC4 ? 1 : R;
+    constexpr int NW = KIND == T_VEC4 ? 1 : NU * R;
+    const int lane = threadIdx.x & 63;
+    const int64_t lng = KIND == T_WIDE ? mt.cols : mt.rows;
+    const int64_t p0 = tidx * 1024 + 4 * (int64_t)threadIdx.x;
+    const bool ok = p0 < lng;
+    float4 TH[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) TH[i] = ok ? ld4<V4>(theta + G::th_off(mt, p0, i)) : float4{0, 0, 0, 0};
+    float acc[4][NU];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int u = 0; u < NU; ++u) acc[v][u] = 0.0f;
+    const int64_t xo = G::x_off(mt, R) + p0 * (KIND == T_VEC4 ? 1 : R);
+    const int64_t uo = G::u_off(mt, R);
+    if (nf > 0) {
+        for (int64_t g = 0; g < n_base; g += 64) {
+            // lane l: base g+l's uniform factors; rank 1 pre-multiplies c_j into them (w = c_j a_j[u]),
+            // the other ranks keep eps_j = (sum_q a b) / sqrt(r) and multiply by c_j afterwards
+            float W[NW], C;
+            {
+                const int64_t jl = g + lane;
+                const bool jok = jl < n_base;
+                C = jok ? s_c[jl] : 0.0f;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) {
+                    const float f = (KIND == T_VEC4 || !jok) ? 1.0f : factors[jl * ld_f + uo + w];
+                    W[w] = (R == 1 && KIND != T_VEC4) ? C * f : f;
+                }
+            }
+            const int n = (int)((n_base - g) < 64 ? (n_base - g) : 64);
+            constexpr int PG = PGrp<KIND, R>::value;
+            for (int j0 = 0; j0 < n; j0 += PG) {
+                float4 X[PG][NX];
+#pragma unroll
+                for (int t = 0; t < PG; ++t)
+#pragma unroll
+                    for (int c = 0; c < NX; ++c)
+                        X[t][c] = (ok && j0 + t < n) ? ld4<true>(factors + (g + j0 + t) * ld_f + xo + 4 * c)
+                                                     : float4{0, 0, 0, 0};
+#pragma unroll
+                for (int t = 0; t < PG; ++t) {
+                    if (j0 + t >= n) break;
+                    const float cj = bcast(C, j0 + t);
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) {
+                            if constexpr (KIND == T_VEC4) {
+                                acc[v][u] = acc[v][u] + cj * f4(X[t][0], v);
+                            } else if constexpr (R == 1) {
+                                acc[v][u] = acc[v][u] + bcast(W[u], j0 + t) * f4(X[t][0], v);
+                            } else {
+                                const float e = fast_eps<KIND, R, NU>(X[t], W, v, u, j0 + t, sqrt_r);
+                                acc[v][u] = acc[v][u] + cj * e;
+                            }
+                        }
+                }
+            }
+        }
+    }
+    float4 O[NU];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const float th = f4(TH[G::vi(v, u)], G::vc(v, u));
+            float val = th;
+            if (nf > 0) {
+                const float gq = acc[v][u] / (float)nf;
+                const float t = lr * gq;
+                val = th + t;
+            }
+            f4set(O[G::vi(v, u)], G::vc(v, u), val);
+            if (NORMS && ok) norm_acc(part, val, th);
+        }
+    if (ok) {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) st4<V4>(out + G::th_off(mt, p0, i), O[i]);
+    }
+}
+
+template <bool VEC1D, bool NORMS>
 __device__ __forceinline__ void update_chunk(const float* __restrict__ theta, const float* __restrict__ factors,
                                              int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
                                              const eggroll_mat_t& mt, int64_t cidx, int r, float sqrt_r, float lr,
                                              float* __restrict__ out, double (&part)[4]) {
 #pragma clang fp contract(off)
-    const Slots sl = make_slots<KIND>(mt, cidx, threadIdx.x);
+    const Slots sl = make_slots<VEC1D>(mt, cidx, threadIdx.x);
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (nf > 0) {
-        // sum_j c_j eps_j in base order j = 0, 1, ... (the order is the oracle's)
+        // sum_j c_j eps_j in base order j = 0, 1, ...
 #pragma unroll 2
         for (int64_t j = 0; j < n_base; ++j) {
             const float* fj = factors + j * ld_f;
             const float cj = s_c[j];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const float ev = eps_rc<KIND, R1>(mt, fj, sl.ok[s] ? sl.row[s] : 0, sl.ok[s] ? sl.col[s] : 0, r, sqrt_r);
+                const float ev = eps_rc<VEC1D>(mt, fj, sl.ok[s] ? sl.row[s] : 0, sl.ok[s] ? sl.col[s] : 0, r, sqrt_r);
                 acc[s] = acc[s] + cj * ev;
             }
         }
@@ -586,7 +636,7 @@ __device__ __forceinline__ void update_chunk(const float* __restrict__ theta, co
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         if (!sl.ok[s]) continue;
-        const int64_t e = mt.theta_off + slot_elem(mt, sl, s, KIND);
+        const int64_t e = mt.theta_off + (VEC1D ? sl.row[s] : sl.row[s] * (int)mt.cols + sl.col[s]);
         const float th = theta[e];
         float v = th;
         if (nf > 0) {
@@ -595,25 +645,23 @@ __device__ __forceinline__ void update_chunk(const float* __restrict__ theta, co
             v = th + t;
         }
         out[e] = v;
-        const double d = (double)v - (double)th;
-        part[0] += d * d;
-        part[1] += (double)v * (double)v;
-        part[2] += (double)th * d;
-        part[3] += (double)th * (double)th;
+        if (NORMS) norm_acc(part, v, th);
     }
 }
 
-template <bool RANK1>
-__global__ __launch_bounds__(256) void k_update_delta(const float* __restrict__ theta, const float* __restrict__ factors,
-                                                      int64_t ld_f, int64_t n_base, const float* __restrict__ fit,
-                                                      const float* __restrict__ stats, int32_t pop, int32_t antithetic,
-                                                      const eggroll_mat_t* __restrict__ mats, int n_mats, int r,
-                                                      float sqrt_r, float lr, float* __restrict__ out,
-                                                      double* __restrict__ partials) {
+template <int R, bool V4, bool NORMS>
+__global__ __launch_bounds__(256) void k_update(const float* __restrict__ theta, const float* __restrict__ factors,
+                                                int64_t ld_f, int64_t n_base, const float* __restrict__ fit,
+                                                const float* __restrict__ stats, int32_t pop, int32_t antithetic,
+                                                const eggroll_mat_t* __restrict__ mats,
+                                                const eggroll_tile_t* __restrict__ tiles, int r, float sqrt_r,
+                                                float lr, float* __restrict__ out, double* __restrict__ partials) {
 #pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) float s_c[];  // [n_base]
     __shared__ double s_red[4][4];
     const int tid = threadIdx.x;
+    const eggroll_tile_t tl = tiles[blockIdx.x];
+    const eggroll_mat_t mt = mats[tl.mat];
     const int nf = (int)stats[1];
     for (int64_t j = tid; j < n_base; j += blockDim.x) {
         float c;
@@ -626,90 +674,99 @@ __global__ __launch_bounds__(256) void k_update_delta(const float* __restrict__ 
         s_c[j] = c;
     }
     __syncthreads();
-    const int64_t chunk = blockIdx.x;
-    const int mi = find_mat(mats, n_mats, chunk);
-    const eggroll_mat_t mt = mats[mi];
-    const int64_t cidx = chunk - mt.chunk_off;
     double part[4] = {0.0, 0.0, 0.0, 0.0};
-#define EGG_UPDATE(KD, R1_) \
-    update_chunk<KD, R1_>(theta, factors, ld_f, n_base, s_c, nf, mt, cidx, r, sqrt_r, lr, out, part)
-    const int kind = chunk_kind(mt);
-#define EGG_UPDATE1(KD, NU_) \
-    update_chunk_r1<KD, NU_>(theta, factors, ld_f, n_base, s_c, nf, mt, cidx, lr, out, part)
-    if constexpr (RANK1) {  // host launches this instantiation only for r == 1
-        const int nu = kind == K_WIDE ? (int)mt.rows : (kind == K_TALL ? (int)mt.cols : 1);
-        if (kind == K_VEC) EGG_UPDATE1(K_VEC, 1);
-        else if (kind == K_WIDE && nu == 1) EGG_UPDATE1(K_WIDE, 1);
-        else if (kind == K_WIDE && nu == 2) EGG_UPDATE1(K_WIDE, 2);
-        else if (kind == K_WIDE) EGG_UPDATE1(K_WIDE, 4);
-        else if (kind == K_TALL && nu == 1) EGG_UPDATE1(K_TALL, 1);
-        else if (kind == K_TALL && nu == 2) EGG_UPDATE1(K_TALL, 2);
-        else if (kind == K_TALL) EGG_UPDATE1(K_TALL, 4);
-        else EGG_UPDATE(K_GEN, true);
-    } else {
-        switch (kind) {
-            case K_VEC: EGG_UPDATE(K_VEC, false); break;
-            case K_WIDE: EGG_UPDATE(K_WIDE, false); break;
-            case K_TALL: EGG_UPDATE(K_TALL, false); break;
-            default: EGG_UPDATE(K_GEN, false); break;
+    dispatch_tile<R, V4>(
+        mt, r,
+        [&](auto KD, auto NUv) {
+            constexpr int KK = decltype(KD)::value;
+            if constexpr (KK == T_VEC4)
+                update_fast<T_VEC4, 1, 1, V4, NORMS>(theta, factors, ld_f, n_base, s_c, nf, mt, tl.index, sqrt_r, lr,
+                                                     out, part);
+            else if constexpr (R > 0)
+                update_fast<KK, R, decltype(NUv)::value, V4, NORMS>(theta, factors, ld_f, n_base, s_c, nf, mt,
+                                                                    tl.index, sqrt_r, lr, out, part);
+        },
+        [&](auto VD) {
+            update_chunk<decltype(VD)::value, NORMS>(theta, factors, ld_f, n_base, s_c, nf, mt, tl.index, r, sqrt_r,
+                                                     lr, out, part);
+        });
+    if constexpr (NORMS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) part[q] = wave_sum_d(part[q]);
+        const int w = tid >> 6, lane = tid & 63;
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s_red[w][q] = part[q];
         }
-    }
-#undef EGG_UPDATE
-#undef EGG_UPDATE1
-#pragma unroll
-    for (int q = 0; q < 4; ++q) part[q] = wave_sum_d(part[q]);
-    const int w = tid >> 6, lane = tid & 63;
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s_red[w][q] = part[q];
-    }
-    __syncthreads();
-    if (tid < 4) {
-        partials[chunk * 4 + tid] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
+        __syncthreads();
+        if (tid < 4) partials[(int64_t)blockIdx.x * 4 + tid] = (s_red[0][tid] + s_red[1][tid]) + (s_red[2][tid] + s_red[3][tid]);
     }
 }
 
-__global__ __launch_bounds__(256) void k_update_finalize(const double* __restrict__ partials, int64_t n_chunks,
-                                                         const float* __restrict__ stats, float max_step,
-                                                         float max_theta, UpdScalars* __restrict__ sc) {
-    __shared__ double s[4][256];
-    const int tid = threadIdx.x;
+// Caps (utills.py:333-349: cap_step_norm then cap_theta_norm).  EVERY workgroup reduces all the
+// per-tile partials in the same fixed order (thread t: tiles t, t+256, ... sequentially, then a
+// fixed LDS tree), so every workgroup — and every rank — derives bit-identical scales with no
+// cross-workgroup handshake; then, only if a cap triggers, the grid rescales theta' (grid-stride).
+__global__ __launch_bounds__(256) void k_update_caps(const float* __restrict__ theta, int64_t D,
+                                                     const double* __restrict__ partials, int64_t n_part,
+                                                     const float* __restrict__ stats, float max_step, float max_theta,
+                                                     UpdScalars* __restrict__ sc, float* __restrict__ out) {
+#pragma clang fp contract(off)
+    __shared__ double s[4][4];
+    __shared__ float s_scale[2];
+    __shared__ int s_on[2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     double a[4] = {0, 0, 0, 0};
-    for (int64_t c = tid; c < n_chunks; c += 256)
-        for (int q = 0; q < 4; ++q) a[q] += partials[c * 4 + q];
-    for (int q = 0; q < 4; ++q) s[q][tid] = a[q];
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if (tid < st)
-            for (int q = 0; q < 4; ++q) s[q][tid] += s[q][tid + st];
-        __syncthreads();
+    for (int64_t c0 = 0; c0 < n_part; c0 += 1024) {  // 4 independent 32-byte loads per thread in flight
+        double4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t c = c0 + u * 256 + tid;
+            v[u] = c < n_part ? reinterpret_cast<const double4*>(partials)[c] : double4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a[0] += v[u].x;
+            a[1] += v[u].y;
+            a[2] += v[u].z;
+            a[3] += v[u].w;
+        }
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = wave_sum_d(a[q]);  // fixed butterfly order: same bits everywhere
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[w][q] = a[q];
+    __syncthreads();
     if (tid == 0) {
-        const double dd = s[0][0], oo = s[1][0], td = s[2][0], tt = s[3][0];
+        const double dd = (s[0][0] + s[1][0]) + (s[2][0] + s[3][0]), oo = (s[0][1] + s[1][1]) + (s[2][1] + s[3][1]);
+        const double td = (s[0][2] + s[1][2]) + (s[2][2] + s[3][2]), tt = (s[0][3] + s[1][3]) + (s[2][3] + s[3][3]);
         const int nf = (int)stats[1];
-        // cap_step_norm (utills.py:342-349) then cap_theta_norm (utills.py:333-339)
         const double dn = sqrt(dd);
-        int step_on = (nf > 0) && (max_step > 0.0f) && (dn > (double)max_step);
-        double ss = step_on ? (double)max_step / (dn + 1e-8) : 1.0;
+        const int step_on = (nf > 0) && (max_step > 0.0f) && (dn > (double)max_step);
+        const double ss = step_on ? (double)max_step / (dn + 1e-8) : 1.0;
         const double n2 = step_on ? (tt + 2.0 * ss * td + ss * ss * dd) : oo;
         const double tn = sqrt(n2 > 0.0 ? n2 : 0.0);
         // no finite member: the reference returns theta unchanged, caps included (unifed_es.py:237-240)
-        int theta_on = (nf > 0) && (max_theta > 0.0f) && (tn > (double)max_theta);
-        sc->step_scale = ss;
-        sc->theta_scale = theta_on ? (double)max_theta / (tn + 1e-8) : 1.0;
-        sc->step_on = step_on;
-        sc->theta_on = theta_on;
-        sc->nf = nf;
+        const int theta_on = (nf > 0) && (max_theta > 0.0f) && (tn > (double)max_theta);
+        const double ts = theta_on ? (double)max_theta / (tn + 1e-8) : 1.0;
+        s_on[0] = step_on;
+        s_on[1] = theta_on;
+        s_scale[0] = (float)ss;
+        s_scale[1] = (float)ts;
+        if (blockIdx.x == 0) {
+            sc->step_scale = ss;
+            sc->theta_scale = ts;
+            sc->step_on = step_on;
+            sc->theta_on = theta_on;
+            sc->nf = nf;
+        }
     }
-}
-
-__global__ __launch_bounds__(256) void k_update_apply(const float* __restrict__ theta, int64_t D,
-                                                      const UpdScalars* __restrict__ sc, float* __restrict__ out) {
-#pragma clang fp contract(off)
-    const int step_on = sc->step_on, theta_on = sc->theta_on;
+    __syncthreads();
+    const int step_on = s_on[0], theta_on = s_on[1];
     if (!step_on && !theta_on) return;
-    const float ss = (float)sc->step_scale, ts = (float)sc->theta_scale;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < D; i += (int64_t)gridDim.x * blockDim.x) {
+    const float ss = s_scale[0], ts = s_scale[1];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + tid; i < D; i += (int64_t)gridDim.x * blockDim.x) {
         float v = out[i];
         if (step_on) {
             const float th = theta[i];
@@ -758,23 +815,32 @@ int eggroll_philox_words(uint64_t seed, int64_t j, int64_t n_quads, uint32_t* ou
     return EGGROLL_OK;
 }
 
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static int launch_rank(int32_t rank) { return (rank == 1 || rank == 2 || rank == 4) ? rank : 0; }
+
 int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int64_t n_base,
-                    const eggroll_mat_t* mats, int32_t n_mats, int64_t total_chunks, int64_t D, int32_t rank,
+                    const eggroll_mat_t* mats, const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank,
                     int32_t pop, int32_t antithetic, int64_t member_lo, int64_t member_hi, float sigma, float* out,
                     int64_t ld_out, void* stream) {
     EGG_CHECK_ARG(rank >= 1, "perturb: rank must be >= 1");
     EGG_CHECK_ARG(pop >= 1 && member_lo >= 0 && member_hi <= pop && member_lo <= member_hi,
                   "perturb: members [%lld,%lld) outside pop %d", (long long)member_lo, (long long)member_hi, pop);
-    EGG_CHECK_ARG(n_mats >= 1 && mats && factors && out && ld_out >= D, "perturb: bad pointers/sizes");
+    EGG_CHECK_ARG(mats && tiles && factors && out && ld_out >= D, "perturb: bad pointers/sizes");
+    EGG_CHECK_ARG(al16(factors) && ld_f % 4 == 0, "perturb: factors must be 16-byte aligned with ld_f %% 4 == 0");
     const int64_t need_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
     EGG_CHECK_ARG(n_base >= need_base, "perturb: n_base %lld < %lld needed", (long long)n_base, (long long)need_base);
     EGG_CHECK_ARG(member_hi - member_lo <= 65535, "perturb: at most 65535 members per call");
-    EGG_CHECK_ARG(total_chunks >= 1 && total_chunks <= (1ll << 21), "perturb: bad total_chunks (<= 2^21: 32-bit element indices)");
+    EGG_CHECK_ARG(n_tiles >= 1 && n_tiles < (1ll << 31), "perturb: bad n_tiles");
     if (member_hi == member_lo || D == 0) return EGGROLL_OK;
     const float sqrt_r = (float)sqrt((double)rank);
-    hipLaunchKernelGGL(rank == 1 ? k_perturb<true> : k_perturb<false>, dim3((unsigned)total_chunks), dim3(256), 0, as_stream(stream), theta, factors, ld_f,
-                       mats, n_mats, rank, sqrt_r, pop, antithetic, member_lo, (int)(member_hi - member_lo), sigma,
-                       out, ld_out);
+    const bool v4 = (theta == nullptr || al16(theta)) && al16(out) && ld_out % 4 == 0;
+    auto* k = launch_rank(rank) == 1 ? (v4 ? k_perturb<1, true> : k_perturb<1, false>)
+            : launch_rank(rank) == 2 ? (v4 ? k_perturb<2, true> : k_perturb<2, false>)
+            : launch_rank(rank) == 4 ? (v4 ? k_perturb<4, true> : k_perturb<4, false>)
+                                     : (v4 ? k_perturb<0, true> : k_perturb<0, false>);
+    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles), dim3(256), 0, as_stream(stream), theta, factors, ld_f, mats, tiles,
+                       rank, sqrt_r, pop, antithetic, member_lo, (int)(member_hi - member_lo), sigma, out, ld_out);
     EGG_CHECK_LAUNCH("perturb");
     return EGGROLL_OK;
 }
@@ -791,40 +857,67 @@ int eggroll_fitness(const float* S, int32_t n, int32_t m, int32_t use_promptnorm
     return EGGROLL_OK;
 }
 
-int64_t eggroll_update_workspace_bytes(int64_t total_chunks) {
-    return total_chunks * 4 * (int64_t)sizeof(double) + 64;
+int64_t eggroll_update_workspace_bytes(int64_t n_tiles) {
+    return n_tiles * 4 * (int64_t)sizeof(double) + 64;
 }
 
 int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64_t n_base, const float* fitness,
-                   const float* stats, int32_t pop, int32_t antithetic, const eggroll_mat_t* mats, int32_t n_mats,
-                   int64_t total_chunks, int64_t D, int32_t rank, float lr, float max_step_norm,
-                   float theta_max_norm, void* workspace, float* theta_out, void* stream) {
-    EGG_CHECK_ARG(rank >= 1 && pop >= 1 && n_mats >= 1, "update: bad rank/pop/n_mats");
-    EGG_CHECK_ARG(theta && factors && fitness && stats && mats && workspace && theta_out, "update: NULL pointer");
+                   const float* stats, int32_t pop, int32_t antithetic, const eggroll_mat_t* mats,
+                   const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank, float lr,
+                   float max_step_norm, float theta_max_norm, void* workspace, float* theta_out, void* stream) {
+    EGG_CHECK_ARG(rank >= 1 && pop >= 1, "update: bad rank/pop");
+    EGG_CHECK_ARG(theta && factors && fitness && stats && mats && tiles && workspace && theta_out, "update: NULL pointer");
     EGG_CHECK_ARG(theta != theta_out, "update: theta_out may not alias theta");
+    EGG_CHECK_ARG(al16(factors) && ld_f % 4 == 0, "update: factors must be 16-byte aligned with ld_f %% 4 == 0");
     const int64_t need_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
     EGG_CHECK_ARG(n_base == need_base, "update: n_base %lld != %lld", (long long)n_base, (long long)need_base);
     EGG_CHECK_ARG(n_base <= 16384, "update: n_base > 16384 unsupported");
-    EGG_CHECK_ARG(total_chunks >= 1 && total_chunks <= (1ll << 21), "update: bad total_chunks (<= 2^21: 32-bit element indices)");
-    EGG_CHECK_ARG(((uintptr_t)workspace & 15) == 0, "update: workspace must be 16-byte aligned");
+    EGG_CHECK_ARG(n_tiles >= 1 && n_tiles < (1ll << 31), "update: bad n_tiles");
+    EGG_CHECK_ARG(al16(workspace), "update: workspace must be 16-byte aligned");
     if (D == 0) return EGGROLL_OK;
     const float sqrt_r = (float)sqrt((double)rank);
     double* partials = reinterpret_cast<double*>(workspace);
-    UpdScalars* sc = reinterpret_cast<UpdScalars*>(partials + total_chunks * 4);
+    UpdScalars* sc = reinterpret_cast<UpdScalars*>(partials + n_tiles * 4);
     hipStream_t st = as_stream(stream);
-    const bool r1 = rank == 1 && ld_f * 4 * 64 < (1ll << 31);  // rank-1 path's 32-bit buffer offsets
-    hipLaunchKernelGGL(r1 ? k_update_delta<true> : k_update_delta<false>, dim3((unsigned)total_chunks), dim3(256), (size_t)n_base * sizeof(float), st,
-                       theta, factors, ld_f, n_base, fitness, stats, pop, antithetic, mats, n_mats, rank, sqrt_r, lr,
-                       theta_out, partials);
-    EGG_CHECK_LAUNCH("update_delta");
-    hipLaunchKernelGGL(k_update_finalize, dim3(1), dim3(256), 0, st, partials, total_chunks, stats, max_step_norm,
-                       theta_max_norm, sc);
-    EGG_CHECK_LAUNCH("update_finalize");
-    int64_t blocks = (D + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(k_update_apply, dim3((unsigned)blocks), dim3(256), 0, st, theta, D, sc, theta_out);
-    EGG_CHECK_LAUNCH("update_apply");
+    const bool v4 = al16(theta) && al16(theta_out);
+    const bool caps = max_step_norm > 0.0f || theta_max_norm > 0.0f;
+    const int lr_ = launch_rank(rank);
+#define EGG_UPD_K(RV, V4V, NV) k_update<RV, V4V, NV>
+#define EGG_UPD_PICK(RV) (v4 ? (caps ? EGG_UPD_K(RV, true, true) : EGG_UPD_K(RV, true, false)) \
+                             : (caps ? EGG_UPD_K(RV, false, true) : EGG_UPD_K(RV, false, false)))
+    auto* k = lr_ == 1 ? EGG_UPD_PICK(1) : lr_ == 2 ? EGG_UPD_PICK(2) : lr_ == 4 ? EGG_UPD_PICK(4) : EGG_UPD_PICK(0);
+#undef EGG_UPD_PICK
+#undef EGG_UPD_K
+    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles), dim3(256), (size_t)n_base * sizeof(float), st, theta, factors, ld_f,
+                       n_base, fitness, stats, pop, antithetic, mats, tiles, rank, sqrt_r, lr, theta_out, partials);
+    EGG_CHECK_LAUNCH("update");
+    if (caps) {
+        int64_t blocks = (D + 1023) / 1024;
+        if (blocks > 256) blocks = 256;
+        hipLaunchKernelGGL(k_update_caps, dim3((unsigned)blocks), dim3(256), 0, st, theta, D, partials, n_tiles, stats,
+                           max_step_norm, theta_max_norm, sc, theta_out);
+        EGG_CHECK_LAUNCH("update_caps");
+    }
     return EGGROLL_OK;
+}
+
+int64_t eggroll_tile_table(const eggroll_mat_t* mats_host, int32_t n_mats, int32_t rank, eggroll_tile_t* tiles_host,
+                           int64_t capacity) {
+    if (!mats_host || n_mats < 1 || rank < 1) {
+        set_error("tile_table: need mats_host, n_mats >= 1, rank >= 1");
+        return EGGROLL_ERR_ARG;
+    }
+    int64_t n = 0;
+    for (int32_t i = 0; i < n_mats; ++i) {
+        const int64_t c = egg_tile_count(mats_host[i], rank);
+        for (int64_t t = 0; t < c; ++t, ++n) {
+            if (tiles_host && n < capacity) {
+                tiles_host[n].mat = i;
+                tiles_host[n].index = (int32_t)t;
+            }
+        }
+    }
+    return n;
 }
 
 }  // extern "C"

@@ -42,15 +42,25 @@ def _stream(device: torch.device):
 # ---------------------------------------------------------------------------------------
 
 
+def _pad4(x: int) -> int:
+    return -(-x // 4) * 4
+
+
 @dataclass
 class ThetaLayout:
-    """Per-parameter records of the flat theta vector and of one base sample's factors."""
+    """Per-parameter records of the flat theta vector and of one base sample's factors.
+
+    Factor layout (include/eggroll.h): per matrix a [rows][r] then b [cols][r], each segment padded
+    to a multiple of 4 floats so every segment is 16-byte aligned; 1-D params: numel values (padded).
+    The reference's contiguous order (torch.cat of the randn blocks, utills.py:59-66) is the same
+    sequence without the pads: `pack_factors` / `unpack_factors` convert."""
 
     shapes: List[Tuple[int, ...]]
     rank: int
     mats: np.ndarray = field(init=False)      # [n_mats, 6] int64 (eggroll_mat_t)
     D: int = field(init=False)
-    factor_len: int = field(init=False)
+    factor_len: int = field(init=False)       # padded length the noise kernel fills
+    factor_len_packed: int = field(init=False)  # useful factor values per base sample (no pads)
     factor_ld: int = field(init=False)        # row stride of factor buffers (multiple of 4)
     total_chunks: int = field(init=False)
     theta_offsets: List[int] = field(init=False)
@@ -59,25 +69,34 @@ class ThetaLayout:
         self.shapes = [tuple(int(x) for x in s) for s in self.shapes]
         if self.rank < 1:
             raise ValueError("egg rank must be >= 1")
-        recs, offs = [], []
-        toff = foff = coff = 0
+        recs, offs, segs = [], [], []
+        toff = foff = coff = packed = 0
         for s in self.shapes:
             if len(s) == 2:
                 m, n = s
-                numel, fl = m * n, self.rank * (m + n)
+                numel = m * n
+                seg = [(foff, m * self.rank), (foff + _pad4(m * self.rank), n * self.rank)]
+                fl = _pad4(m * self.rank) + _pad4(n * self.rank)
             else:
                 m, n = int(np.prod(s)), 0
-                numel, fl = m, m
+                numel = m
+                seg = [(foff, m)]
+                fl = _pad4(m)
             recs.append((m, n, toff, foff, coff, 0))
             offs.append(toff)
+            segs.extend(seg)
+            packed += sum(ln for _, ln in seg)
             toff += numel
             foff += fl
             coff += -(-numel // CHUNK)
         self.mats = np.array(recs, dtype=np.int64).reshape(-1, 6)
         self.D, self.factor_len, self.total_chunks = toff, foff, coff
-        self.factor_ld = -(-foff // 4) * 4
+        self.factor_len_packed = packed
+        self.factor_ld = _pad4(foff)
         self.theta_offsets = offs
+        self._segments = segs
         self._dev_cache: Dict[str, torch.Tensor] = {}
+        self._tiles: Optional[np.ndarray] = None
 
     @property
     def n_mats(self) -> int:
@@ -90,6 +109,48 @@ class ThetaLayout:
             t = torch.from_numpy(self.mats.copy()).to(device)
             self._dev_cache[key] = t
         return t
+
+    def tile_table(self) -> np.ndarray:
+        """[n_tiles, 2] int32 (eggroll_tile_t) from the library's host builder eggroll_tile_table."""
+        if self._tiles is None:
+            lib = _lib.load()
+            mats = np.ascontiguousarray(self.mats)
+            n = int(lib.eggroll_tile_table(mats.ctypes.data, self.n_mats, self.rank, None, 0))
+            if n < 1:
+                raise _lib.EggrollError(f"eggroll_tile_table failed ({n}): {lib.eggroll_last_error().decode()}")
+            tiles = np.zeros((n, 2), dtype=np.int32)
+            got = int(lib.eggroll_tile_table(mats.ctypes.data, self.n_mats, self.rank, tiles.ctypes.data, n))
+            if got != n:
+                raise _lib.EggrollError("eggroll_tile_table: size changed between calls")
+            self._tiles = tiles
+        return self._tiles
+
+    @property
+    def n_tiles(self) -> int:
+        return int(self.tile_table().shape[0])
+
+    def tiles_on(self, device) -> torch.Tensor:
+        key = "tiles:" + str(torch.device(device))
+        t = self._dev_cache.get(key)
+        if t is None:
+            t = torch.from_numpy(self.tile_table().copy()).to(device)
+            self._dev_cache[key] = t
+        return t
+
+    def pack_factors(self, contig) -> np.ndarray:
+        """Reference-order factors [p, factor_len_packed] -> this layout [p, factor_ld] (pads = 0)."""
+        contig = np.asarray(contig, dtype=np.float32)
+        out = np.zeros((contig.shape[0], self.factor_ld), np.float32)
+        src = 0
+        for off, ln in self._segments:
+            out[:, off:off + ln] = contig[:, src:src + ln]
+            src += ln
+        return out
+
+    def unpack_factors(self, padded) -> np.ndarray:
+        """This layout [p, >= factor_len] -> the reference's contiguous order [p, factor_len_packed]."""
+        padded = np.asarray(padded, dtype=np.float32)
+        return np.concatenate([padded[:, off:off + ln] for off, ln in self._segments], axis=1)
 
 
 def n_base_samples(pop: int, antithetic: bool) -> int:
@@ -128,13 +189,16 @@ def perturb(theta: Optional[torch.Tensor], factors: torch.Tensor, layout: ThetaL
     if theta is not None:
         _dev(theta, "perturb(theta)", torch.float32)
     n = member_hi - member_lo
-    if out is None:
-        out = torch.empty((n, layout.D), dtype=torch.float32, device=device)
-    _dev(out, "perturb(out)", torch.float32)
+    if out is None:  # rows padded to a multiple of 4 floats: 16-byte aligned rows take the vector path
+        out = torch.empty((n, _pad4(layout.D)), dtype=torch.float32, device=device)[:, :layout.D]
+    if out.dim() != 2 or out.stride(1) != 1 or out.shape[1] < layout.D:
+        raise _lib.EggrollError("perturb(out): expected a [n, >= D] fp32 device tensor with unit inner stride")
+    if out.device.type != "cuda" or out.dtype != torch.float32:
+        raise _lib.EggrollError("perturb(out): expected a ROCm fp32 tensor (no CPU fallback)")
     _lib.call("eggroll_perturb", _p(theta), factors.data_ptr(), factors.stride(0), factors.shape[0],
-              layout.mats_on(device).data_ptr(), layout.n_mats, layout.total_chunks, layout.D, layout.rank, pop,
-              int(bool(antithetic)), member_lo, member_hi, float(sigma), out.data_ptr(), out.stride(0),
-              _stream(device))
+              layout.mats_on(device).data_ptr(), layout.tiles_on(device).data_ptr(), layout.n_tiles, layout.D,
+              layout.rank, pop, int(bool(antithetic)), member_lo, member_hi, float(sigma), out.data_ptr(),
+              out.stride(0), _stream(device))
     return out
 
 
@@ -172,7 +236,7 @@ def fitness(S: torch.Tensor, promptnorm: bool, eps: float = 1e-8) -> Dict[str, t
 
 class UpdateWorkspace:
     def __init__(self, layout: ThetaLayout, device):
-        nbytes = int(_lib.load().eggroll_update_workspace_bytes(layout.total_chunks))
+        nbytes = int(_lib.load().eggroll_update_workspace_bytes(layout.n_tiles))
         self.buf = torch.zeros(-(-nbytes // 16) * 16, dtype=torch.uint8, device=device)  # done counter starts at 0
 
 
@@ -189,7 +253,8 @@ def update(theta: torch.Tensor, factors: torch.Tensor, fit: Dict[str, torch.Tens
         workspace = UpdateWorkspace(layout, dev)
     _lib.call("eggroll_update", theta.data_ptr(), factors.data_ptr(), factors.stride(0), factors.shape[0],
               fit["fitness"].data_ptr(), fit["stats"].data_ptr(), pop, int(bool(antithetic)),
-              layout.mats_on(dev).data_ptr(), layout.n_mats, layout.total_chunks, layout.D, layout.rank, float(lr),
+              layout.mats_on(dev).data_ptr(), layout.tiles_on(dev).data_ptr(), layout.n_tiles, layout.D, layout.rank,
+              float(lr),
               float(max_step_norm or 0.0), float(theta_max_norm or 0.0), workspace.buf.data_ptr(), out.data_ptr(),
               _stream(dev))
     return out

@@ -3,10 +3,12 @@
 Used by bench.py and tools/aux_probe.py.  Each kernel is timed with HIP events recorded on the
 stream it is launched on (torch's current stream — every libeggroll wrapper launches there) and
 priced against its ALGORITHMIC bytes:
-  noise_factors  4 * n_base * factor_len                       (factors written once)
-  perturb        4 * (n_local * D + D + n_used * factor_len)   (theta_pop written, theta + the
-                                                                local members' factor sets read)
-  update         4 * (n_base * factor_len + 2 * D)             (factors + theta read, theta' written)
+  noise_factors  4 * n_base * F                       (factors written once)
+  perturb        4 * (n_local * D + D + n_used * F)    (theta_pop written, theta + the local members'
+                                                       factor sets read)
+  update         4 * (n_base * F + 2 * D)              (factors + theta read, theta' written)
+with F = layout.factor_len_packed, the useful factor values per base sample (the 16-byte alignment
+pads of the device layout, < 0.2 % at the Sana shapes, are not counted).
 The fitness kernel reads a [pop, m] score matrix: latency-bound, reported in microseconds.
 """
 from __future__ import annotations
@@ -68,11 +70,12 @@ def aux_kernel_rooflines(layout: ThetaLayout, pop: int, member_lo: int, member_h
     out: Dict[str, Dict[str, float]] = {}
     fac = K.noise_factors(0, nb, layout, device)
     sec = _time(lambda: K.noise_factors(0, nb, layout, device, out=fac), it)
-    out["noise_factors"] = _entry(sec, 4.0 * nb * layout.factor_len)
+    F = layout.factor_len_packed
+    out["noise_factors"] = _entry(sec, 4.0 * nb * F)
     tp = torch.empty((nl, D), dtype=torch.float32, device=device)
     sec = _time(lambda: K.perturb(theta, fac, layout, pop, antithetic, member_lo, member_hi, sigma, out=tp), it)
     nu = used_bases(pop, antithetic, member_lo, member_hi)
-    out["perturb"] = _entry(sec, 4.0 * (nl * D + D + nu * layout.factor_len))
+    out["perturb"] = _entry(sec, 4.0 * (nl * D + D + nu * F))
     S = torch.randn(pop, m, device=device) + 21
     fit = K.fitness(S, True)
     sec = _time(lambda: K.fitness(S, True), it)
@@ -80,7 +83,7 @@ def aux_kernel_rooflines(layout: ThetaLayout, pop: int, member_lo: int, member_h
     ws = K.UpdateWorkspace(layout, device)
     newt = torch.empty_like(theta)
     sec = _time(lambda: K.update(theta, fac, fit, layout, pop, antithetic, lr, 0.0, 40.0, out=newt, workspace=ws), it)
-    out["update"] = _entry(sec, 4.0 * (nb * layout.factor_len + 2 * D))
+    out["update"] = _entry(sec, 4.0 * (nb * F + 2 * D))
     out["sizes"] = {"pop": pop, "members": [member_lo, member_hi], "n_base": nb, "D": D,
-                    "factor_len": layout.factor_len}
+                    "factor_len": F, "n_tiles": layout.n_tiles}
     return out

@@ -42,16 +42,35 @@ extern "C" {
 
 /* One trainable parameter inside the flat theta vector (reference `utills.py:141-162`:
  * theta = concat of module.parameters() with requires_grad, row-major views).
- * Passed to kernels as a DEVICE array of n_mats records (int64 fields).              */
+ * Passed to kernels as a DEVICE array of n_mats records (int64 fields).
+ * Factor layout of one base sample (the noise kernel fills the whole padded vector): a matrix's
+ * a [rows][r] starts at factor_off, its b [cols][r] at factor_off + pad4(rows*r) (pad4(x) = x
+ * rounded up to a multiple of 4); a 1-D param's numel values start at factor_off.  Hosts place
+ * every factor_off at a multiple of 4 (segments padded to 4 floats) so the kernels move factors
+ * as 16-byte vectors; other offsets are accepted and run the per-element path.                 */
 typedef struct eggroll_mat {
     int64_t rows;       /* m: first dim (or numel for a 1-D param)                    */
     int64_t cols;       /* n: second dim; 0 marks a 1-D param (dense Gaussian noise)  */
     int64_t theta_off;  /* element offset of this param in theta                       */
     int64_t factor_off; /* element offset of its factors in one base sample's factor   *
-                         * vector: a [rows][r] then b [cols][r]; 1-D: numel values     */
-    int64_t chunk_off;  /* prefix count of EGGROLL_CHUNK-element work chunks           */
+                         * vector (see the layout note above)                          */
+    int64_t chunk_off;  /* informational: prefix count of EGGROLL_CHUNK-element chunks */
     int64_t reserved;
 } eggroll_mat_t;
+
+/* One workgroup's share of perturb / update: matrix `mat`, tile `index` inside it.  Built on the
+ * host by eggroll_tile_table (depends on the mats records and the egg rank) and passed as a
+ * DEVICE array: the kernels find their matrix with one load instead of a search.              */
+typedef struct eggroll_tile {
+    int32_t mat;
+    int32_t index;
+} eggroll_tile_t;
+
+/* Host function (host pointers, no GPU work): writes the tile table of mats_host for egg rank
+ * `rank` into tiles_host[0, capacity) and returns the tile count (call with tiles_host = NULL to
+ * size it); negative on a bad argument.                                                        */
+int64_t eggroll_tile_table(const eggroll_mat_t* mats_host, int32_t n_mats, int32_t rank,
+                           eggroll_tile_t* tiles_host, int64_t capacity);
 
 #define EGGROLL_CHUNK 1024
 
@@ -76,11 +95,12 @@ int eggroll_philox_words(uint64_t seed, int64_t j, int64_t n_quads, uint32_t* ou
  *   out[(k - member_lo) * ld_out + d] = theta[d] + sigma * s_k * E_{j(k)}[d]
  * with E computed as (sum_q a[i,q] b[c,q]) / sqrt(r) in fp32 (reference op order).
  * factors: base samples [0, n_base) with row stride ld_f (as written by noise_factors,
- * base_lo = 0).  mats: device array of n_mats records; total_chunks = sum over mats of
- * ceil(numel / EGGROLL_CHUNK) (host-known); D = total theta length.                     */
+ * base_lo = 0), 16-byte aligned, ld_f % 4 == 0.  mats: device array of n_mats records; tiles:
+ * device array of the n_tiles records eggroll_tile_table built for (mats, rank); D = total theta
+ * length.  16-byte aligned theta / out with ld_out % 4 == 0 take the vector path.               */
 int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int64_t n_base,
-                    const eggroll_mat_t* mats, int32_t n_mats, int64_t total_chunks, int64_t D,
-                    int32_t rank,
+                    const eggroll_mat_t* mats, const eggroll_tile_t* tiles, int64_t n_tiles,
+                    int64_t D, int32_t rank,
                     int32_t pop, int32_t antithetic, int64_t member_lo, int64_t member_hi,
                     float sigma, float* out, int64_t ld_out, void* stream);
 
@@ -103,15 +123,17 @@ int eggroll_fitness(const float* S, int32_t n, int32_t m, int32_t use_promptnorm
  *   theta_out = theta + (lr_scale*sigma) * (1/N_f) * sum_k f_k eps_k
  * evaluated in factor form as a rank-(n_base*r) reduction per matrix (antithetic pairs
  * collapsed: c_j = f_j - f_{j+h}).  N_f is read from stats[1] (device, written by
- * eggroll_fitness); N_f == 0 leaves theta unchanged (unifed_es.py:237-240).
- * max_step_norm / theta_max_norm <= 0 disable the caps.
- * workspace: >= eggroll_update_workspace_bytes(n_mats_chunks) bytes.
+ * eggroll_fitness); N_f == 0 leaves theta unchanged, caps included (unifed_es.py:237-240).
+ * max_step_norm / theta_max_norm <= 0 disable the caps; with both disabled the update is ONE
+ * launch, else a second launch reduces the per-tile norms in a fixed order and rescales only
+ * if a cap triggers.  tiles / n_tiles as for eggroll_perturb.
+ * workspace: >= eggroll_update_workspace_bytes(n_tiles) bytes, 16-byte aligned.
  * theta_out may not alias theta.                                                          */
-int64_t eggroll_update_workspace_bytes(int64_t total_chunks);
+int64_t eggroll_update_workspace_bytes(int64_t n_tiles);
 int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64_t n_base,
                    const float* fitness, const float* stats, int32_t pop, int32_t antithetic,
-                   const eggroll_mat_t* mats, int32_t n_mats, int64_t total_chunks, int64_t D,
-                   int32_t rank, float lr, float max_step_norm, float theta_max_norm,
+                   const eggroll_mat_t* mats, const eggroll_tile_t* tiles, int64_t n_tiles,
+                   int64_t D, int32_t rank, float lr, float max_step_norm, float theta_max_norm,
                    void* workspace, float* theta_out, void* stream);
 
 /* (2) Population-batched perturbed LoRA linear — replaces per-member

@@ -74,19 +74,25 @@ def n_base_samples(pop: int, antithetic: bool) -> int:
 # ---------------------------------------------------------------------------------------
 
 
+def _pad4(x: int) -> int:
+    return -(-x // 4) * 4
+
+
 def layout(shapes: Sequence[Sequence[int]], rank: int) -> Dict[str, object]:
     """theta = concat(p.view(-1)) in parameter order; factors per base sample = for each
-    matrix a [m][r] then b [n][r]; 1-D params: numel dense values."""
+    matrix a [m][r] then b [n][r]; 1-D params: numel dense values.  The device buffer pads every
+    segment to a multiple of 4 floats (include/eggroll.h); the functions below that take factor
+    arrays use the reference's contiguous order (ThetaLayout.unpack_factors converts)."""
     recs = []
     toff = foff = coff = 0
     for s in shapes:
         s = tuple(int(x) for x in s)
         if len(s) == 2:
             m, n = s
-            numel, fl = m * n, rank * (m + n)
+            numel, fl = m * n, _pad4(rank * m) + _pad4(rank * n)
         else:
             m, n = int(np.prod(s)), 0
-            numel, fl = m, m
+            numel, fl = m, _pad4(m)
         recs.append((m, n, toff, foff, coff, 0))
         toff += numel
         foff += fl

@@ -66,3 +66,40 @@ def test_layout_matches_oracle():
         b = O.layout(shapes, r)
         assert np.array_equal(a.mats, b["mats"]) and a.D == b["D"] and a.factor_len == b["factor_len"]
         assert a.total_chunks == b["total_chunks"] and a.factor_ld % 4 == 0
+
+
+def _tile_kind(m, n, toff, foff, r):
+    """include/eggroll.h tile rule restated (common.h egg_tile_kind)."""
+    al = toff % 4 == 0 and foff % 4 == 0
+    if n == 0:
+        return "vec4" if (al and m % 4 == 0) else "vec"
+    rok = r in (1, 2, 4)
+    if rok and al and m <= n and m in (1, 2, 4) and n % 4 == 0:
+        return "wide"
+    if rok and al and n < m and n in (1, 2, 4) and m % 4 == 0:
+        return "tall"
+    return "gen"
+
+
+def test_tile_table_covers_every_matrix():
+    shapes = [(2, 2240), (2240, 2), (6,), (7,), (2, 256), (13440, 2), (3, 5), (4, 12), (12, 4), (1, 1), (2, 30)]
+    for r in (1, 2, 3, 4):
+        lay = ThetaLayout(shapes, r)
+        t = lay.tile_table()
+        assert t.dtype == np.int32 and t.shape[1] == 2
+        want = []
+        for i, (m, n, toff, foff, _, _) in enumerate(lay.mats.tolist()):
+            k = _tile_kind(m, n, toff, foff, r)
+            long = {"wide": n, "tall": m, "vec4": m, "vec": m, "gen": m * n}[k]
+            want += [(i, j) for j in range(-(-long // 1024))]
+        assert [tuple(x) for x in t.tolist()] == want, r
+        assert all(f % 4 == 0 for f in lay.mats[:, 3])            # every factor segment 16-byte aligned
+
+
+def test_factor_pack_roundtrip():
+    shapes = [(2, 7), (5, 2), (3,), (1, 1)]
+    lay = ThetaLayout(shapes, 2)
+    x = np.arange(3 * lay.factor_len_packed, dtype=np.float32).reshape(3, -1)
+    p = lay.pack_factors(x)
+    assert p.shape == (3, lay.factor_ld) and np.array_equal(lay.unpack_factors(p), x)
+    assert lay.factor_len_packed == 2 * (2 + 7) + 2 * (5 + 2) + 3 + 2 * 2

@@ -67,9 +67,8 @@ def test_injected_reference_factors_reproduce_reference_eps(dev, golden):
         pop, rank, anti = int(pop), int(rank[1:]), bool(int(anti[1:]))
         shapes = SHAPE_SETS[sname]
         lay = K.ThetaLayout(shapes, rank)
-        fac = torch.zeros((d["factors"].shape[0], lay.factor_ld), dtype=torch.float32)
-        fac[:, :lay.factor_len] = torch.from_numpy(d["factors"])
-        fac = fac.to(dev)
+        fac = torch.from_numpy(lay.pack_factors(d["factors"])).to(dev)
+        assert np.array_equal(lay.unpack_factors(fac.cpu().numpy()), d["factors"])
         eps = K.perturb(None, fac, lay, pop, anti, 0, pop, 1.0).cpu().numpy()
         if rank == 1:
             assert np.array_equal(eps, d["eps"]), key
@@ -96,7 +95,7 @@ def test_perturb_member_ranges_consistent(dev):
     eps = n.eps_from_factors(fac, pop)
     h = pop // 2
     assert torch.equal(eps[:h], -eps[h:2 * h])
-    ref = O.dev_eps_rows(fac[:, :n.layout.factor_len].cpu().numpy(), shapes, pop, 1, True, 0, pop)
+    ref = O.dev_eps_rows(n.layout.unpack_factors(fac.cpu().numpy()), shapes, pop, 1, True, 0, pop)
     assert np.array_equal(eps.cpu().numpy(), ref)
 
 
