@@ -284,6 +284,113 @@ def gen_s_aggregation():
     return len(recs)
 
 
+TINY_ARCH = dict(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=2,
+                 cross_attention_head_dim=64, caption_channels=2304)
+
+
+def gen_member_eval_injection(u):
+    """g10: reference EggRollNoiser factors captured on the LoRA theta layout of the tiny Sana
+    architecture the GPU parity tests build (tests/test_gpu_parity_fp32.py), pop 8, egg rank 1,
+    antithetic, for sigma 1e-2 and 0.5: the injected noise of the bf16-vs-fp32 member-eval test."""
+    sys.path.insert(0, str(OUT.parent.parent))
+    from hyperscalees_t2i_amd.sana import SanaArch, sana_lora_shapes
+    shapes = sana_lora_shapes(SanaArch(**TINY_ARCH))
+    recs = {"shapes": np.array(shapes, np.int64)}
+    for seed, sigma in ((0, 1e-2), (1, 0.5)):
+        torch.manual_seed(seed)
+        noiser = u.EggRollNoiser([torch.Size(s) for s in shapes], sigma=sigma, lr_scale=0.1, rank=1,
+                                 use_antithetic=True)
+        with RandnRecorder() as rr:
+            eps = noiser.sample_eps(8, "cpu")
+        parts = [t.reshape(4, -1) for t in rr.calls]
+        key = f"s{seed}"
+        recs[key + "/factors"] = torch.cat(parts, dim=1).numpy()
+        recs[key + "/eps"] = eps.numpy()
+        recs[key + "/sigma"] = np.array(sigma, np.float32)
+    np.savez_compressed(OUT / "g10_member_eval_injection.npz", **recs)
+    return len(recs)
+
+
+VAR_TARGETS = ["mat_qkv", "proj", "fc1", "fc2", "ada_lin.1", "head_nm.ada_lin.1", "head"]  # unifed_es.py:406
+
+
+def gen_var():
+    """g8: BASELINE configs[0] (VAR-d16, LoRA r 4 / alpha 16, unifed_es.py:403-406) from the reference's
+    own VAR_models (importable here): the theta layout (PEFT suffix matching of the targets over
+    var.named_modules(), lora_A [r, in] then lora_B [out, r] per target) and LoRA'd-linear
+    activations of one class-conditional generation at seeded init.  build_vae_var leaves the VQVAE
+    weights uninitialised (NaN images), so they are initialised explicitly (seeded
+    N(0, 1/fan_in)).  Per distinct linear shape: 64 input rows of the largest call (the last scale,
+    CFG-doubled), the first 64 output features of W / bias, the module's own fp32 output on those
+    rows, seeded LoRA factors and the PEFT-formula output in fp64 on the bf16-rounded operands."""
+    sys.path.insert(0, str(REF))
+    import torch.nn as nn
+    from VAR_models import build_vae_var
+    torch.manual_seed(0)
+    vae, var = build_vae_var(device="cpu", depth=16, flash_if_available=False, fused_if_available=False)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for name, p in vae.named_parameters():
+            if p.dim() > 1:
+                p.copy_(torch.randn(p.shape, generator=g) / math.sqrt(p[0].numel()))
+            elif name.endswith("weight"):
+                p.fill_(1.0)
+            else:
+                p.zero_()
+    var.eval()
+    targets = [(n, m) for n, m in var.named_modules()
+               if isinstance(m, nn.Linear) and any(n == t or n.endswith("." + t) for t in VAR_TARGETS)]
+    r = 4
+    shapes = []
+    for n, m in targets:
+        shapes += [(r, m.in_features), (m.out_features, r)]
+    recs = {"shapes": np.array(shapes, np.int64), "names": np.array("\x1f".join(n for n, _ in targets))}
+    captured = {}
+
+    def hook(name):
+        def f(mod, inp, out):
+            x = inp[0].detach().reshape(-1, inp[0].shape[-1])
+            if name not in captured or x.shape[0] > captured[name][0].shape[0]:
+                captured[name] = (x.clone(), out.detach().reshape(-1, out.shape[-1]).clone())
+        return f
+
+    hs = [m.register_forward_hook(hook(n)) for n, m in targets]
+    with torch.no_grad():
+        var.autoregressive_infer_cfg(B=2, label_B=torch.tensor([207, 980]), cfg=1.5, top_k=900, top_p=0.96,
+                                     g_seed=0, more_smooth=False)
+    for h in hs:
+        h.remove()
+    seen = set()
+    gl = torch.Generator().manual_seed(2)
+    for n, m in targets:
+        key = (m.in_features, m.out_features)
+        if key in seen or n not in captured:
+            continue
+        seen.add(key)
+        x, y = captured[n]
+        assert torch.isfinite(x).all() and torch.isfinite(y).all(), n
+        rows = torch.linspace(0, x.shape[0] - 1, 64).round().long()
+        xs = x[rows].to(torch.bfloat16).float()
+        W = m.weight.detach()[:64].to(torch.bfloat16).float()
+        b = None if m.bias is None else m.bias.detach()[:64].to(torch.bfloat16).float()
+        A = (torch.rand(r, m.in_features, generator=gl) * 2 - 1) / math.sqrt(m.in_features)
+        B = torch.randn(64, r, generator=gl) * 0.02
+        s = 16.0 / r
+        y64 = xs.double() @ W.double().T + (0 if b is None else b.double()) + s * ((xs.double() @ A.double().T) @ B.double().T)
+        tag = f"lin_{m.in_features}x{m.out_features}"
+        recs[tag + "/x"] = xs.numpy()
+        recs[tag + "/W"] = W.numpy()
+        if b is not None:
+            recs[tag + "/b"] = b.numpy()
+        recs[tag + "/A"] = A.numpy()
+        recs[tag + "/B"] = B.numpy()
+        recs[tag + "/y"] = y64.numpy()
+        recs[tag + "/y_module"] = y[rows][:, :64].numpy()      # the VAR module's own fp32 output
+        recs[tag + "/meta"] = np.array([x.shape[0], s], np.float64)
+    np.savez_compressed(OUT / "g8_var.npz", **recs)
+    return len(recs)
+
+
 def gen_es_tail(u):
     """unifed_es.py:227-281 composed from the reference's own functions (unifed_es.py itself does
     not import here: wandb / lovely_tensors / peft are absent)."""
@@ -347,6 +454,8 @@ def gen_lora(u):
 if __name__ == "__main__":
     u = load_reference()
     torch.set_num_threads(1)
-    for fn in (gen_eps, gen_fitness, gen_update, gen_indices, gen_sampling_info, gen_es_tail, gen_lora):
+    for fn in (gen_eps, gen_fitness, gen_update, gen_indices, gen_sampling_info, gen_es_tail, gen_lora,
+               gen_member_eval_injection):
         print(fn.__name__, fn(u))
     print("gen_s_aggregation", gen_s_aggregation())
+    print("gen_var", gen_var())

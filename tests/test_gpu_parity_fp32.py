@@ -1,0 +1,159 @@
+"""bf16 member-eval (the build) vs an fp32 restatement of the reference's per-member path, with
+REFERENCE-GENERATED noise injected (north_star: "perturbed activations, rewards and LoRA updates
+within a stated bf16/fp32 tolerance, verified by injecting reference-generated noise").
+
+Setup: the tiny Sana / DC-AE / CLIP stack of tests/test_gpu_engine.py (same architecture as the
+1.6B model, seeded synthetic weights), pop 8, egg rank 1, antithetic; factors captured from the
+reference's own EggRollNoiser (tests/golden/g10, made by make_golden.py from utills.py).
+  build:  perturb kernel -> one population-batched bf16 forward on the HIP kernels -> batched
+          bf16 rewards -> S (es_step.aggregate_member_rewards) -> fitness kernel -> ranks
+  fp32:   theta_k = theta + sigma * eps_k (reference eps) -> oracle/member_eval_fp32.py per member
+          (PEFT LoRA formula, same weights upcast, fp16 SCM casts of models/SanaSprint.py) -> S
+Measured drift per tensor is asserted against the bounds below; ranks are
+compared as the exact order and as Kendall's tau.  Two noise scales: sigma = 1e-2 (the BASELINE
+configs) and 0.5 (member differences well above the bf16 noise floor).
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from hyperscalees_t2i_amd import kernels as K
+from hyperscalees_t2i_amd.backend import SanaBackend, SanaConfig
+from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params
+from hyperscalees_t2i_amd.es_step import aggregate_member_rewards
+from hyperscalees_t2i_amd.lora import LoRALinear
+from hyperscalees_t2i_amd.rewards import RewardModels
+from hyperscalees_t2i_amd.sana import SanaArch
+from oracle import eggroll_oracle as O
+from oracle import member_eval_fp32 as R
+
+pytestmark = pytest.mark.gpu
+
+TINY = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=2,
+                cross_attention_head_dim=64, caption_channels=2304)
+
+# Stated tolerances (bf16 storage / MFMA inputs vs fp32; measured values in DESIGN.md §3).
+# s0 = the BASELINE noise scale sigma = 1e-2; s1 = sigma 0.5, where the perturbed network amplifies
+# the bf16 rounding with depth (measured: 0.3 % at the first linears -> 21 % at block 0's attn2 out)
+# while the member spread of S (1.5) still dwarfs |dS| — so ranks must agree exactly there.
+BOUNDS = {
+    "s0": {"lora_rel": 1.5e-2,   # every LoRA'd / frozen linear output, ||y - y32|| / ||y32|| (measured 0.6 %)
+           "eps_rel": 1.5e-2,    # transformer output (0.57 %)
+           "image_rel": 3e-2,    # decoded image (1.2 %)
+           "reward_abs": 0.1,    # per-image combined reward, PickScore scale exp(logit_scale) = 14.3 (0.043)
+           "S_abs": 0.1},        # S[k, j] (0.040)
+    "s1": {"lora_rel": 0.35, "eps_rel": 0.1, "image_rel": 0.15, "reward_abs": 0.15, "S_abs": 0.1},
+}
+KEYS = ("lora_rel", "eps_rel", "image_rel", "reward_abs", "S_abs")
+
+
+def kendall_tau(a, b):
+    n = len(a)
+    c = d = 0
+    for i in range(n):
+        for j in range(i + 1, n):
+            s = np.sign(a[i] - a[j]) * np.sign(b[i] - b[j])
+            c += s > 0
+            d += s < 0
+    return (c - d) / max(1, n * (n - 1) // 2)
+
+
+def rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def stack(dev):
+    cfg = SanaConfig(width_latent=4, height_latent=4, batches_per_gen=2, arch=TINY,
+                     vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
+    be = SanaBackend(str(dev), cfg)
+    be.init_and_attach_lora()
+    rewards = RewardModels.build(dev, tiny=True)
+    return be, rewards, R.Rewards32(rewards)
+
+
+@pytest.mark.parametrize("case", ["s0", "s1"])
+def test_member_eval_bf16_vs_fp32_with_reference_noise(stack, dev, golden, case):
+    be, rewards, rewards32 = stack
+    g = golden("g10_member_eval_injection.npz")
+    params, shapes = be.collect_lora_params()
+    assert [tuple(s) for s in shapes] == [tuple(s) for s in g["shapes"].tolist()]
+    sigma = float(g[f"{case}/sigma"])
+    pop = 8
+    theta = flatten_params(params).to(dev)
+    noiser = EggRollNoiser(shapes, sigma=sigma, lr_scale=0.1, rank=1, use_antithetic=True)
+    fac = torch.from_numpy(noiser.layout.pack_factors(g[f"{case}/factors"])).to(dev)
+    eps_ref = torch.from_numpy(g[f"{case}/eps"]).to(dev)
+    tp = noiser.perturb(theta, fac, pop, 0, pop)
+    assert torch.equal(tp, theta[None] + sigma * eps_ref)          # injected noise reproduced bit-exactly
+
+    seed, gs = 5, 4.5
+    info = be.step_sampling_info(seed)
+    flat, m = info["flat_ids"], info["m"]
+    B = len(flat)
+    pe, am = be._gather(flat)
+
+    # ---- build path (bf16, population-batched HIP kernels), LoRA outputs captured by hooks
+    lin_out, tr_out = [], []
+    hooks = [mod.register_forward_hook(lambda _m, _i, o: lin_out.append(o)) for mod in be.es_model.transformer.modules()
+             if isinstance(mod, LoRALinear)]
+    hooks.append(be.es_model.transformer.register_forward_hook(lambda _m, _i, o: tr_out.append(o)))
+    try:
+        imgs = be.generate_population(flat, seed, gs, tp)
+    finally:
+        for h in hooks:
+            h.remove()
+    j_of = torch.tensor([info["pid_to_j"][p] for p in flat], device=dev)
+    feats = rewards.prompt_features(info["unique_texts"])
+    rew = rewards.score(imgs, j_of.repeat(pop), feats)
+    S, _ = aggregate_member_rewards(rew, flat, info["pid_to_j"], pop, m)
+    fit = K.fitness(S, True)
+
+    # ---- fp32 restatement, member by member (the reference loop)
+    lat = be.es_model._latents(B, seed, 4, 4)
+    feats32 = rewards32.prompt_features(info["unique_texts"])
+    S32 = torch.empty((pop, m), device=dev)
+    worst = {k: 0.0 for k in KEYS}
+    worst["reward_model_abs"] = 0.0   # bf16 reward nets on the fp32 image vs fp32 reward nets (diagnostic)
+    per_lin = {}
+    lin_names = [n for n, mod in be.es_model.transformer.named_modules() if isinstance(mod, LoRALinear)]
+    for k in range(pop):
+        rec = []
+        theta_k = theta + sigma * eps_ref[k]
+        eps32, img32 = R.generate_fp32(be.es_model, theta_k, pe, am, lat, gs, rec)
+        rw32 = rewards32.score(img32, j_of, feats32)
+        rw_mix = rewards.score(img32.to(torch.bfloat16), j_of, feats)
+        worst["reward_model_abs"] = max(worst["reward_model_abs"],
+                                        float((rw_mix["combined"] - rw32["combined"]).abs().max()))
+        S32[k] = aggregate_member_rewards(rw32, flat, info["pid_to_j"], 1, m)[0][0]
+        assert len(rec) == len(lin_out)
+        for li, (a, b) in enumerate(zip(lin_out, rec)):
+            a2 = a.reshape(-1, a.shape[-1])
+            a2 = a2.view(pop, -1, a2.shape[-1])[k]
+            e = rel(a2, b.reshape(-1, b.shape[-1]))
+            per_lin[li] = max(per_lin.get(li, 0.0), e)
+            worst["lora_rel"] = max(worst["lora_rel"], e)
+        worst["eps_rel"] = max(worst["eps_rel"], rel(tr_out[0][k * B:(k + 1) * B], eps32))
+        worst["image_rel"] = max(worst["image_rel"], rel(imgs[k * B:(k + 1) * B], img32))
+        worst["reward_abs"] = max(worst["reward_abs"],
+                                  float((rew["combined"][k * B:(k + 1) * B] - rw32["combined"]).abs().max()))
+    worst["S_abs"] = float((S - S32).abs().max())
+    sc = fit["scores"].cpu().numpy()
+    sc32, _, _ = O.ref_promptnorm(S32.cpu().numpy())
+    spread = float(S32.std(0).mean())
+    order, order32 = np.argsort(sc, kind="stable"), np.argsort(sc32, kind="stable")
+    report = {"case": case, "sigma": sigma, **{k: round(v, 6) for k, v in worst.items()},
+              "S_member_spread": round(spread, 6), "rank_exact": bool(np.array_equal(order, order32)),
+              "kendall_tau": round(float(kendall_tau(sc, sc32)), 4),
+              "best_same": bool(order[-1] == order32[-1]), "worst_same": bool(order[0] == order32[0])}
+    print("[fp32-parity]", json.dumps(report))
+    print("[fp32-parity] per-linear rel", case, {lin_names[i] if i < len(lin_names) else i: round(v, 5)
+                                                 for i, v in per_lin.items()})
+    for k, b in BOUNDS[case].items():
+        assert worst[k] <= b, (k, worst[k], b, report)
+    if case == "s1":   # member signal >> bf16 noise: the fitness order must be the reference's
+        assert report["rank_exact"] and report["kendall_tau"] == 1.0, report
+    else:              # |dS| ~ member spread at sigma 1e-2 on random weights: rank agreement is partial
+        assert report["kendall_tau"] >= 0.6, report

@@ -95,3 +95,14 @@ def test_mix_weights_forms():
     assert split_mix_weights([0, 0, 0, 1]) == (0.0, 0.0, 0.0, 1.0)
     with pytest.raises(ValueError):
         split_mix_weights((1.0, 2.0))
+
+
+def test_var_d16_layout_matches_reference_module_tree(golden):
+    """model_shapes.var_d16_lora_shapes == the theta layout make_golden.py walked out of the
+    reference's VAR_models (PEFT suffix matching of unifed_es.py:406's targets)."""
+    from hyperscalees_t2i_amd.model_shapes import var_d16_lora_shapes
+    g8 = golden("g8_var.npz")
+    assert [tuple(s) for s in g8["shapes"].tolist()] == var_d16_lora_shapes()
+    names = str(g8["names"]).split("\x1f")
+    assert len(names) == 82 and names[0] == "blocks.0.attn.mat_qkv" and names[-1] == "head"
+    assert sum(a * b for a, b in var_d16_lora_shapes()) == 1_540_096
