@@ -168,6 +168,22 @@ class SanaBackend(ESBackend):
                "base_model_name_or_path": self.cfg.model_name, "bias": "none", "task_type": None}
         (save_dir / "adapter_config.json").write_text(json.dumps(cfg, indent=2))
 
+    def load_lora(self, save_dir: Path) -> None:
+        """Inverse of save_lora (resume; the reference is write-only): copy the adapter tensors of
+        save_dir/adapter_model.safetensors back into the LoRA parameters.  Every trainable parameter
+        must be present with its shape, and no extra key may exist (ValueError otherwise)."""
+        from safetensors.torch import load_file
+        tensors = load_file(str(Path(save_dir) / "adapter_model.safetensors"))
+        want = {f"base_model.model.{n}": p for n, p in self.es_model.transformer.named_parameters() if p.requires_grad}
+        if set(tensors) != set(want):
+            raise ValueError(f"adapter keys differ: missing {sorted(set(want) - set(tensors))[:3]}, "
+                             f"unexpected {sorted(set(tensors) - set(want))[:3]}")
+        with torch.no_grad():
+            for k, p in want.items():
+                if tuple(tensors[k].shape) != tuple(p.shape):
+                    raise ValueError(f"{k}: shape {tuple(tensors[k].shape)} != {tuple(p.shape)}")
+                p.copy_(tensors[k].to(p.device, p.dtype))
+
     def step_sampling_info(self, seed: int) -> Dict[str, Any]:
         """es_backend.py:234-263 (bit-exact indices: np.random.RandomState(seed).choice)."""
         P = int(self.base_prompt_embeds.shape[0])

@@ -308,3 +308,14 @@ def save_latest_checkpoint(*, theta, backend, lora_params, lora_shapes, save_dir
                "summary_mean_reward": stats.get("summary/mean_reward", float("nan")), "backend": backend.name,
                **extra_meta}
     torch.save(payload, meta_path)
+
+
+def load_latest_checkpoint(meta_path: Path, device=None) -> Tuple[torch.Tensor, Dict[str, Any]]:
+    """Resume (new; the reference only writes checkpoints): the meta .pt written by
+    save_latest_checkpoint, loaded with torch.load(weights_only=True) — nothing in the file is
+    executed.  Returns (theta_latest on `device`, the rest of the payload)."""
+    meta = torch.load(Path(meta_path), map_location="cpu", weights_only=True)
+    theta = meta.pop("theta_latest")
+    if not torch.is_tensor(theta) or theta.ndim != 1:
+        raise ValueError(f"{meta_path}: theta_latest must be a 1-D tensor")
+    return (theta.to(device) if device is not None else theta), meta

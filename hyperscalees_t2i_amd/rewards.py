@@ -10,8 +10,9 @@ unifed_es.py:175-191):
   combined       = w_aes*aes + w_txt*txt + w_noart*noart + w_pick*pick
 Images reach the reward models as the reference's PIL path would deliver them: VAE output ->
 (x/2+0.5).clamp(0,1) -> *255 rounded to uint8 (PixArtImageProcessor.postprocess) -> CLIP fast
-processor: bicubic antialiased resize of the shortest edge to 224 -> center crop -> /255 ->
-CLIP mean/std normalisation.  Done here as tensor ops on the device.
+processor (PIL backend): Pillow's fixed-point bicubic resize of the shortest edge to 224 -> center
+crop -> /255 -> CLIP mean/std normalisation.  Done here as tensor ops on the device, bit-exact
+with Pillow's resampling (tests/test_checkpoint_rewards.py).
 
 Weights: the hub checkpoints (openai/clip-vit-base-patch32, yuvalkirstain/PickScore_v1) are not
 available offline, so both models are built from their published configs with seeded random
@@ -25,6 +26,7 @@ import zlib
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -70,13 +72,74 @@ def postprocess_uint8(images: torch.Tensor) -> torch.Tensor:
     return torch.round((images.float() / 2 + 0.5).clamp(0, 1) * 255.0)
 
 
-def clip_preprocess(u8: torch.Tensor, size: int = 224) -> torch.Tensor:
-    """CLIP fast image processor on uint8-valued images [n,3,H,W] -> normalized [n,3,224,224]."""
+_PIL_PRECISION_BITS = 32 - 8 - 2  # Pillow's Resample.c fixed point for 8-bit images
+_COEF_CACHE: Dict[tuple, torch.Tensor] = {}
+
+
+def _pil_bicubic_coeffs(in_size: int, out_size: int) -> np.ndarray:
+    """Pillow's precompute_coeffs + normalize_coeffs_8bpc for the BICUBIC filter (a = -0.5):
+    the integer (22-bit fixed-point) weights as a dense [out_size, in_size] matrix."""
+    def bicubic(x):
+        a = -0.5
+        x = abs(x)
+        if x < 1.0:
+            return ((a + 2.0) * x - (a + 3.0)) * x * x + 1
+        if x < 2.0:
+            return (((x - 5) * x + 8) * x - 4) * a
+        return 0.0
+    scale = in_size / out_size
+    filterscale = max(scale, 1.0)
+    support = 2.0 * filterscale
+    mat = np.zeros((out_size, in_size), np.float64)
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        ss = 1.0 / filterscale
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        w = [bicubic((x + xmin - center + 0.5) * ss) for x in range(xmax)]
+        ww = sum(w)
+        for x in range(xmax):
+            k = w[x] / ww if ww != 0.0 else w[x]
+            mat[xx, xmin + x] = int(-0.5 + k * (1 << _PIL_PRECISION_BITS)) if k < 0 else \
+                int(0.5 + k * (1 << _PIL_PRECISION_BITS))
+    return mat
+
+
+def _pil_pass(x: torch.Tensor, coeffs: torch.Tensor) -> torch.Tensor:
+    """One separable 8-bit pass over the last dim: clip8(sum(in * k_int) + 2^21) >> 22.  fp64
+    holds every partial sum exactly (|sum| < 2^36), so the dense matmul is the integer result."""
+    acc = torch.matmul(x, coeffs.t()) + float(1 << (_PIL_PRECISION_BITS - 1))
+    return torch.floor(acc / float(1 << _PIL_PRECISION_BITS)).clamp_(0.0, 255.0)
+
+
+def pil_bicubic_resize(u8: torch.Tensor, out_h: int, out_w: int) -> torch.Tensor:
+    """PIL Image.resize((out_w, out_h), BICUBIC) of uint8-valued images [n, c, H, W] (any float dtype),
+    bit-exact: horizontal pass first, each pass rounded and clipped to 8 bits (Resample.c)."""
     n, c, h, w = u8.shape
-    s = size / min(h, w)
-    nh, nw = max(size, round(h * s)), max(size, round(w * s))
-    x = F.interpolate(u8.float(), size=(nh, nw), mode="bicubic", antialias=True, align_corners=False)
-    x = torch.round(x).clamp(0, 255)
+    x = u8.to(torch.float64)
+    for dim_in, dim_out, horiz in ((w, out_w, True), (h, out_h, False)):
+        if dim_in == dim_out:
+            continue
+        key = (dim_in, dim_out, str(x.device))
+        cf = _COEF_CACHE.get(key)
+        if cf is None:
+            cf = _COEF_CACHE[key] = torch.from_numpy(_pil_bicubic_coeffs(dim_in, dim_out)).to(x.device)
+        x = _pil_pass(x, cf) if horiz else _pil_pass(x.transpose(-1, -2), cf).transpose(-1, -2)
+    return x
+
+
+def clip_preprocess(u8: torch.Tensor, size: int = 224) -> torch.Tensor:
+    """transformers CLIPImageProcessor (PIL backend, rewards.py:86-90 / 133-147) on uint8-valued
+    images [n,3,H,W] -> normalized [n,3,224,224]: BICUBIC resize of the short edge to `size`
+    (bit-exact Pillow resampling), center crop, /255, CLIP mean/std."""
+    n, c, h, w = u8.shape
+    # transformers get_resize_output_image_size(default_to_square=False): the short edge becomes
+    # `size`, the long edge int(size * long / short) (truncation)
+    if h <= w:
+        nh, nw = size, int(size * w / h)
+    else:
+        nh, nw = int(size * h / w), size
+    x = pil_bicubic_resize(u8, nh, nw).float()
     top, left = (nh - size) // 2, (nw - size) // 2
     x = x[:, :, top:top + size, left:left + size] / 255.0
     mean = torch.tensor(CLIP_MEAN, device=x.device).view(1, 3, 1, 1)

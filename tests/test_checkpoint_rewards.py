@@ -1,0 +1,104 @@
+"""Checkpoint format (es_backend.py:1025-1054) and reward preprocessing (rewards.py:86-90,133-147)
+parity, CPU.
+
+* save_latest_checkpoint writes theta into the LoRA params, a PEFT-style adapter dir
+  (adapter_model.safetensors with keys base_model.model.<module>.lora_{A,B}.weight + adapter_config.json)
+  and the meta .pt with theta_latest; theta_latest loads with torch.load(weights_only=True) and the
+  adapter reproduces theta through the reference's unflatten order; load_lora / load_latest_checkpoint
+  resume it.
+* clip_preprocess(postprocess_uint8(x)) vs transformers' CLIPImageProcessor on the PIL images the
+  reference builds (PixArtImageProcessor.postprocess -> PIL).  torchvision is absent in this image, so
+  transformers runs its PIL backend (CLIPImageProcessorPil): Pillow BICUBIC resize of the short edge
+  to 224, center crop 224, /255, CLIP mean/std.  The build restates Pillow's fixed-point separable
+  resampling on the device (rewards.pil_bicubic_resize): BIT-EXACT, square and non-square sizes.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from hyperscalees_t2i_amd.backend import SanaBackend, SanaConfig
+from hyperscalees_t2i_amd.es import flatten_params
+from hyperscalees_t2i_amd.es_step import load_latest_checkpoint, save_latest_checkpoint
+from hyperscalees_t2i_amd.pipeline import to_pil
+from hyperscalees_t2i_amd.rewards import clip_preprocess, postprocess_uint8
+from hyperscalees_t2i_amd.sana import SanaArch
+
+TINY = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=2,
+                cross_attention_head_dim=64, caption_channels=2304)
+
+
+@pytest.fixture(scope="module")
+def backend_cpu():
+    cfg = SanaConfig(width_latent=4, height_latent=4, arch=TINY, vae_widths=(16, 32, 32, 64, 64, 64),
+                     vae_layers=(1, 1, 1, 1, 1, 1))
+    be = SanaBackend("cpu", cfg)
+    be.init_and_attach_lora()
+    return be
+
+
+def test_checkpoint_roundtrip_peft_format(backend_cpu, tmp_path):
+    from safetensors.torch import load_file
+    be = backend_cpu
+    params, shapes = be.collect_lora_params()
+    theta = torch.randn(sum(p.numel() for p in params), generator=torch.Generator().manual_seed(3))
+    save_latest_checkpoint(theta=theta, backend=be, lora_params=params, lora_shapes=shapes,
+                           save_dir=tmp_path / "lora_latest", meta_path=tmp_path / "latest_lora_meta.pt", epoch=7,
+                           stats={"summary/mean_reward": 0.25}, extra_meta={"run_name": "r", "wandb_project": "p"})
+    ad = load_file(str(tmp_path / "lora_latest" / "adapter_model.safetensors"))
+    names = [n for n, p in be.es_model.transformer.named_parameters() if p.requires_grad]
+    assert list(ad) and set(ad) == {f"base_model.model.{n}" for n in names}
+    assert all(k.endswith((".lora_A.weight", ".lora_B.weight")) for k in ad)
+    # the adapter tensors, flattened in parameter order, ARE theta (utills.py:141-162 layout)
+    assert torch.equal(torch.cat([ad[f"base_model.model.{n}"].reshape(-1) for n in names]), theta)
+    cfg = json.loads((tmp_path / "lora_latest" / "adapter_config.json").read_text())
+    assert cfg["peft_type"] == "LORA" and cfg["r"] == 2 and cfg["lora_alpha"] == 8
+    assert cfg["target_modules"] == be.cfg.lora_target_modules
+    th, meta = load_latest_checkpoint(tmp_path / "latest_lora_meta.pt")
+    assert torch.equal(th, theta) and meta["epoch"] == 7 and meta["backend"] == be.name
+    assert meta["summary_mean_reward"] == 0.25 and meta["run_name"] == "r"
+    # resume: scramble the params, reload the adapter dir -> theta again
+    with torch.no_grad():
+        for p in params:
+            p.zero_()
+    be.load_lora(tmp_path / "lora_latest")
+    assert torch.equal(flatten_params(params), theta)
+
+
+def test_load_lora_rejects_foreign_adapter(backend_cpu, tmp_path):
+    from safetensors.torch import save_file
+    (tmp_path / "x").mkdir()
+    save_file({"base_model.model.nope.lora_A.weight": torch.zeros(2, 2)}, str(tmp_path / "x" / "adapter_model.safetensors"))
+    with pytest.raises(ValueError):
+        backend_cpu.load_lora(tmp_path / "x")
+
+
+def _images(n, H, W, seed):
+    g = torch.Generator().manual_seed(seed)
+    base = torch.nn.functional.interpolate(torch.rand(n, 3, max(2, H // 16), max(2, W // 16), generator=g) * 2 - 1,
+                                           size=(H, W), mode="bilinear", align_corners=False)
+    return (base + 0.15 * torch.randn(n, 3, H, W, generator=g)).clamp(-1.1, 1.1)
+
+
+@pytest.mark.parametrize("H,W", [(128, 128), (256, 256), (512, 512), (224, 336), (300, 200), (97, 301)])
+def test_clip_preprocess_matches_transformers_processor(H, W):
+    from transformers import CLIPImageProcessorPil
+    proc = CLIPImageProcessorPil()
+    x = _images(3, H, W, H * 7 + W)
+    ours = clip_preprocess(postprocess_uint8(x)).numpy()
+    ref = proc(images=to_pil(x), return_tensors="pt")["pixel_values"].numpy()
+    assert ours.shape == ref.shape == (3, 3, 224, 224)
+    assert np.array_equal(ours, ref), (H, W, float(np.abs(ours - ref).max()))
+
+
+@pytest.mark.gpu
+def test_clip_preprocess_on_device_1024(dev):
+    """The on-device path at the benchmark resolution (1024 px), bit-exact vs the HF processor."""
+    from transformers import CLIPImageProcessorPil
+    x = _images(4, 1024, 1024, 11)
+    ref = CLIPImageProcessorPil()(images=to_pil(x), return_tensors="pt")["pixel_values"].numpy()
+    ours = clip_preprocess(postprocess_uint8(x.to(dev).to(torch.bfloat16).float())).cpu().numpy()
+    ref2 = CLIPImageProcessorPil()(images=to_pil(x.to(torch.bfloat16).float()), return_tensors="pt")["pixel_values"]
+    assert np.array_equal(ours, ref2.numpy())
+    assert ref.shape == ours.shape
