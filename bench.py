@@ -228,9 +228,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline
-        cpu = cpu_baseline.run(pop=pop, budget_s=15.0)
-        cpu.pop("es_breakdown_s", None)
-        cpu.pop("wall_s", None)
+        cpu = cpu_baseline.run()
+        log(f"cpu baseline: {cpu['value']:.4g} member-evals/s on {cpu['cores']} threads ({cpu.pop('wall_s'):.1f}s)")
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "member-evals/s", "n_gpus": world, "steps": args.steps,
