@@ -72,13 +72,21 @@ def parse():
 
 
 def dist_setup(args):
+    """One process per GPU (torchrun env).  RCCL ("nccl") by default; EGGROLL_DIST_BACKEND=gloo with
+    EGGROLL_SAME_DEVICE=1 rehearses the N>1 path with every rank on cuda:0 (a 1-GPU box)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("EGGROLL_SAME_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        backend = os.environ.get("EGGROLL_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     return rank, world, local
 
 
