@@ -203,10 +203,17 @@ struct FastGeo {
     }
 };
 
-// eps(v, u) of one base sample from its long factors X (4 positions x R) and the uniform factors
-// broadcast from lane `ln` (W[u * R + q]); reference op order.
+// Uniform factors of the base sample / member held by lane `ln`, broadcast once (NU * R SGPRs).
+template <int NW>
+__device__ __forceinline__ void bcast_all(float (&wb)[NW], const float (&W)[NW], int ln) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w) wb[w] = bcast(W[w], ln);
+}
+
+// eps(v, u) of one base sample from its long factors X (4 positions x R) and its broadcast uniform
+// factors wb[u * R + q]; reference op order.
 template <int KIND, int R, int NU>
-__device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&W)[NU * R], int v, int u, int ln,
+__device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&wb)[NU * R], int v, int u,
                                           float sqrt_r) {
 #pragma clang fp contract(off)
     if constexpr (KIND == T_VEC4) {
@@ -216,7 +223,7 @@ __device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&W)
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const float x = f4(X[(v * R + q) >> 2], (v * R + q) & 3);
-            const float w = bcast(W[u * R + q], ln);
+            const float w = wb[u * R + q];
             const float pr = KIND == T_WIDE ? w * x : x * w;  // a * b
             acc = q == 0 ? pr : acc + pr;
         }
@@ -226,9 +233,12 @@ __device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&W)
 
 // members / base samples whose long-factor loads are in flight together: 8 float4 loads per
 // thread whatever the rank (rank 4 at 8 samples needed 228 VGPRs and halved the occupancy)
-template <int KIND, int R>
+#ifndef EGG_UPD_PGRP1
+#define EGG_UPD_PGRP1 8
+#endif
+template <int KIND, int R, bool UPD = false>
 struct PGrp {
-    static constexpr int value = (KIND == T_VEC4 || R == 1) ? 8 : 8 / R;
+    static constexpr int value = (KIND == T_VEC4 || R == 1) ? (UPD ? EGG_UPD_PGRP1 : 8) : 8 / R;
 };
 
 // ------------------------------------------------------------------------------------
@@ -254,13 +264,15 @@ __device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, co
     const int64_t xo = G::x_off(mt, R) + p0 * (KIND == T_VEC4 ? 1 : R);
     const int64_t uo = G::u_off(mt, R);
     for (int g = 0; g < n_members; g += 64) {
-        // lane l: member g+l's uniform factors
+        // lane l: member g+l's base sample, sign and uniform factors
         float W[NW];
+        int jl;
+        float sl;
         {
             int64_t jb;
-            float sg;
-            member_to_base(member_lo + g + lane, pop, antithetic, jb, sg);
+            member_to_base(member_lo + g + lane, pop, antithetic, jb, sl);
             const bool mok = g + lane < n_members;
+            jl = mok ? (int)jb : 0;
 #pragma unroll
             for (int w = 0; w < NW; ++w) W[w] = (KIND == T_VEC4 || !mok) ? 1.0f : factors[jb * ld_f + uo + w];
         }
@@ -270,9 +282,7 @@ __device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, co
             float4 X[PG][NX];
 #pragma unroll
             for (int t = 0; t < PG; ++t) {
-                int64_t j;
-                float sgn;
-                member_to_base(member_lo + g + i0 + t, pop, antithetic, j, sgn);
+                const int64_t j = __builtin_amdgcn_readlane(jl, (i0 + t) & 63);
                 const bool lok = ok && (i0 + t < n);
 #pragma unroll
                 for (int c = 0; c < NX; ++c)
@@ -281,15 +291,15 @@ __device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, co
 #pragma unroll
             for (int t = 0; t < PG; ++t) {
                 if (i0 + t >= n) break;
-                int64_t j;
-                float sgn;
-                member_to_base(member_lo + g + i0 + t, pop, antithetic, j, sgn);
+                const float sgn = bcast(sl, i0 + t);
+                float wb[NW];
+                bcast_all(wb, W, i0 + t);
                 float4 O[NU];
 #pragma unroll
                 for (int v = 0; v < 4; ++v)
 #pragma unroll
                     for (int u = 0; u < NU; ++u) {
-                        const float e = sgn * fast_eps<KIND, R, NU>(X[t], W, v, u, i0 + t, sqrt_r);
+                        const float e = sgn * fast_eps<KIND, R, NU>(X[t], wb, v, u, sqrt_r);
                         const float th = f4(TH[G::vi(v, u)], G::vc(v, u));
                         float val;
                         if (theta) {
@@ -561,7 +571,7 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
                 }
             }
             const int n = (int)((n_base - g) < 64 ? (n_base - g) : 64);
-            constexpr int PG = PGrp<KIND, R>::value;
+            constexpr int PG = PGrp<KIND, R, true>::value;
             for (int j0 = 0; j0 < n; j0 += PG) {
                 float4 X[PG][NX];
 #pragma unroll
@@ -574,6 +584,8 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
                 for (int t = 0; t < PG; ++t) {
                     if (j0 + t >= n) break;
                     const float cj = bcast(C, j0 + t);
+                    float wb[NW];
+                    bcast_all(wb, W, j0 + t);
 #pragma unroll
                     for (int v = 0; v < 4; ++v)
 #pragma unroll
@@ -581,9 +593,9 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
                             if constexpr (KIND == T_VEC4) {
                                 acc[v][u] = acc[v][u] + cj * f4(X[t][0], v);
                             } else if constexpr (R == 1) {
-                                acc[v][u] = acc[v][u] + bcast(W[u], j0 + t) * f4(X[t][0], v);
+                                acc[v][u] = acc[v][u] + wb[u] * f4(X[t][0], v);
                             } else {
-                                const float e = fast_eps<KIND, R, NU>(X[t], W, v, u, j0 + t, sqrt_r);
+                                const float e = fast_eps<KIND, R, NU>(X[t], wb, v, u, sqrt_r);
                                 acc[v][u] = acc[v][u] + cj * e;
                             }
                         }
