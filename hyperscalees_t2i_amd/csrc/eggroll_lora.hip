@@ -1151,14 +1151,18 @@ static int launch_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, c
 }
 
 // ------------------------------------------------------------------------------------
-// Implicit-GEMM 3x3 convolution (stride 1, zero pad 1), NHWC bf16, on the 8-phase 256x256 template.
+// Implicit-GEMM 3x3 convolution (stride 1, zero pad 1), NHWC bf16, on the 8-phase template.
 // The DC-AE decoder's ResBlock convs (models/SanaSprint.py:157-160 -> diffusers AutoencoderDC):
 //   GEMM rows    = "super-pixels" of PX horizontally adjacent output pixels (M' = B*H*W/PX)
 //   GEMM columns = PX * Cout (the PX pixels' output channels, contiguous in NHWC)
 //   GEMM K       = 3 * (PX+2) taps * Cin: tap (ty, tx) reads input pixel (y+ty-1, x0+tx-1) of the
 //                  super-pixel whose first pixel is x0; K-tile kt = (tap, 64-channel slice)
-// PX = 2 serves Cout = 128 with a full 256-column tile (the packed weight is zero where a tap does
-// not touch a pixel: 25 % of the MACs) — the 256x256 tile would otherwise run half empty.
+// Two tile shapes, the same 8-phase schedule and wave tile (128 x 64, 8 waves, BK = 64):
+//   WMW = 2: 256 x 256 (2 x 4 waves) for PX * Cout >= 256.  PX = 2 serves Cout = 128 with a full
+//            256-column tile, but the packed weight is zero where a tap does not touch a pixel
+//            (25 % of the MACs).
+//   WMW = 4: 512 x 128 (4 x 2 waves) for Cout = 128 at PX = 1 — no zero MACs.  The A half-tile is
+//            32 KiB (4 DMAs per wave), the B half-tile 8 KiB (1 DMA); the ring is the whole 160 KiB.
 // A operand: each lane's DMA rows keep ONE byte offset (its pixel, relative to a per-block buffer
 // base) and a tap-validity bit mask; the tap's shift and channel slice go in the wave-uniform
 // soffset, and a tap outside the image turns the lane's offset out of range (0x80000000 >
@@ -1166,14 +1170,32 @@ static int launch_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, c
 // per DMA.  B operand: the packed weight [PX*Cout][3][PX+2][Cin] streams like the GEMM's W.
 // Epilogue: bias through the MFMA addend (one k-step), optional SiLU in fp32, one bf16 rounding.
 // ------------------------------------------------------------------------------------
-struct ConvStage {
-    uint32_t off[2];   // lane byte offset of its pixel's channel chunk, tap (0,0) = pixel - (W+1)
-    uint32_t mask[2];  // bit t set: tap t reads inside the image
+template <int WMW>
+struct G8 {
+    static constexpr int WNW = 8 / WMW, BM = WMW * 128, BN = WNW * 64;
+    static constexpr int HA = BM * 64, HB = BN * 64;  // half-tile region bytes ((BM or BN)/2 rows x 128 B)
+    static constexpr int RA0 = 0, RA1 = HA, RB0 = 2 * HA, RB1 = 2 * HA + HB;
+    static constexpr int BUF = 2 * HA + 2 * HB, LDS = 2 * BUF;
+    static constexpr int NA = HA / 8192, NB = HB / 8192;  // DMAs per wave per half-tile (8 waves x 1 KiB)
+    // glds left in flight when a K-tile retires (the next K-tile's A0, B1, A1 halves; T3/T4 formula)
+    static constexpr int VMC = 2 * NA + NB;
+    static constexpr int CSTAGE = 8 * 128 * 64 * 2;  // epilogue C staging: one 128x64 bf16 tile per wave
+    static_assert(LDS <= 160 * 1024, "ring exceeds the 160 KiB LDS");
 };
 
-template <int PX, int KS>
-__device__ __forceinline__ ConvStage make_conv_stage(int m0, int Mp, int H, int W, int Cin, int h, int wave,
-                                                     int lane) {
+template <int ND>
+struct ConvStage {
+    uint32_t off[ND];   // lane byte offset of its pixel's channel chunk, tap (0,0) = pixel - (W+1)
+    uint32_t mask[ND];  // bit t set: tap t reads inside the image
+};
+template <int ND>
+struct WStage {
+    uint32_t off[ND];
+};
+
+template <int PX, int KS, int ND>
+__device__ __forceinline__ ConvStage<ND> make_conv_stage(int m0, int Mp, int H, int W, int Cin, int h, int wave,
+                                                         int lane) {
     constexpr int TW = PX + KS - 1;
     const int Ho = H + 3 - KS, Ws = (W + 3 - KS) / PX;  // output grid (pad 1)
     // input pixel of a super-pixel row's first output pixel (monotone in the row index)
@@ -1182,12 +1204,12 @@ __device__ __forceinline__ ConvStage make_conv_stage(int m0, int Mp, int H, int 
         return ((int64_t)(yrow / Ho) * H + yrow % Ho) * W + xs * PX;
     };
     const int64_t pin0 = pin(m0);
-    ConvStage s;
+    ConvStage<ND> s;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < ND; ++i) {
         const int j = (i * 8 + wave) * 8 + (lane >> 3);  // region row (as make_stage<true>)
         const int chunk = (lane & 7) ^ (j & 7);
-        const int tr = (j >> 6) * 128 + h * 64 + (j & 63);
+        const int tr = (j >> 6) * 128 + h * 64 + (j & 63);  // wave row wm = j / 64
         const int gr = m0 + tr;
         uint32_t mk = 0;
         int64_t pg = pin0;
@@ -1208,23 +1230,56 @@ __device__ __forceinline__ ConvStage make_conv_stage(int m0, int Mp, int H, int 
     return s;
 }
 
-__device__ __forceinline__ void issue_conv_half(__amdgpu_buffer_rsrc_t rs, const ConvStage& s, int tap, int kbytes,
+// B (weight) half-tile staging with ND DMAs per wave: region row j -> tile column
+// (j / 32) * 64 + h * 32 + j % 32 (wave column wn = j / 32), as make_stage<false>.
+template <int ND>
+__device__ __forceinline__ WStage<ND> make_stage_b(int base_row, int row_max, int64_t ld, int h, int wave, int lane) {
+    WStage<ND> s;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+        const int j = (i * 8 + wave) * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ (j & 7);
+        int gr = base_row + (j >> 5) * 64 + h * 32 + (j & 31);
+        gr = gr < row_max ? gr : row_max;
+        s.off[i] = ((uint32_t)gr * (uint32_t)ld + chunk * 8) * 2;
+    }
+    return s;
+}
+
+template <int ND>
+__device__ __forceinline__ void issue_conv_half(__amdgpu_buffer_rsrc_t rs, const ConvStage<ND>& s, int tap, int kbytes,
                                                 char* region, int wave) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < ND; ++i) {
         const uint32_t v = ((s.mask[i] >> tap) & 1u) ? s.off[i] : 0x80000000u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(region + (i * 8 + wave) * 1024), 16, v, kbytes, 0, 0);
     }
 }
+template <int ND>
+__device__ __forceinline__ void issue_half_n(__amdgpu_buffer_rsrc_t rs, const WStage<ND>& s, int kbytes, char* region,
+                                             int wave) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+        const uint32_t v = s.off[i];  // (a local: hipcc rejects the member access inside the builtin here)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(region + (i * 8 + wave) * 1024), 16, v, kbytes, 0, 0);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N == 6 || N == 9, "add the literal");
+    if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+}
 
 // p8_phase with the DMA supplied by the caller (A: masked conv staging, B: weight staging)
-template <int QA, int QB, int RD, bool VM, class Issue>
+template <class G, int QA, int QB, int RD, bool VM, class Issue>
 __device__ __forceinline__ void p8c_phase(f32x4 (&acc)[8][4], bf16x8 (&a)[4][2], bf16x8 (&b)[2][2], const char* buf,
                                           const int (&oA)[2], const int (&oB)[2], Issue&& issue) {
-    if (RD != 2) p8_read_b(b, buf + (QB ? p8::RB1 : p8::RB0), oB);
-    if (RD != 1) p8_read_a(a, buf + (QA ? p8::RA1 : p8::RA0), oA);
+    if (RD != 2) p8_read_b(b, buf + (QB ? G::RB1 : G::RB0), oB);
+    if (RD != 1) p8_read_a(a, buf + (QA ? G::RA1 : G::RA0), oA);
     issue();
-    if (VM) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (VM) wait_vm<G::VMC>();
     P8_LGKM0_;
     P8_BAR();
     p8_mma<QA, QB, true>(acc, a, b);
@@ -1250,16 +1305,18 @@ __device__ __forceinline__ void store_tile_t_act(f32x4 (&acc)[8][4], char* smem,
     store_tile_t(acc, smem, wave, lane, m0, n0, rbase, cbase, M, N, Y, ldy);
 }
 
-// ResBlock tail fused into conv2's epilogue (NORM): RMSNorm over each pixel's COUT = 256 / PX
-// channels (a 256-column tile holds whole pixels), * w[c] + b[c] + res[row, col], on the fp32
+// ResBlock tail fused into conv2's epilogue (NORM): RMSNorm over each pixel's COUT = BN / PX
+// channels (a tile holds whole pixels: N = BN), * w[c] + b[c] + res[row, col], on the fp32
 // accumulators.  Row sums of squares: 16 values per lane, xor-16/32 shuffles across the wave's 4
-// column lanes, then a [256 rows][4 waves] LDS table for the waves that share a pixel.
-template <int PX>
+// column lanes, then a [BM rows][WNW waves] LDS table for the WPP = COUT / 64 waves that share a
+// pixel, summed in a fixed order.
+template <int PX, int WMW>
 __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float* red, int wm, int wn, int lane, int m0,
                                                       int Mp, float eps, const unsigned short* __restrict__ nw,
                                                       const unsigned short* __restrict__ nb,
                                                       const unsigned short* __restrict__ res) {
-    constexpr int COUT = 256 / PX;
+    constexpr int WNW = 8 / WMW, BN = WNW * 64, COUT = BN / PX, WPP = COUT / 64;
+    static_assert(WPP == 2 || WPP == 4, "a pixel spans 2 or 4 waves");
     const int rl = lane & 15, cg = lane >> 4;
     float ss[8];
 #pragma unroll
@@ -1275,7 +1332,7 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
     }
     if (cg == 0)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) red[(wm * 128 + 16 * i + rl) * 4 + wn] = ss[i];
+        for (int i = 0; i < 8; ++i) red[(wm * 128 + 16 * i + rl) * WNW + wn] = ss[i];
     __syncthreads();
     float wv[4][4], bv[4][4];
 #pragma unroll
@@ -1286,24 +1343,32 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
             wv[j][e] = bf16_to_f32(nw[c]);
             bv[j][e] = nb ? bf16_to_f32(nb[c]) : 0.0f;
         }
+    const int w0 = (wn / WPP) * WPP;  // first wave of this pixel
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int rr = wm * 128 + 16 * i + rl;
-        const float* rp = red + rr * 4;
-        const float tot = PX == 1 ? (rp[0] + rp[1]) + (rp[2] + rp[3]) : rp[(wn >> 1) * 2] + rp[(wn >> 1) * 2 + 1];
+        const float* rp = red + rr * WNW + w0;
+        const float tot = WPP == 4 ? (rp[0] + rp[1]) + (rp[2] + rp[3]) : rp[0] + rp[1];
         const float rs = rsqrtf(tot / COUT + eps);
         int row = m0 + rr;
         row = row < Mp ? row : Mp - 1;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const u16x4 r4 = *reinterpret_cast<const u16x4*>(res + (int64_t)row * 256 + wn * 64 + 16 * j + 4 * cg);
+            const u16x4 r4 = *reinterpret_cast<const u16x4*>(res + (int64_t)row * BN + wn * 64 + 16 * j + 4 * cg);
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[i][j][e] = acc[i][j][e] * rs * wv[j][e] + bv[j][e] + bf16_to_f32(r4[e]);
         }
     }
 }
 
-template <int PX, int ACT, bool NORM = false, int KS = 3>
+template <int WMW, bool NORM>
+constexpr int conv_smem_bytes() {
+    using G = G8<WMW>;
+    constexpr int need = G::CSTAGE + (NORM ? G::BM * G::WNW * 4 : 0);  // RMSNorm table after the C staging
+    return G::LDS > need ? G::LDS : need;
+}
+
+template <int PX, int ACT, bool NORM = false, int KS = 3, int WMW = 2>
 __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* __restrict__ X,
                                                           const unsigned short* __restrict__ Wt,
                                                           const unsigned short* __restrict__ bias, int H, int W,
@@ -1312,29 +1377,31 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
                                                           const unsigned short* __restrict__ nw = nullptr,
                                                           const unsigned short* __restrict__ nb = nullptr,
                                                           const unsigned short* __restrict__ res = nullptr) {
+    using G = G8<WMW>;
     constexpr int TW = PX + KS - 1;
-    __shared__ __attribute__((aligned(16))) char smem[p8::LDS + (NORM ? 256 * 4 * 4 : 0)];
+    __shared__ __attribute__((aligned(16))) char smem[conv_smem_bytes<WMW, NORM>()];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
+    const int wm = wave / G::WNW, wn = wave % G::WNW;
+    const int grp8 = wave >> 2;  // the two staggered wave groups (one wave of each per SIMD)
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
     const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
-    const int tiles_m = (Mp + 255) / 256;
+    const int tiles_m = (Mp + G::BM - 1) / G::BM;
     const int per_group = GROUP_M * tiles_n;
     const int grp = tile / per_group, first_m = grp * GROUP_M;
     const int gsize = (tiles_m - first_m) < GROUP_M ? (tiles_m - first_m) : GROUP_M;
     const int in_grp = tile - grp * per_group;
     const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
-    const int m0 = tm * 256, n0 = tn * 256;
+    const int m0 = tm * G::BM, n0 = tn * G::BN;
     const int64_t K = (int64_t)KS * TW * Cin;
     const int nk = (int)(K / BK);
 
-    const ConvStage sA0 = make_conv_stage<PX, KS>(m0, Mp, H, W, Cin, 0, wave, lane);
-    const ConvStage sA1 = make_conv_stage<PX, KS>(m0, Mp, H, W, Cin, 1, wave, lane);
-    const HalfStage sB0 = make_stage<false>(n0, N - 1, K, 0, wave, lane);
-    const HalfStage sB1 = make_stage<false>(n0, N - 1, K, 1, wave, lane);
+    const ConvStage<G::NA> sA0 = make_conv_stage<PX, KS, G::NA>(m0, Mp, H, W, Cin, 0, wave, lane);
+    const ConvStage<G::NA> sA1 = make_conv_stage<PX, KS, G::NA>(m0, Mp, H, W, Cin, 1, wave, lane);
+    const WStage<G::NB> sB0 = make_stage_b<G::NB>(n0, N - 1, K, 0, wave, lane);
+    const WStage<G::NB> sB1 = make_stage_b<G::NB>(n0, N - 1, K, 1, wave, lane);
     char* const e_buf = smem;
-    char* const o_buf = smem + p8::BUF;
+    char* const o_buf = smem + G::BUF;
     // block base = input pixel of output row m0, minus (W+1); tap (ty, tx) adds (ty*W + tx) pixels in
     // soffset, so every address offset is >= 0
     int64_t pin0;
@@ -1363,51 +1430,52 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
 
     const int cmask = (1 << lcpt) - 1;
     // K-tile t (clamped to the last one, as the GEMM): tap = t >> lcpt, channel slice t & cmask
-    auto A = [&](const ConvStage& s, int t, char* dst) {
+    auto A = [&](const ConvStage<G::NA>& s, int t, char* dst) {
         t = t < nk ? t : nk - 1;
         const int tap = t >> lcpt, ty = tap / TW, tx = tap - ty * TW;
         const int soff = __builtin_amdgcn_readfirstlane(((ty * W + tx) * Cin + (t & cmask) * BK) * 2);
         issue_conv_half(rX, s, tap, soff, dst, wave);
     };
-    auto B = [&](const HalfStage& s, int t, char* dst) {
+    auto B = [&](const WStage<G::NB>& s, int t, char* dst) {
         t = t < nk ? t : nk - 1;
-        issue_half(rW, s, t * (BK * 2), dst, wave);
+        issue_half_n(rW, s, t * (BK * 2), dst, wave);
     };
-    A(sA0, 0, e_buf + p8::RA0);
-    B(sB1, 0, e_buf + p8::RB1);
-    A(sA1, 0, e_buf + p8::RA1);
-    B(sB0, 0, e_buf + p8::RB0);
-    A(sA0, 1, o_buf + p8::RA0);
-    B(sB1, 1, o_buf + p8::RB1);
-    A(sA1, 1, o_buf + p8::RA1);
-    P8_VM6();
+    A(sA0, 0, e_buf + G::RA0);
+    B(sB1, 0, e_buf + G::RB1);
+    A(sA1, 0, e_buf + G::RA1);
+    B(sB0, 0, e_buf + G::RB0);
+    A(sA0, 1, o_buf + G::RA0);
+    B(sB1, 1, o_buf + G::RB1);
+    A(sA1, 1, o_buf + G::RA1);
+    wait_vm<G::VMC>();
     P8_BAR();
-    if (wm == 1) P8_BAR();
+    if (grp8 == 1) P8_BAR();
 
     int t0 = 0;
     for (; t0 + 1 < nk; t0 += 2) {
-        p8c_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + p8::RB0); });
-        p8c_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + p8::RA0); });
-        p8c_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + p8::RB1); });
-        p8c_phase<1, 0, 1, true>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + p8::RA1); });
-        p8c_phase<0, 0, 0, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB0, t0 + 2, e_buf + p8::RB0); });
-        p8c_phase<0, 1, 1, false>(acc, a, b, o_buf, oA, oB, [&] { A(sA0, t0 + 3, o_buf + p8::RA0); });
-        p8c_phase<1, 1, 2, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB1, t0 + 3, o_buf + p8::RB1); });
-        p8c_phase<1, 0, 1, true>(acc, a, b, o_buf, oA, oB, [&] { A(sA1, t0 + 3, o_buf + p8::RA1); });
+        p8c_phase<G, 0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + G::RB0); });
+        p8c_phase<G, 0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + G::RA0); });
+        p8c_phase<G, 1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + G::RB1); });
+        p8c_phase<G, 1, 0, 1, true>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + G::RA1); });
+        p8c_phase<G, 0, 0, 0, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB0, t0 + 2, e_buf + G::RB0); });
+        p8c_phase<G, 0, 1, 1, false>(acc, a, b, o_buf, oA, oB, [&] { A(sA0, t0 + 3, o_buf + G::RA0); });
+        p8c_phase<G, 1, 1, 2, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB1, t0 + 3, o_buf + G::RB1); });
+        p8c_phase<G, 1, 0, 1, true>(acc, a, b, o_buf, oA, oB, [&] { A(sA1, t0 + 3, o_buf + G::RA1); });
     }
     if (t0 < nk) {
-        p8c_phase<0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + p8::RB0); });
-        p8c_phase<0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + p8::RA0); });
-        p8c_phase<1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + p8::RB1); });
-        p8c_phase<1, 0, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + p8::RA1); });
+        p8c_phase<G, 0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + G::RB0); });
+        p8c_phase<G, 0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + G::RA0); });
+        p8c_phase<G, 1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + G::RB1); });
+        p8c_phase<G, 1, 0, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + G::RA1); });
     }
-    if (wm == 0) P8_BAR();
+    if (grp8 == 0) P8_BAR();
     P8_VM0();
     __syncthreads();
     if (bias)
         lora_mfma_addend<0>(acc, lane, m0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, Mp, N);
     if constexpr (NORM) {
-        conv_rmsnorm_epilogue<PX>(acc, reinterpret_cast<float*>(smem + p8::LDS), wm, wn, lane, m0, Mp, eps, nw, nb, res);
+        conv_rmsnorm_epilogue<PX, WMW>(acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane, m0, Mp, eps, nw,
+                                       nb, res);
         store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
     } else {
         store_tile_t_act<ACT>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
@@ -1550,26 +1618,32 @@ int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int
                   (long long)N);
     const int64_t Mp = B * Ho * (Wo / px);
     const int64_t K = ks * (px + ks - 1) * Cin;
-    EGG_CHECK_ARG(Mp < (1ll << 31) && (256 * (px + 1) + 2 * W + 8) * Cin * 2 < (1ll << 30) && N * K * 2 < (1ll << 31),
+    // Cout = 128 at px 1 (3x3): the 512 x 128 tile (no zero MACs); everything else 256 x 256
+    const bool tall = ks == 3 && px == 1 && N == 128;
+    const int64_t BM = tall ? 512 : 256, BN = tall ? 128 : 256;
+    EGG_CHECK_ARG(Mp < (1ll << 31) && (BM * (px + 1) + 2 * W + 8) * Cin * 2 < (1ll << 30) && N * K * 2 < (1ll << 31),
                   "conv_nhwc: sizes exceed the kernel's 32-bit offsets");
     EGG_CHECK_ARG(x && w_packed && y, "conv_nhwc: NULL pointer");
-    const int64_t tiles_m = (Mp + 255) / 256, tiles_n = (N + 255) / 256;
+    const int64_t tiles_m = (Mp + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "conv_nhwc: grid too large");
     int lcpt = 0;
     while ((64ll << lcpt) < Cin) ++lcpt;
     const dim3 grid((unsigned)(tiles_m * tiles_n));
     hipStream_t st = as_stream(stream);
-#define EGG_CONV(PX_, ACT_, KS_)                                                                               \
-    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, ACT_, false, KS_>), grid, dim3(512), 0, st, (const unsigned short*)x, \
-                       (const unsigned short*)w_packed, (const unsigned short*)bias, (int)H, (int)W, (int)Cin, lcpt, \
-                       (int)Mp, (int)N, (int)tiles_n, (unsigned short*)y, 0.0f, nullptr, nullptr, nullptr)
+#define EGG_CONV(PX_, ACT_, KS_, WMW_)                                                                          \
+    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, ACT_, false, KS_, WMW_>), grid, dim3(512), 0, st,                  \
+                       (const unsigned short*)x, (const unsigned short*)w_packed, (const unsigned short*)bias, \
+                       (int)H, (int)W, (int)Cin, lcpt, (int)Mp, (int)N, (int)tiles_n, (unsigned short*)y, 0.0f,   \
+                       nullptr, nullptr, nullptr)
     if (ks == 2) {
-        if (act == 0) EGG_CONV(1, 0, 2);
-        else EGG_CONV(1, 1, 2);
-    } else if (px == 1 && act == 0) EGG_CONV(1, 0, 3);
-    else if (px == 1) EGG_CONV(1, 1, 3);
-    else if (act == 0) EGG_CONV(2, 0, 3);
-    else EGG_CONV(2, 1, 3);
+        if (act == 0) EGG_CONV(1, 0, 2, 2);
+        else EGG_CONV(1, 1, 2, 2);
+    } else if (tall && act == 0) EGG_CONV(1, 0, 3, 4);
+    else if (tall) EGG_CONV(1, 1, 3, 4);
+    else if (px == 1 && act == 0) EGG_CONV(1, 0, 3, 2);
+    else if (px == 1) EGG_CONV(1, 1, 3, 2);
+    else if (act == 0) EGG_CONV(2, 0, 3, 2);
+    else EGG_CONV(2, 1, 3, 2);
 #undef EGG_CONV
     EGG_CHECK_LAUNCH("conv_nhwc");
     return EGGROLL_OK;
@@ -1585,26 +1659,30 @@ int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void
                                  int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
                                  const void* norm_b, const void* res, void* y, void* stream) {
     EGG_CHECK_ARG(px == 1 || px == 2, "conv3x3_rmsnorm_nhwc: px must be 1 or 2 (got %d)", px);
-    EGG_CHECK_ARG(N == 256, "conv3x3_rmsnorm_nhwc: N = px * Cout must be 256 (got %lld)", (long long)N);
+    EGG_CHECK_ARG(N == 256 || (N == 128 && px == 1),
+                  "conv3x3_rmsnorm_nhwc: N = px * Cout must be 256, or 128 at px 1 (got %lld, px %d)", (long long)N, px);
+    const bool tall = N == 128;  // 512 x 128 tile
     EGG_CHECK_ARG(B > 0 && H > 0 && W > 0 && W % px == 0, "conv3x3_rmsnorm_nhwc: bad B/H/W (W %% px == 0 required)");
     EGG_CHECK_ARG(Cin >= 64 && Cin <= 2048 && (Cin & (Cin - 1)) == 0,
                   "conv3x3_rmsnorm_nhwc: Cin=%lld must be a power of two in [64, 2048]", (long long)Cin);
     const int64_t Mp = B * H * (W / px);
-    EGG_CHECK_ARG(Mp < (1ll << 31) && (256 * px + 2 * W + 8) * Cin * 2 < (1ll << 30),
+    const int64_t BM = tall ? 512 : 256;
+    EGG_CHECK_ARG(Mp < (1ll << 31) && (BM * (px + 1) + 2 * W + 8) * Cin * 2 < (1ll << 30),
                   "conv3x3_rmsnorm_nhwc: sizes exceed the kernel's 32-bit offsets");
     EGG_CHECK_ARG(x && w_packed && y && norm_w && res, "conv3x3_rmsnorm_nhwc: NULL pointer");
     EGG_CHECK_ARG(res != y && x != y, "conv3x3_rmsnorm_nhwc: y may not alias x or res");
     int lcpt = 0;
     while ((64ll << lcpt) < Cin) ++lcpt;
-    const dim3 grid((unsigned)((Mp + 255) / 256));
+    const dim3 grid((unsigned)((Mp + BM - 1) / BM));
     hipStream_t st = as_stream(stream);
-#define EGG_CONVN(PX_)                                                                                          \
-    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, 0, true>), grid, dim3(512), 0, st, (const unsigned short*)x,       \
+#define EGG_CONVN(PX_, WMW_)                                                                                    \
+    hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, 0, true, 3, WMW_>), grid, dim3(512), 0, st, (const unsigned short*)x, \
                        (const unsigned short*)w_packed, (const unsigned short*)bias, (int)H, (int)W, (int)Cin, lcpt, \
-                       (int)Mp, 256, 1, (unsigned short*)y, eps, (const unsigned short*)norm_w,                 \
+                       (int)Mp, (int)N, 1, (unsigned short*)y, eps, (const unsigned short*)norm_w,              \
                        (const unsigned short*)norm_b, (const unsigned short*)res)
-    if (px == 1) EGG_CONVN(1);
-    else EGG_CONVN(2);
+    if (tall) EGG_CONVN(1, 4);
+    else if (px == 1) EGG_CONVN(1, 2);
+    else EGG_CONVN(2, 2);
 #undef EGG_CONVN
     EGG_CHECK_LAUNCH("conv3x3_rmsnorm_nhwc");
     return EGGROLL_OK;

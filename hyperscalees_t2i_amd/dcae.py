@@ -10,7 +10,7 @@ shapes and FLOPs (~7.5 TFLOP per 1024^2 image) follow the architecture.
 
 Execution (not one of the ES hot-path kernels): activations stay NHWC
 contiguous; the ResBlocks' dense 3x3 convs run as libeggroll's implicit-GEMM MFMA kernel
-(eggroll_conv3x3_nhwc, conv1's bias + SiLU in its epilogue), the remaining dense convs go to MIOpen
+(eggroll_conv3x3_nhwc, conv1's bias + SiLU in its epilogue; conv2 + RMSNorm + residual in one launch), the remaining dense convs go to MIOpen
 on channels-last views, 1x1 convs to hipBLASLt, and depthwise convs (+SiLU / GLU gate) to
 libeggroll's eggroll_dwconv_nhwc.
 """
@@ -64,10 +64,10 @@ class Conv3x3(nn.Module):
 
 def conv_gemm_px(c: int) -> int:
     """Super-pixel width for libeggroll's implicit-GEMM 3x3 conv at c -> c channels (0: not eligible):
-    2 for c = 128 (fills the 256-column tile), 1 for 256..2048, 0 otherwise (MIOpen)."""
+    1 for 128..2048 (c = 128 runs the 512 x 128 tile), 0 otherwise (MIOpen)."""
     if c < 128 or c > 2048 or c & (c - 1):
         return 0
-    return 2 if c == 128 else 1
+    return 1
 
 
 class ResBlock(nn.Module):
@@ -96,7 +96,7 @@ class ResBlock(nn.Module):
                 self.refresh_packed_weights()
             w1, b1, w2 = self.packed
             h = K.conv3x3_nhwc(x, w1, b1, self.px, "silu")
-            if w2.shape[0] == 256:  # whole pixels per tile: RMSNorm + residual in conv2's epilogue
+            if w2.shape[0] in (128, 256):  # whole pixels per tile: RMSNorm + residual in conv2's epilogue
                 n = self.norm
                 return K.conv3x3_rmsnorm_nhwc(h, w2, None, self.px, n.eps, n.weight, n.bias, x)
             return self.norm(K.conv3x3_nhwc(h, w2, None, self.px), res=x)

@@ -648,7 +648,7 @@ def conv3x3_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.T
 def conv3x3_rmsnorm_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], px: int, eps: float,
                          norm_w: torch.Tensor, norm_b: Optional[torch.Tensor], res: torch.Tensor) -> torch.Tensor:
     """conv3x3_nhwc followed by RMSNorm over channels (* norm_w + norm_b) + res, in one launch
-    (the DC-AE ResBlock tail); px * Cout must be 256."""
+    (the DC-AE ResBlock tail); px * Cout must be 256, or Cout = 128 at px 1 (512 x 128 tile)."""
     _dev(x, "conv3x3_rmsnorm(x)", torch.bfloat16)
     _dev(w_packed, "conv3x3_rmsnorm(w)", torch.bfloat16)
     _dev(norm_w, "conv3x3_rmsnorm(norm_w)", torch.bfloat16)
@@ -656,9 +656,10 @@ def conv3x3_rmsnorm_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional
     x, res = x.contiguous(), res.contiguous()
     B, H, W, Cin = x.shape
     N = w_packed.shape[0]
-    if N != 256 or w_packed.shape[1] != 3 * (px + 2) * Cin or res.shape != (B, H, W, N // px):
+    if (N != 256 and not (N == 128 and px == 1)) or w_packed.shape[1] != 3 * (px + 2) * Cin \
+            or res.shape != (B, H, W, N // px):
         raise ValueError(f"conv3x3_rmsnorm: packed weight {tuple(w_packed.shape)} / res {tuple(res.shape)} do not "
-                         f"match x {tuple(x.shape)}, px={px} (px * Cout must be 256)")
+                         f"match x {tuple(x.shape)}, px={px} (px * Cout must be 256, or 128 at px 1)")
     for t, nm in ((bias, "bias"), (norm_b, "norm_b")):
         if t is not None:
             _dev(t, f"conv3x3_rmsnorm({nm})", torch.bfloat16)

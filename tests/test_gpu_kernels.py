@@ -506,8 +506,8 @@ def test_bias_act_and_resblock(dev):
 
 @pytest.mark.parametrize("c", [64, 128, 256])
 def test_resblock_matches_reference(dev, c):
-    """ResBlock.forward (c = 64: MIOpen + bias/SiLU pass; 128: implicit-GEMM conv with 2-pixel
-    super-pixels; 256: 1-pixel) vs the literal conv -> SiLU -> conv -> RMSNorm + residual."""
+    """ResBlock.forward (c = 64: MIOpen + bias/SiLU pass; 128: implicit-GEMM conv on the 512 x 128
+    tile; 256: the 256 x 256 tile) vs the literal conv -> SiLU -> conv -> RMSNorm + residual."""
     from hyperscalees_t2i_amd.dcae import ResBlock, conv_gemm_px
     torch.manual_seed(1)
     with torch.device(dev):
@@ -526,6 +526,9 @@ def test_resblock_matches_reference(dev, c):
     (2, 16, 16, 64, 64, 1, True, None),
     (2, 16, 32, 128, 128, 2, True, "silu"),
     (1, 7, 10, 128, 128, 2, False, None),     # odd H, tail super-pixel rows (M' % 256 != 0)
+    (2, 16, 32, 128, 128, 1, True, "silu"),   # Cout 128 at px 1: the 512 x 128 tile
+    (1, 7, 10, 128, 128, 1, False, None),     # 512 x 128 tile with a ragged last tile (70 rows)
+    (3, 40, 24, 256, 128, 1, True, None),     # 512 x 128, Cin 256, several tiles + tail (2880 = 5.6 x 512)
     (1, 24, 40, 256, 256, 1, True, "silu"),
     (1, 9, 12, 512, 512, 1, False, None),     # N = 512: two column tiles
     (3, 5, 6, 64, 256, 1, True, None),        # Cin != Cout, tiny image (every pixel is a border pixel)
@@ -555,10 +558,12 @@ def test_conv3x3_nhwc_rejects_bad_shapes(dev):
         K.conv3x3_nhwc(x, w, None, 1)
 
 
-@pytest.mark.parametrize("B,H,W,Cin,px", [(2, 16, 32, 128, 2), (1, 7, 10, 128, 2), (1, 9, 12, 256, 1), (2, 5, 6, 64, 1)])
-def test_conv3x3_rmsnorm_nhwc_vs_torch(dev, B, H, W, Cin, px):
-    """conv3x3 -> RMSNorm(* w + b) -> + res in one launch vs torch fp32 on the same bf16 inputs."""
-    Cout = 256 // px
+@pytest.mark.parametrize("B,H,W,Cin,px,Cout", [(2, 16, 32, 128, 2, 128), (1, 7, 10, 128, 2, 128), (1, 9, 12, 256, 1, 256),
+                                               (2, 5, 6, 64, 1, 256), (2, 16, 32, 128, 1, 128), (1, 7, 10, 128, 1, 128),
+                                               (3, 40, 24, 64, 1, 128)])
+def test_conv3x3_rmsnorm_nhwc_vs_torch(dev, B, H, W, Cin, px, Cout):
+    """conv3x3 -> RMSNorm(* w + b) -> + res in one launch vs torch fp32 on the same bf16 inputs
+    (Cout 128 at px 1: the 512 x 128 tile, RMSNorm across its two column waves)."""
     g = torch.Generator().manual_seed(7 + H)
     x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
     w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)

@@ -52,7 +52,7 @@ for B, C, hw, pxs in [(8, 128, 1024, (2, 1)), (8, 256, 512, (1, 2)), (8, 512, 25
         row[f"px{px}_tflops"] = round(fl / ms / 1e9, 1)
         row[f"px{px}_bias_silu_ms"] = round(ms_f, 3)
         row[f"px{px}_relerr"] = float(f"{err:.2e}")
-        if wp.shape[0] == 256:  # conv2 + RMSNorm + residual fused
+        if wp.shape[0] == 256 or (px == 1 and C == 128):  # conv2 + RMSNorm + residual fused
             nw = torch.ones(C, device=dev, dtype=torch.bfloat16)
             row[f"px{px}_norm_ms"] = round(t(lambda: K.conv3x3_rmsnorm_nhwc(x, wp, None, px, 1e-5, nw, nw, x)), 3)
             row["rownorm_ms"] = round(t(lambda: K.rownorm(out, 1e-5, layer=False, w=nw, b=nw, res=x)), 3)
