@@ -156,6 +156,35 @@ constexpr int BK = 64;
 #endif
 constexpr int GROUP_M = EGG_GROUP_M;  // row-tiles per rasterisation group
 
+// Phase stamps for the tools-only diagnostic build (tools/stamp_probe.py compiles this file with
+// -DEGG_STAMPS into a separate library; the shipped libeggroll.so has none): wave 0 of every
+// workgroup records s_memtime at fixed points of the 8-phase kernels (vector stores from lane 0).
+#ifdef EGG_STAMPS
+constexpr int EGG_NSTAMP = 8;
+__device__ unsigned long long g_egg_stamps[131072 * EGG_NSTAMP];
+#define EGG_STAMP(k)                                                                                         \
+    do {                                                                                                     \
+        if (threadIdx.x == 0)                                                                                \
+            g_egg_stamps[(size_t)blockIdx.x * EGG_NSTAMP + (k)] = __builtin_amdgcn_s_memtime();              \
+    } while (0)
+#define EGG_STAMP_RT(k)                                                                                      \
+    do {                                                                                                     \
+        if (threadIdx.x == 0)                                                                                \
+            g_egg_stamps[(size_t)blockIdx.x * EGG_NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime();          \
+    } while (0)
+#define EGG_STAMP_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define EGG_STAMP(k) \
+    do {             \
+    } while (0)
+#define EGG_STAMP_RT(k) \
+    do {                \
+    } while (0)
+#define EGG_STAMP_DRAIN() \
+    do {                  \
+    } while (0)
+#endif
+
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
@@ -618,6 +647,19 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
         }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+    const bool full = m0 + rbase + 128 <= M && n0 + cbase + 64 <= N && (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0;
+    if (full) {  // interior wave tile: all 16 row reads in flight, then 16 unconditional 16-B stores
+        u16x8 v[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int rr = it * 8 + (lane >> 3), sl = lane & 7;
+            v[it] = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+        }
+        unsigned short* dst = Y + (int64_t)(m0 + rbase + (lane >> 3)) * ldy + n0 + cbase + (lane & 7) * 8;
+#pragma unroll
+        for (int it = 0; it < 16; ++it) *reinterpret_cast<u16x8*>(dst + (int64_t)it * 8 * ldy) = v[it];
+        return;
+    }
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int rr = it * 8 + (lane >> 3), sl = lane & 7;
@@ -703,13 +745,108 @@ __device__ __forceinline__ void lora_mfma_addend(f32x4 (&acc)[8][4], int lane, i
     }
 }
 
+// Epilogue operands of the MFMA LoRA addend, prefetched into LDS (after the 128 KiB ring) by
+// 4-byte LDS-DMAs issued before the GEMM prologue — the prologue's counted vmcnt retires them, so
+// the epilogue reads LDS instead of waiting on dependent global loads after the last MFMA:
+// T rows [m0, m0 + 256) x R, B_k columns [n0, n0 + 256) x R of the tile's first member (and of the
+// next one when the tile straddles two), bias[n0, n0 + 256).  Out-of-range bytes read as 0.
+namespace epi {
+constexpr int T = 0, B0 = 2048, B1 = 4096, BIAS = 6144, BYTES = 6656;
+}
+
+template <int R>
+__device__ __forceinline__ void epi_prefetch(char* ep, int wave, int lane, int m0, int n0, int M, int N,
+                                             const float* __restrict__ T, const float* __restrict__ theta_pop,
+                                             int64_t ld_theta, int64_t offB, const unsigned short* __restrict__ bias,
+                                             int rows_per_member) {
+    static_assert(R >= 0 && R <= 2, "MFMA addend: r <= 2");
+    constexpr int TB = 256 * R * 4;  // bytes of the tile's T rows / B_k columns
+    const uint32_t vo = lane * 4;
+    if (R > 0 && wave * 256 < TB) {
+        const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(T + (int64_t)m0 * R), (short)0, (int)((int64_t)(M - m0) * R * 4), 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void*)(ep + epi::T + wave * 256), 4, vo, wave * 256, 0, 0);
+        const int ma = m0 / rows_per_member;
+        const int nrec = (N - n0) * R * 4;
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(theta_pop + (int64_t)ma * ld_theta + offB + (int64_t)n0 * R), (short)0, nrec, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(ep + epi::B0 + wave * 256), 4, vo, wave * 256, 0, 0);
+        const int last = m0 + 255 < M ? m0 + 255 : M - 1;
+        if (last / rows_per_member != ma) {
+            const __amdgpu_buffer_rsrc_t rb1 = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(theta_pop + (int64_t)(ma + 1) * ld_theta + offB + (int64_t)n0 * R), (short)0, nrec, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb1, (lds_void*)(ep + epi::B1 + wave * 256), 4, vo, wave * 256, 0,
+                                                     0);
+        }
+    }
+    if (bias && wave < 2) {
+        const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(bias + n0), (short)0,
+                                                                            (N - n0) * 2, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_void*)(ep + epi::BIAS + wave * 256), 4, vo, wave * 256, 0, 0);
+    }
+}
+
+// lora_mfma_addend with every operand read from the prefetched LDS block (same k-slot layout).
+template <int R>
+__device__ __forceinline__ void lora_mfma_addend_lds(f32x4 (&acc)[8][4], int lane, int m0, int rbase, int cbase,
+                                                     const char* ep, bool has_bias, float scale, int rows_per_member,
+                                                     int M) {
+    const int h = lane >> 4, l16 = lane & 15;
+    const int ma = m0 / rows_per_member;
+    const int last = (m0 + 255 < M ? m0 + 255 : M - 1);
+    const bool straddle = last / rows_per_member != ma;
+    const float* Tl = reinterpret_cast<const float*>(ep + epi::T);
+    const unsigned short* bl = reinterpret_cast<const unsigned short*>(ep + epi::BIAS);
+    bf16x8 rf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = cbase + j * 16 + l16;  // tile-local column
+        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (h == 0 || (h == 1 && straddle)) {
+            const float* Bk = reinterpret_cast<const float*>(ep + (h ? epi::B1 : epi::B0));
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const float sb = scale * Bk[c * R + q];
+                const short hi = bf16_bits(sb);
+                v[q] = hi;
+                v[R + q] = hi;
+                v[2 * R + q] = bf16_bits(sb - bf16_to_f32((unsigned short)hi));
+            }
+            v[3 * R] = has_bias ? (short)bl[c] : (short)0;
+        }
+        rf[j] = *reinterpret_cast<bf16x8*>(v);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int rl = rbase + i * 16 + l16;  // tile-local row
+        int row = m0 + rl;
+        row = row < M ? row : M - 1;
+        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (h == row / rows_per_member - ma) {
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const float t = Tl[rl * R + q];
+                const short th = bf16_bits(t);
+                v[q] = th;
+                v[R + q] = bf16_bits(t - bf16_to_f32((unsigned short)th));
+                v[2 * R + q] = th;
+            }
+            v[3 * R] = (short)0x3F80;  // 1.0
+        }
+        const bf16x8 lf = *reinterpret_cast<bf16x8*>(v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)  // transposed fragments (TR main loop): D[n][m]
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rf[j], lf, acc[i][j], 0, 0, 0);
+    }
+}
+
 template <int R, bool MF>
 __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
     const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
     int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int M, int N, int64_t K, int tiles_n,
     unsigned short* __restrict__ Y, int64_t ldy) {
-    __shared__ __attribute__((aligned(16))) char smem[p8::LDS];
+    __shared__ __attribute__((aligned(16))) char smem[p8::LDS + (MF ? epi::BYTES : 0)];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     // XCD-aware bijective remap + grouped rasterisation (as k_lora_gemm).
@@ -723,6 +860,8 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     const int in_grp = tile - grp * per_group;
     const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
     const int m0 = tm * 256, n0 = tn * 256;
+    EGG_STAMP_RT(6);
+    EGG_STAMP(0);
 
     const HalfStage sA0 = make_stage<true>(m0, M - 1, ldx, 0, wave, lane);
     const HalfStage sA1 = make_stage<true>(m0, M - 1, ldx, 1, wave, lane);
@@ -747,6 +886,9 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     // K-tile byte offset; tiles past the end re-load the last K-tile (into regions nothing reads
     // again), so every phase issues exactly 2 DMAs and the vmcnt counts stay static.
     auto kb = [nk](int t) -> int { return (t < nk ? t : nk - 1) * (BK * 2); };
+    if constexpr (MF)  // older than every ring DMA: the prologue's vmcnt(6) retires it
+        epi_prefetch<(MF ? R : 0)>(smem + p8::LDS, wave, lane, m0, n0, M, N, T, theta_pop, ld_theta, offB, bias,
+                                   rows_per_member);
     // prologue: K-tile 0 complete, K-tile 1 minus its B0 half (issued in phase 1)
     issue_half(rX, sA0, 0, e_buf + p8::RA0, wave);
     issue_half(rW, sB1, 0, e_buf + p8::RB1, wave);
@@ -757,6 +899,7 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     issue_half(rX, sA1, kb(1), o_buf + p8::RA1, wave);
     P8_VM6();
     P8_BAR();
+    EGG_STAMP(1);
     if (wm == 1) P8_BAR();  // stagger: group 1 runs one barrier behind
 
     // Phase p restages the region last read in phase p-1 (quadrant order (0,0) (0,1) (1,1) (1,0)):
@@ -782,13 +925,19 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
         p8_phase<1, 0, 1, false, MF>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
     }
     if (wm == 0) P8_BAR();  // balance the stagger
+    EGG_STAMP(2);
     P8_VM0();
     __syncthreads();  // every wave is past its last LDS read: the epilogue reuses the ring
+    EGG_STAMP(3);
 
     if constexpr (MF) {  // bias + LoRA term as one extra MFMA k-step, then a plain bf16 store
-        lora_mfma_addend<R>(acc, lane, m0, n0, wm * 128, wn * 64, bias, T, theta_pop, ld_theta, offB, scale,
-                            rows_per_member, M, N);
+        lora_mfma_addend_lds<(MF ? R : 0)>(acc, lane, m0, wm * 128, wn * 64, smem + p8::LDS, bias != nullptr, scale,
+                                           rows_per_member, M);
+        EGG_STAMP(4);
         store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, M, N, Y, ldy);
+        EGG_STAMP_DRAIN();
+        EGG_STAMP(5);
+        EGG_STAMP_RT(7);
     } else {
         lora_epilogue<R, 128, 64>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, bias, T, theta_pop, ld_theta,
                                   offB, scale, rows_per_member, 256, M, N, Y, ldy);
@@ -1395,6 +1544,8 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     const int m0 = tm * G::BM, n0 = tn * G::BN;
     const int64_t K = (int64_t)KS * TW * Cin;
     const int nk = (int)(K / BK);
+    EGG_STAMP_RT(6);
+    EGG_STAMP(0);
 
     const ConvStage<G::NA> sA0 = make_conv_stage<PX, KS, G::NA>(m0, Mp, H, W, Cin, 0, wave, lane);
     const ConvStage<G::NA> sA1 = make_conv_stage<PX, KS, G::NA>(m0, Mp, H, W, Cin, 1, wave, lane);
@@ -1449,6 +1600,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     A(sA1, 1, o_buf + G::RA1);
     wait_vm<G::VMC>();
     P8_BAR();
+    EGG_STAMP(1);
     if (grp8 == 1) P8_BAR();
 
     int t0 = 0;
@@ -1469,17 +1621,24 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
         p8c_phase<G, 1, 0, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + G::RA1); });
     }
     if (grp8 == 0) P8_BAR();
+    EGG_STAMP(2);
     P8_VM0();
     __syncthreads();
+    EGG_STAMP(3);
     if (bias)
         lora_mfma_addend<0>(acc, lane, m0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, Mp, N);
     if constexpr (NORM) {
         conv_rmsnorm_epilogue<PX, WMW>(acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane, m0, Mp, eps, nw,
                                        nb, res);
+        EGG_STAMP(4);
         store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
     } else {
+        EGG_STAMP(4);
         store_tile_t_act<ACT>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
     }
+    EGG_STAMP_DRAIN();
+    EGG_STAMP(5);
+    EGG_STAMP_RT(7);
 }
 
 }  // namespace eggroll
@@ -1487,6 +1646,15 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
 using namespace eggroll;
 
 extern "C" {
+
+#ifdef EGG_STAMPS
+// diagnostic build only: copy the first n stamps (n <= 131072 * 8) to host memory
+int eggroll_debug_stamps(unsigned long long* host, int64_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_egg_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? EGGROLL_OK
+               : EGGROLL_ERR_LAUNCH;
+}
+#endif
 
 int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta, int64_t offA, int32_t r,
                          int64_t rows_per_member, int64_t M, int64_t K, float* T, void* stream) {
