@@ -520,15 +520,33 @@ __device__ __forceinline__ void p8_frag_offsets(int (&off)[2], int r0, int lane)
 }
 
 #define P8_LGKM0_ asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+// s_waitcnt vmcnt(N) with a compile-time N (the counts of the 8-phase tiles: see G8)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N == 6 || N == 9 || N == 10 || N == 14, "add the literal");
+    if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+}
+
+// Early first K-tile.  The prologue issues K-tile 0 as A0, B0, B1, A1 and waits only for A0 + B0
+// (what phase 1 reads); phase 1 retires B1 (read in phase 2) and phase 2 retires A1 (read in phase 3),
+// each before its first barrier — "wait in phase q, read in phase q+1", which also covers the wave
+// group that runs one barrier behind.  Younger than each of these DMAs are exactly 3 A-halves + 2
+// B-halves (NA / NB DMAs each), so all three waits are vmcnt(3 NA + 2 NB); in steady state at most
+// that many are outstanding at those points, so the two in-loop waits are no-ops after K-tile 0.
 // One phase: read the quadrant's fragments (RD: 0 = A+B, 1 = B only, 2 = A only), issue one
 // half-tile DMA, [vmcnt(6)], retire the reads, barrier, 16 MFMA, barrier.
-template <int QA, int QB, int RD, bool VM, bool TR>
+template <int QA, int QB, int RD, bool VM, bool TR, int EW = 0>
 __device__ __forceinline__ void p8_phase(f32x4 (&acc)[8][4], bf16x8 (&a)[4][2], bf16x8 (&b)[2][2], const char* buf,
                                          const int (&oA)[2], const int (&oB)[2], __amdgpu_buffer_rsrc_t rs,
                                          const HalfStage& st, int kbytes, char* dst, int wave) {
     if (RD != 2) p8_read_b(b, buf + (QB ? p8::RB1 : p8::RB0), oB);
     if (RD != 1) p8_read_a(a, buf + (QA ? p8::RA1 : p8::RA0), oA);
     issue_half(rs, st, kbytes, dst, wave);
+    if constexpr (EW > 0) wait_vm<EW>();  // early first K-tile (no-op in steady state)
     if (VM) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     P8_LGKM0_;
     P8_BAR();
@@ -891,13 +909,13 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
                                    rows_per_member);
     // prologue: K-tile 0 complete, K-tile 1 minus its B0 half (issued in phase 1)
     issue_half(rX, sA0, 0, e_buf + p8::RA0, wave);
+    issue_half(rW, sB0, 0, e_buf + p8::RB0, wave);
     issue_half(rW, sB1, 0, e_buf + p8::RB1, wave);
     issue_half(rX, sA1, 0, e_buf + p8::RA1, wave);
-    issue_half(rW, sB0, 0, e_buf + p8::RB0, wave);
     issue_half(rX, sA0, kb(1), o_buf + p8::RA0, wave);
     issue_half(rW, sB1, kb(1), o_buf + p8::RB1, wave);
     issue_half(rX, sA1, kb(1), o_buf + p8::RA1, wave);
-    P8_VM6();
+    wait_vm<10>();  // K-tile 0's A0 + B0 only (early first K-tile, above)
     P8_BAR();
     EGG_STAMP(1);
     if (wm == 1) P8_BAR();  // stagger: group 1 runs one barrier behind
@@ -908,8 +926,8 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     int t0 = 0;
     for (; t0 + 1 < nk; t0 += 2) {
         const int k1 = kb(t0 + 1), k2 = kb(t0 + 2), k3 = kb(t0 + 3);
-        p8_phase<0, 0, 0, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
-        p8_phase<0, 1, 1, false, MF>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
+        p8_phase<0, 0, 0, false, MF, 10>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false, MF, 10>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
         p8_phase<1, 1, 2, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
         p8_phase<1, 0, 1, true, MF>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
         p8_phase<0, 0, 0, false, MF>(acc, a, b, o_buf, oA, oB, rW, sB0, k2, e_buf + p8::RB0, wave);
@@ -919,8 +937,8 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     }
     if (t0 < nk) {  // odd K-tile count: the last tile is in the even buffer (retired by phase 8)
         const int k1 = kb(t0 + 1), k2 = kb(t0 + 2);
-        p8_phase<0, 0, 0, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
-        p8_phase<0, 1, 1, false, MF>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
+        p8_phase<0, 0, 0, false, MF, 10>(acc, a, b, e_buf, oA, oB, rW, sB0, k1, o_buf + p8::RB0, wave);
+        p8_phase<0, 1, 1, false, MF, 10>(acc, a, b, e_buf, oA, oB, rX, sA0, k2, e_buf + p8::RA0, wave);
         p8_phase<1, 1, 2, false, MF>(acc, a, b, e_buf, oA, oB, rW, sB1, k2, e_buf + p8::RB1, wave);
         p8_phase<1, 0, 1, false, MF>(acc, a, b, e_buf, oA, oB, rX, sA1, k2, e_buf + p8::RA1, wave);
     }
@@ -1328,6 +1346,7 @@ struct G8 {
     static constexpr int NA = HA / 8192, NB = HB / 8192;  // DMAs per wave per half-tile (8 waves x 1 KiB)
     // glds left in flight when a K-tile retires (the next K-tile's A0, B1, A1 halves; T3/T4 formula)
     static constexpr int VMC = 2 * NA + NB;
+    static constexpr int VMC0 = 3 * NA + 2 * NB;  // early first K-tile waits (see wait_vm)
     static constexpr int CSTAGE = 8 * 128 * 64 * 2;  // epilogue C staging: one 128x64 bf16 tile per wave
     static_assert(LDS <= 160 * 1024, "ring exceeds the 160 KiB LDS");
 };
@@ -1414,20 +1433,14 @@ __device__ __forceinline__ void issue_half_n(__amdgpu_buffer_rsrc_t rs, const WS
     }
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    static_assert(N == 6 || N == 9, "add the literal");
-    if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-}
-
 // p8_phase with the DMA supplied by the caller (A: masked conv staging, B: weight staging)
-template <class G, int QA, int QB, int RD, bool VM, class Issue>
+template <class G, int QA, int QB, int RD, bool VM, bool EW, class Issue>
 __device__ __forceinline__ void p8c_phase(f32x4 (&acc)[8][4], bf16x8 (&a)[4][2], bf16x8 (&b)[2][2], const char* buf,
                                           const int (&oA)[2], const int (&oB)[2], Issue&& issue) {
     if (RD != 2) p8_read_b(b, buf + (QB ? G::RB1 : G::RB0), oB);
     if (RD != 1) p8_read_a(a, buf + (QA ? G::RA1 : G::RA0), oA);
     issue();
+    if constexpr (EW) wait_vm<G::VMC0>();  // early first K-tile (no-op in steady state)
     if (VM) wait_vm<G::VMC>();
     P8_LGKM0_;
     P8_BAR();
@@ -1592,33 +1605,33 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
         issue_half_n(rW, s, t * (BK * 2), dst, wave);
     };
     A(sA0, 0, e_buf + G::RA0);
+    B(sB0, 0, e_buf + G::RB0);
     B(sB1, 0, e_buf + G::RB1);
     A(sA1, 0, e_buf + G::RA1);
-    B(sB0, 0, e_buf + G::RB0);
     A(sA0, 1, o_buf + G::RA0);
     B(sB1, 1, o_buf + G::RB1);
     A(sA1, 1, o_buf + G::RA1);
-    wait_vm<G::VMC>();
+    wait_vm<G::VMC0>();  // K-tile 0's A0 + B0 only (early first K-tile, see wait_vm)
     P8_BAR();
     EGG_STAMP(1);
     if (grp8 == 1) P8_BAR();
 
     int t0 = 0;
     for (; t0 + 1 < nk; t0 += 2) {
-        p8c_phase<G, 0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + G::RB0); });
-        p8c_phase<G, 0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + G::RA0); });
-        p8c_phase<G, 1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + G::RB1); });
-        p8c_phase<G, 1, 0, 1, true>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + G::RA1); });
-        p8c_phase<G, 0, 0, 0, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB0, t0 + 2, e_buf + G::RB0); });
-        p8c_phase<G, 0, 1, 1, false>(acc, a, b, o_buf, oA, oB, [&] { A(sA0, t0 + 3, o_buf + G::RA0); });
-        p8c_phase<G, 1, 1, 2, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB1, t0 + 3, o_buf + G::RB1); });
-        p8c_phase<G, 1, 0, 1, true>(acc, a, b, o_buf, oA, oB, [&] { A(sA1, t0 + 3, o_buf + G::RA1); });
+        p8c_phase<G, 0, 0, 0, false, true>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + G::RB0); });
+        p8c_phase<G, 0, 1, 1, false, true>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + G::RA0); });
+        p8c_phase<G, 1, 1, 2, false, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + G::RB1); });
+        p8c_phase<G, 1, 0, 1, true, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + G::RA1); });
+        p8c_phase<G, 0, 0, 0, false, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB0, t0 + 2, e_buf + G::RB0); });
+        p8c_phase<G, 0, 1, 1, false, false>(acc, a, b, o_buf, oA, oB, [&] { A(sA0, t0 + 3, o_buf + G::RA0); });
+        p8c_phase<G, 1, 1, 2, false, false>(acc, a, b, o_buf, oA, oB, [&] { B(sB1, t0 + 3, o_buf + G::RB1); });
+        p8c_phase<G, 1, 0, 1, true, false>(acc, a, b, o_buf, oA, oB, [&] { A(sA1, t0 + 3, o_buf + G::RA1); });
     }
     if (t0 < nk) {
-        p8c_phase<G, 0, 0, 0, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + G::RB0); });
-        p8c_phase<G, 0, 1, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + G::RA0); });
-        p8c_phase<G, 1, 1, 2, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + G::RB1); });
-        p8c_phase<G, 1, 0, 1, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + G::RA1); });
+        p8c_phase<G, 0, 0, 0, false, true>(acc, a, b, e_buf, oA, oB, [&] { B(sB0, t0 + 1, o_buf + G::RB0); });
+        p8c_phase<G, 0, 1, 1, false, true>(acc, a, b, e_buf, oA, oB, [&] { A(sA0, t0 + 2, e_buf + G::RA0); });
+        p8c_phase<G, 1, 1, 2, false, false>(acc, a, b, e_buf, oA, oB, [&] { B(sB1, t0 + 2, e_buf + G::RB1); });
+        p8c_phase<G, 1, 0, 1, false, false>(acc, a, b, e_buf, oA, oB, [&] { A(sA1, t0 + 2, e_buf + G::RA1); });
     }
     if (grp8 == 0) P8_BAR();
     EGG_STAMP(2);
