@@ -9,7 +9,7 @@ import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from hyperscalees_t2i_amd import kernels as K  # noqa: E402
-from oracle.cpu_baseline import sana_lora_layers  # noqa: E402  (shape table only)
+from tools.sana_layers import sana_lora_layers  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 members = 8

@@ -9,7 +9,7 @@ import csv, json, sys
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-from oracle.cpu_baseline import sana_lora_layers  # noqa: E402
+from tools.sana_layers import sana_lora_layers  # noqa: E402
 
 fetch_dir, write_dir = sys.argv[1], sys.argv[2]
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
