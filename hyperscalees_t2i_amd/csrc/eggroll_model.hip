@@ -424,11 +424,30 @@ constexpr int LA_D = 32;
 constexpr int LA_PART = LA_D * LA_D + LA_D;   // kv + ksum floats per partial
 constexpr int LA_T = 256;                     // tokens per chunk
 
-// Pass 1 per (image*head, chunk of LA_T tokens): k (ReLU'd) and v staged into LDS as bf16 with all
-// 8 loads per thread in flight; thread (token group g, i-block a, j-block c) accumulates a 4x4 block
-// kv[4a..4a+3][4c..4c+3] (+ ksum[4c..4c+3]) over its group's 64 tokens from two 8-byte LDS reads per
-// token (8 pk-FMA), then the four token groups are summed in a fixed order through LDS.
-constexpr int LA_RS = LA_D + 8;  // bf16 LDS row stride (80 B: 16-B aligned rows)
+// Pass 1 per (image*head, chunk of LA_T tokens) on MFMA: k (ReLU'd) and v staged into LDS token-major
+// as bf16 (all 8 loads per thread in flight), then kv^T-free: C[i][j] = sum_n v[n][i] relu(k[n][j]) as
+// 16x16x32 bf16 MFMAs with the TOKEN axis as K — both operands need 8 consecutive tokens of one
+// feature per lane, which ds_read_b64_tr_b16 (gfx950 transpose read: per 16-lane group a 4-row x
+// 16-column block delivered column-major) reads straight from the token-major image.  ksum[j] is one
+// more MFMA with a row of ones as A.  Each wave covers 64 tokens (2 K-steps); the 4 waves' partials
+// are summed in a fixed order through LDS.  Products of bf16 inputs are exact in fp32, as in the VALU
+// form; only the accumulation order differs.
+typedef __attribute__((ext_vector_type(8))) __bf16 la_bf16x8;
+typedef __attribute__((ext_vector_type(4))) float la_f32x4;
+constexpr int LA_RS = LA_D + 8;  // bf16 LDS row stride (80 B: 8-B aligned rows for the transpose reads)
+typedef __attribute__((ext_vector_type(4))) short la_s4;
+typedef __attribute__((address_space(3))) la_s4 la_lds_s4;
+
+__device__ __forceinline__ la_bf16x8 la_tr8(const unsigned short* base, int lane) {
+    // rows base + 8g + {0..3} and {4..7} of the 16-lane group g; lane 4q+p addresses row q, columns 4p..4p+3
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const unsigned short* r0 = base + (8 * g + q) * LA_RS + 4 * p;
+    const la_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((la_lds_s4*)(r0));
+    const la_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((la_lds_s4*)(r0 + 4 * LA_RS));
+    typedef __attribute__((ext_vector_type(8))) short s8;
+    const s8 f = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(la_bf16x8, f);
+}
 
 __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict__ k, const unsigned short* __restrict__ v,
                                                int64_t ld, int64_t hstride, int heads, int N, int nchunk, int relu,
@@ -436,7 +455,7 @@ __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict_
     __shared__ __attribute__((aligned(16))) unsigned short lds_kv[2 * LA_T * LA_RS];  // sk | sv, then red
     unsigned short* sk = lds_kv;
     unsigned short* sv = lds_kv + LA_T * LA_RS;
-    float(*red)[LA_PART] = reinterpret_cast<float(*)[LA_PART]>(lds_kv);  // after the token loop
+    float(*red)[LA_PART] = reinterpret_cast<float(*)[LA_PART]>(lds_kv);  // after the MFMAs
     static_assert(4 * LA_PART * 4 <= 2 * LA_T * LA_RS * 2, "reduction buffer fits in the staging LDS");
     const int lb = xcd_remap(blockIdx.x, gridDim.x);  // adjacent heads share 128-B lines: same L2
     const int bh = lb / nchunk, c = lb - bh * nchunk;
@@ -466,36 +485,44 @@ __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict_
         *reinterpret_cast<u16x8m*>(sv + t * LA_RS + q4 * 8) = vr[it];
     }
     __syncthreads();
-    const int g = tid >> 6, l = tid & 63, ia = l >> 3, jc = l & 7;
-    float acc[4][4], ks[4];
+    const int lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+    la_bf16x8 ones;
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-        ks[x] = 0.f;
+    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(r16 == 0 ? 1.0f : 0.0f);  // A row 0 = ones -> ksum
+    la_f32x4 acc[2][2], ks[2];
 #pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = 0.f;
+    for (int x = 0; x < 2; ++x) {
+        ks[x] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = la_f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const int t_end = cnt < (g + 1) * 64 ? cnt : (g + 1) * 64;
-    for (int t = g * 64; t < t_end; ++t) {
-        const u16x4m vv = *reinterpret_cast<const u16x4m*>(sv + t * LA_RS + ia * 4);
-        const u16x4m kk = *reinterpret_cast<const u16x4m*>(sk + t * LA_RS + jc * 4);
-        float vf[4], kf[4];
 #pragma unroll
-        for (int x = 0; x < 4; ++x) { vf[x] = b2f(vv[x]); kf[x] = b2f(kk[x]); }
+    for (int s = 0; s < 2; ++s) {  // this wave's 64 tokens as 2 K-steps of 32
+        const int t0 = w * 64 + s * 32;
+        la_bf16x8 av[2], bk[2];
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            ks[x] += kf[x];
+        for (int x = 0; x < 2; ++x) {
+            av[x] = la_tr8(sv + t0 * LA_RS + 16 * x, lane);  // A[i = 16x + r16][n]
+            bk[x] = la_tr8(sk + t0 * LA_RS + 16 * x, lane);  // B[n][j = 16x + r16]
+        }
 #pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] += vf[x] * kf[y];
+        for (int x = 0; x < 2; ++x) {
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[x], bk[y], acc[x][y], 0, 0, 0);
+            ks[x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bk[x], ks[x], 0, 0, 0);
         }
     }
     __syncthreads();  // every wave is done reading sk / sv: reuse the staging LDS for the reduction
+    // C layout: lane holds C[4g + e][r16]
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
+    for (int x = 0; x < 2; ++x)
 #pragma unroll
-        for (int y = 0; y < 4; ++y) red[g][(ia * 4 + x) * LA_D + jc * 4 + y] = acc[x][y];
-    if (ia == 0) {
+        for (int y = 0; y < 2; ++y)
 #pragma unroll
-        for (int y = 0; y < 4; ++y) red[g][LA_D * LA_D + jc * 4 + y] = ks[y];
+            for (int e = 0; e < 4; ++e) red[w][(16 * x + 4 * g + e) * LA_D + 16 * y + r16] = acc[x][y][e];
+    if (g == 0) {
+#pragma unroll
+        for (int y = 0; y < 2; ++y) red[w][LA_D * LA_D + 16 * y + r16] = ks[y][0];
     }
     __syncthreads();
     float* dst = part + (int64_t)lb * LA_PART;  // slot bh * nchunk + c: k_la_reduce sums chunks in order
@@ -524,55 +551,87 @@ __global__ __launch_bounds__(256) void k_la_reduce(const float* __restrict__ par
     }
 }
 
+// Pass 3 on MFMA: out^T[i][t] = sum_j kv[i][j] relu(q[t][j]) as 16x16x32 bf16 MFMAs with kv as the A
+// operand (row i, 8 consecutive j per lane — the natural [i][j] layout) and 16 tokens' q as the B
+// operand (each lane's 16-B load is 8 consecutive features of one token), so the accumulator lane
+// holds 4 consecutive output features of one token (one 8-byte store).  kv (fp32) enters as a bf16
+// hi + lo pair (two MFMAs: ~2^-16 relative, fp32-class), and the denominator relu(q) . ksum is one
+// more hi/lo MFMA pair with ksum as row 0 of a 16-row A tile.  The VALU form spent 1056 FMAs + as many
+// LDS broadcast reads per token-head; this one is 6 MFMAs per 16 tokens and memory-bound.
+
+__device__ __forceinline__ void la_split8(const float (&f)[8], la_bf16x8& hi, la_bf16x8& lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const __bf16 h = (__bf16)f[e];
+        hi[e] = h;
+        lo[e] = (__bf16)(f[e] - (float)h);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict__ q, int64_t ld, int64_t hstride,
                                                 int heads, int N, int nchunk, int relu, const float* __restrict__ kvsum,
                                                 unsigned short* __restrict__ out, int64_t ldo) {
-    __shared__ float skv[LA_PART];
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = lb / nchunk, c = lb - bh * nchunk;
     const int b = bh / heads, h = bh - b * heads;
-    const int tid = threadIdx.x;
-    float kvr[(LA_PART + 255) / 256];  // all loads in flight before the first LDS write
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r16 = lane & 15, g = lane >> 4;
+    const float* kvh = kvsum + (int64_t)bh * LA_PART;
+    la_bf16x8 akv[2][2], aden[2];  // [feature block][hi, lo]
 #pragma unroll
-    for (int it = 0; it < (LA_PART + 255) / 256; ++it) {
-        const int e = tid + it * 256;
-        kvr[it] = e < LA_PART ? kvsum[(int64_t)bh * LA_PART + e] : 0.f;
+    for (int cb = 0; cb < 2; ++cb) {
+        const float4 x0 = *reinterpret_cast<const float4*>(kvh + (16 * cb + r16) * LA_D + 8 * g);
+        const float4 x1 = *reinterpret_cast<const float4*>(kvh + (16 * cb + r16) * LA_D + 8 * g + 4);
+        const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        la_split8(f, akv[cb][0], akv[cb][1]);
     }
-#pragma unroll
-    for (int it = 0; it < (LA_PART + 255) / 256; ++it) {
-        const int e = tid + it * 256;
-        if (e < LA_PART) skv[e] = kvr[it];
-    }
-    __syncthreads();
-    const int n = c * LA_T + tid;
-    if (n >= N) return;
-    const int64_t row = (int64_t)b * N + n;
-    float qv[LA_D];
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-        const u16x8m q8 = *reinterpret_cast<const u16x8m*>(q + row * ld + (int64_t)h * hstride + q4 * 8);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float x = b2f(q8[i]);
-            qv[q4 * 8 + i] = relu ? (x > 0.f ? x : 0.f) : x;
+    {
+        float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (r16 == 0) {  // A row 0 = ksum, rows 1..15 = 0
+            const float4 x0 = *reinterpret_cast<const float4*>(kvh + LA_D * LA_D + 8 * g);
+            const float4 x1 = *reinterpret_cast<const float4*>(kvh + LA_D * LA_D + 8 * g + 4);
+            f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w;
+            f[4] = x1.x; f[5] = x1.y; f[6] = x1.z; f[7] = x1.w;
         }
+        la_split8(f, aden[0], aden[1]);
     }
-    float den = 0.f;
+    const int n0 = c * LA_T + wave * (LA_T / 4);
+    u16x8m qr[LA_T / 64];  // this wave's 4 tiles of 16 tokens: all loads in flight first
 #pragma unroll
-    for (int j = 0; j < LA_D; ++j) den += qv[j] * skv[LA_D * LA_D + j];
-    const float inv = 1.0f / (den + 1e-15f);
-    unsigned short* o = out + row * ldo + h * LA_D;
+    for (int tt = 0; tt < LA_T / 64; ++tt) {
+        const int tok = n0 + tt * 16 + r16;
+        qr[tt] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+        if (tok < N) qr[tt] = *reinterpret_cast<const u16x8m*>(q + ((int64_t)b * N + tok) * ld + (int64_t)h * hstride + 8 * g);
+    }
 #pragma unroll
-    for (int i0 = 0; i0 < LA_D; i0 += 8) {
-        u16x8m o8;
+    for (int tt = 0; tt < LA_T / 64; ++tt) {
+        const int tok = n0 + tt * 16 + r16;
+        u16x8m qv = qr[tt];
+        if (relu) {
 #pragma unroll
-        for (int ii = 0; ii < 8; ++ii) {
-            float s = 0.f;
-#pragma unroll
-            for (int j = 0; j < LA_D; ++j) s += qv[j] * skv[(i0 + ii) * LA_D + j];
-            o8[ii] = f2b(s * inv);
+            for (int e = 0; e < 8; ++e) qv[e] = (qv[e] & 0x8000) ? (unsigned short)0 : qv[e];  // bf16 ReLU
         }
-        *reinterpret_cast<u16x8m*>(o + i0) = o8;
+        const la_bf16x8 bq = *reinterpret_cast<const la_bf16x8*>(&qv);
+        la_f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, ad = a0;
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[0][0], bq, a0, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[0][1], bq, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[1][0], bq, a1, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[1][1], bq, a1, 0, 0, 0);
+        ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[0], bq, ad, 0, 0, 0);
+        ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[1], bq, ad, 0, 0, 0);
+        const float den = __shfl(ad[0], r16, 64);  // denominator of token r16 sits in lane r16 (row 0)
+        const float inv = 1.0f / (den + 1e-15f);
+        if (tok < N) {
+            unsigned short* o = out + ((int64_t)b * N + tok) * ldo + h * LA_D + 4 * g;
+            u16x4m o0, o1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o0[e] = f2b(a0[e] * inv);
+                o1[e] = f2b(a1[e] * inv);
+            }
+            *reinterpret_cast<u16x4m*>(o) = o0;
+            *reinterpret_cast<u16x4m*>(o + 16) = o1;
+        }
     }
 }
 
