@@ -48,6 +48,9 @@ SIGNATURES = {
     "eggroll_conv_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, i32, i32, vp, vp]),
     "eggroll_conv3x3_rmsnorm_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, C.c_float, vp, vp, vp, vp,
                                                vp]),
+    "eggroll_conv_nhwc_sel": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, i32, i32, vp, i32, vp]),
+    "eggroll_conv3x3_rmsnorm_nhwc_sel": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, C.c_float, vp, vp, vp,
+                                                   vp, i32, vp]),
     "eggroll_dcae_head": (C.c_int, [vp, i64, i64, i64, i64, f32, vp, vp, vp, vp, vp, vp]),
     "eggroll_linear_attention_workspace_bytes": (i64, [i64, i64, i64]),
     "eggroll_linear_attention": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, vp, i64, vp, vp]),

@@ -1472,9 +1472,10 @@ __device__ __forceinline__ void store_tile_t_act(f32x4 (&acc)[8][4], char* smem,
 // accumulators.  Row sums of squares: 16 values per lane, xor-16/32 shuffles across the wave's 4
 // column lanes, then a [BM rows][WNW waves] LDS table for the WPP = COUT / 64 waves that share a
 // pixel, summed in a fixed order.
-template <int PX, int WMW>
-__device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float* red, int wm, int wn, int lane, int m0,
-                                                      int Mp, float eps, const unsigned short* __restrict__ nw,
+// RowOf(tile row) -> the row of res (and of the output) that tile row holds.
+template <int PX, int WMW, class RowOf>
+__device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float* red, int wm, int wn, int lane,
+                                                      RowOf row_of, float eps, const unsigned short* __restrict__ nw,
                                                       const unsigned short* __restrict__ nb,
                                                       const unsigned short* __restrict__ res) {
     constexpr int WNW = 8 / WMW, BN = WNW * 64, COUT = BN / PX, WPP = COUT / 64;
@@ -1512,11 +1513,10 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
         const float* rp = red + rr * WNW + w0;
         const float tot = WPP == 4 ? (rp[0] + rp[1]) + (rp[2] + rp[3]) : rp[0] + rp[1];
         const float rs = rsqrtf(tot / COUT + eps);
-        int row = m0 + rr;
-        row = row < Mp ? row : Mp - 1;
+        const int64_t row = row_of(rr);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const u16x4 r4 = *reinterpret_cast<const u16x4*>(res + (int64_t)row * BN + wn * 64 + 16 * j + 4 * cg);
+            const u16x4 r4 = *reinterpret_cast<const u16x4*>(res + row * BN + wn * 64 + 16 * j + 4 * cg);
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[i][j][e] = acc[i][j][e] * rs * wv[j][e] + bv[j][e] + bf16_to_f32(r4[e]);
         }
@@ -1641,13 +1641,283 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     if (bias)
         lora_mfma_addend<0>(acc, lane, m0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, Mp, N);
     if constexpr (NORM) {
-        conv_rmsnorm_epilogue<PX, WMW>(acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane, m0, Mp, eps, nw,
-                                       nb, res);
+        conv_rmsnorm_epilogue<PX, WMW>(
+            acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane,
+            [&](int rr) -> int64_t { return m0 + rr < Mp ? m0 + rr : Mp - 1; }, eps, nw, nb, res);
         EGG_STAMP(4);
         store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
     } else {
         EGG_STAMP(4);
         store_tile_t_act<ACT>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, Mp, N, Y, N);
+    }
+    EGG_STAMP_DRAIN();
+    EGG_STAMP(5);
+    EGG_STAMP_RT(7);
+}
+
+// ------------------------------------------------------------------------------------
+// Halo-staged 3x3 conv (stride 1, pad 1, px 1): the tile-sliced implicit GEMM above re-stages its
+// A operand once per tap (9 x the input bytes through the LDS-DMA path, which is what bounds it:
+// DESIGN.md §5).  Here a tile is TH x TWD output pixels (16 x 32 for the 512 x 128 tile, 16 x 16
+// for 256 x 256) and its (TH+2) x (TWD+2) input halo is staged ONCE per 32-channel slice; the nine
+// taps read their A fragments from it at a pixel shift.  K-step = (slice, tap), K = 32:
+//   halo    [halo pixel][32 ch] bf16, 64-B rows, double-buffered by slice: slice s+1 streams in as
+//           one 1-KiB piece per wave at taps 0..NPW-1 of slice s
+//   weights [BN rows][32 ch] per K-step, a ring of D+1 slots, K-step k+D issued during step k
+// 64-B rows read as 16x16x32 fragments (lane: row l&15, chunk l>>4) are bank-conflict-free for any
+// run of 16 consecutive rows with slot = chunk ^ 2*((row >> 2) & 1), i.e. byte L -> L ^ ((L>>3)&32);
+// the tap shift is added to the logical byte before the swizzle.  Per K-step each wave runs two
+// phases of 16 MFMAs (A fragments 0-3, then 4-7, against the same 4 B fragments) with the p8 wave-
+// group stagger; all DMA waits are counted vmcnt (compile-time per tap, see hc_wait_n).
+// ------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wait_vmn() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WMW>
+struct HC {
+    static constexpr int WNW = 8 / WMW, BM = WMW * 128, BN = WNW * 64;
+    static constexpr int TH = 16, TWD = BM / TH;                 // output pixels of a tile
+    static constexpr int HW2 = TWD + 2, HP = (TH + 2) * HW2;     // halo pixels
+    static constexpr int NPW = (HP + 127) / 128;                 // halo pieces (16 px x 64 B) per wave
+    static constexpr int HALO = NPW * 8 * 1024;
+    static constexpr int NBW = BN / 128;                          // weight pieces per wave per K-step
+    static constexpr int BSLOT = BN * 64;
+    static constexpr int D = 3, NBUF = D + 1;                     // weight prefetch distance / ring slots
+    static constexpr int RB = 2 * HALO, LDS = 2 * HALO + NBUF * BSLOT;
+    // the halo of slice s+1 (taps 0..NPW-1 of slice s) is older than the weights of K-step (s+1, 0)
+    // (issued at tap 9-D of slice s), so the weight wait also retires the halo
+    static_assert(NPW <= 9 - D, "halo pieces must precede the next slice's first weight DMA");
+    static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+__device__ __forceinline__ uint32_t hc_swz(uint32_t L) { return L ^ ((L >> 3) & 32u); }
+
+// DMAs younger than K-step k+1's weights when step k (tap T) retires them in its second phase
+template <int WMW, int T, bool NEXT, bool LAST>
+constexpr int hc_wait_n() {
+    using G = HC<WMW>;
+    int n = 0;
+    for (int i = 2; i <= G::D; ++i)
+        if (!LAST || T + i < 9) n += G::NBW;
+    if (NEXT)
+        for (int t = T + 1 - G::D; t <= T; ++t)
+            if (t >= 0 && t < G::NPW) n += 1;
+    return n;
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void hc_static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        hc_static_for<I + 1, N>(f);
+    }
+}
+
+template <int WMW, bool NORM>
+constexpr int halo_smem_bytes() {
+    using G = HC<WMW>;
+    constexpr int need = G8<WMW>::CSTAGE + (NORM ? G::BM * G::WNW * 4 : 0);
+    return G::LDS > need ? G::LDS : need;
+}
+
+// store_tile_t (fast path only: every conv tile is full) with tile row -> output row through row_of
+template <int ACT, class RowOf>
+__device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int rbase,
+                                                int col0, unsigned short* __restrict__ Y, int64_t ldy, RowOf row_of) {
+    constexpr int ROWB = 128, SLOTS = 8;
+    char* ctile = smem + wave * (128 * ROWB);
+    const int r_l = lane & 15, c_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int rr = i * 16 + r_l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int cc = j * 16 + c_l;
+            const int slot = (cc >> 3) ^ (rr & (SLOTS - 1));
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = acc[i][j][e];
+                if constexpr (ACT == 1) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+                o[e] = f32_to_bf16(v);
+            }
+            *reinterpret_cast<u16x4*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) = o;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+    u16x8 v[16];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int rr = it * 8 + (lane >> 3), sl = lane & 7;
+        v[it] = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+    }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int rr = it * 8 + (lane >> 3);
+        *reinterpret_cast<u16x8*>(Y + row_of(rbase + rr) * ldy + col0 + (lane & 7) * 8) = v[it];
+    }
+}
+
+template <int ACT, bool NORM, int WMW>
+__global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* __restrict__ X,
+                                                         const unsigned short* __restrict__ Wt,
+                                                         const unsigned short* __restrict__ bias, int H, int W,
+                                                         int Cin, int N, int tiles_n, unsigned short* __restrict__ Y,
+                                                         float eps = 0.0f, const unsigned short* __restrict__ nw = nullptr,
+                                                         const unsigned short* __restrict__ nb = nullptr,
+                                                         const unsigned short* __restrict__ res = nullptr) {
+    using G = HC<WMW>;
+    __shared__ __attribute__((aligned(16))) char smem[halo_smem_bytes<WMW, NORM>()];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / G::WNW, wn = wave % G::WNW;
+    const int grp8 = wave >> 2;
+    // XCD-contiguous tile ranges (neighbouring tiles share halo rows and all share the weights);
+    // the N-tiles of one pixel tile are adjacent
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+    const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int n0 = tn * G::BN;
+    const int tpr = W / G::TWD, tpi = (H / G::TH) * tpr;
+    const int img = tm / tpi, trm = tm - img * tpi;
+    const int y0 = (trm / tpr) * G::TH, x0 = (trm - (trm / tpr) * tpr) * G::TWD;
+    const int K = 9 * Cin, S = Cin / 32;
+    EGG_STAMP_RT(6);
+    EGG_STAMP(0);
+
+    // halo DMA: piece i*8 + wave holds halo pixels 16p .. 16p+15; out-of-image pixels (and the pad
+    // past HP) read as zeros through an out-of-range offset
+    uint32_t hoff[G::NPW];
+#pragma unroll
+    for (int i = 0; i < G::NPW; ++i) {
+        const int hp = (i * 8 + wave) * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ (((hp >> 2) & 1) << 1);
+        const int hy = hp / G::HW2, hx = hp - hy * G::HW2;
+        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+        const bool ok = hp < G::HP && y >= 0 && y < H && x >= 0 && x < W;
+        hoff[i] = ok ? (uint32_t)(((hy * W + hx) * Cin + c * 8) * 2) : 0x80000000u;
+    }
+    uint32_t boff[G::NBW];
+#pragma unroll
+    for (int i = 0; i < G::NBW; ++i) {
+        const int n = (i * 8 + wave) * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ (((n >> 2) & 1) << 1);
+        boff[i] = (uint32_t)(((n0 + n) * K + c * 8) * 2);
+    }
+    // fragment reads: A row f of the wave at tap (0,0) as a logical halo byte; B rows + j*1024
+    uint32_t la[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+        const int m = wm * 128 + 16 * f + (lane & 15);
+        const int ty = m / G::TWD, tx = m % G::TWD;
+        la[f] = (uint32_t)((ty * G::HW2 + tx) * 64 + (lane >> 4) * 16);
+    }
+    const uint32_t lb = hc_swz((uint32_t)((wn * 64 + (lane & 15)) * 64 + (lane >> 4) * 16));
+
+    const int64_t pb = ((int64_t)img * H + y0 - 1) * W + (x0 - 1);  // halo pixel (0, 0)
+    const uint64_t xbu = (uint64_t)(X + pb * Cin);
+    const unsigned short* xb = (const unsigned short*)(
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(xbu >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xbu));
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
+
+    auto issue_b = [&](int sl, int tap, int slot) {
+        const int so = __builtin_amdgcn_readfirstlane((tap * Cin + sl * 32) * 2);
+        char* dst = smem + G::RB + slot * G::BSLOT;
+#pragma unroll
+        for (int i = 0; i < G::NBW; ++i) {
+            const uint32_t v = boff[i];
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(dst + (i * 8 + wave) * 1024), 16, v, so, 0, 0);
+        }
+    };
+    auto issue_h = [&](auto I, int sl) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t v = hoff[i];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(smem + (sl & 1) * G::HALO + (i * 8 + wave) * 1024),
+                                                 16, v, sl * 64, 0, 0);
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a[4], b[4];
+
+    hc_static_for<0, G::NPW>([&](auto I) { issue_h(I, 0); });
+#pragma unroll
+    for (int d = 0; d < G::D; ++d) issue_b(0, d, d);
+    wait_vmn<(G::D - 1) * G::NBW>();  // halo 0 + weights of K-step 0
+    P8_BAR();
+    EGG_STAMP(1);
+    if (grp8 == 1) P8_BAR();
+
+    auto slice = [&](int s, auto NEXT_, auto LAST_) {
+        constexpr bool NEXT = decltype(NEXT_)::value, LAST = decltype(LAST_)::value;
+        const char* hb = smem + (s & 1) * G::HALO;
+        hc_static_for<0, 9>([&](auto T_) {
+            constexpr int T = decltype(T_)::value;
+            constexpr uint32_t delta = (uint32_t)(((T / 3) * G::HW2 + (T % 3)) * 64);
+            const int k = s * 9 + T;
+            const char* bs = smem + G::RB + (k & (G::NBUF - 1)) * G::BSLOT;
+            // phase 1: weights + A fragments 0-3, prefetch K-step k+D's weights
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + lb + j * 1024);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[u] + delta));
+            if constexpr (!LAST || T + G::D < 9) {
+                if constexpr (T + G::D < 9) issue_b(s, T + G::D, (k + G::D) & (G::NBUF - 1));
+                else issue_b(s + 1, T + G::D - 9, (k + G::D) & (G::NBUF - 1));
+            }
+            P8_LGKM0_;
+            P8_BAR();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[u], acc[u][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            P8_BAR();
+            // phase 2: A fragments 4-7, one halo piece of slice s+1, retire K-step k+1's weights
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[4 + u] + delta));
+            if constexpr (NEXT && T < G::NPW) issue_h(std::integral_constant<int, T>{}, s + 1);
+            if constexpr (!(LAST && T == 8)) wait_vmn<hc_wait_n<WMW, T, NEXT, LAST>()>();
+            P8_LGKM0_;
+            P8_BAR();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[4 + u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[u], acc[4 + u][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            P8_BAR();
+        });
+    };
+    for (int s = 0; s < S - 1; ++s) slice(s, std::true_type{}, std::false_type{});
+    slice(S - 1, std::false_type{}, std::true_type{});
+    if (grp8 == 0) P8_BAR();
+    EGG_STAMP(2);
+    P8_VM0();
+    __syncthreads();
+    EGG_STAMP(3);
+    const int64_t prow = ((int64_t)img * H + y0) * W + x0;  // output pixel of tile row 0
+    auto row_of = [&](int r) -> int64_t { return prow + (int64_t)(r / G::TWD) * W + (r % G::TWD); };
+    if (bias)
+        lora_mfma_addend<0>(acc, lane, 0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, 1 << 30, N);
+    if constexpr (NORM) {
+        conv_rmsnorm_epilogue<1, WMW>(acc, reinterpret_cast<float*>(smem + G8<WMW>::CSTAGE), wm, wn, lane, row_of, eps,
+                                      nw, nb, res);
+        EGG_STAMP(4);
+        store_tile_rows<0>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of);
+    } else {
+        EGG_STAMP(4);
+        store_tile_rows<ACT>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of);
     }
     EGG_STAMP_DRAIN();
     EGG_STAMP(5);
@@ -1784,9 +2054,47 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
                                        rows_per_member, M, N, K, Y, ldy, T_ws, 0, stream);
 }
 
-/* Implicit-GEMM ks x ks conv, pad 1 (k_conv3x3_gemm8): see include/eggroll.h */
+}  // extern "C"
+
+// The halo-staged kernel takes 3x3 px-1 convs whose tiles are all full: H % 16 == 0, W % TWD == 0
+// (TWD = 32 for Cout 128, else 16), N % BN == 0.
+static bool halo_ok(int64_t ks, int64_t px, int64_t H, int64_t W, int64_t Cin, int64_t N) {
+    if (ks != 3 || px != 1 || H % 16 || 18 * (W + 2) * Cin * 2 >= (1ll << 31)) return false;  // 32-bit halo offsets
+    if (N == 128) return W % HC<4>::TWD == 0;
+    return N % 256 == 0 && W % HC<2>::TWD == 0;
+}
+
+template <int ACT, bool NORM>
+static void launch_halo(const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W, int64_t Cin,
+                        int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
+                        hipStream_t st) {
+    if (N == 128) {
+        const int64_t tiles = B * (H / 16) * (W / HC<4>::TWD);
+        hipLaunchKernelGGL((k_conv3x3_halo<ACT, NORM, 4>), dim3((unsigned)tiles), dim3(512), 0, st,
+                           (const unsigned short*)x, (const unsigned short*)w, (const unsigned short*)bias, (int)H,
+                           (int)W, (int)Cin, (int)N, 1, (unsigned short*)y, eps, (const unsigned short*)nw,
+                           (const unsigned short*)nb, (const unsigned short*)res);
+    } else {
+        const int64_t tiles = B * (H / 16) * (W / HC<2>::TWD), tn = N / HC<2>::BN;
+        hipLaunchKernelGGL((k_conv3x3_halo<ACT, NORM, 2>), dim3((unsigned)(tiles * tn)), dim3(512), 0, st,
+                           (const unsigned short*)x, (const unsigned short*)w, (const unsigned short*)bias, (int)H,
+                           (int)W, (int)Cin, (int)N, (int)tn, (unsigned short*)y, eps, (const unsigned short*)nw,
+                           (const unsigned short*)nb, (const unsigned short*)res);
+    }
+}
+
+extern "C" {
+
+/* Implicit-GEMM ks x ks conv, pad 1 (k_conv3x3_gemm8 / k_conv3x3_halo): see include/eggroll.h */
 int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
                       int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, void* stream) {
+    return eggroll_conv_nhwc_sel(x, w_packed, bias, B, H, W, Cin, N, ks, px, act, y, 0, stream);
+}
+
+int eggroll_conv_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
+                          int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, int32_t kernel,
+                          void* stream) {
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 2, "conv_nhwc: kernel must be 0 (auto), 1 (tap-staged) or 2 (halo)");
     EGG_CHECK_ARG(ks == 2 || ks == 3, "conv_nhwc: ks must be 2 or 3 (got %d)", ks);
     EGG_CHECK_ARG(px == 1 || px == 2, "conv_nhwc: px must be 1 or 2 (got %d)", px);
     EGG_CHECK_ARG(ks == 3 || px == 1, "conv_nhwc: px 2 needs ks 3");
@@ -1807,10 +2115,19 @@ int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int
     EGG_CHECK_ARG(x && w_packed && y, "conv_nhwc: NULL pointer");
     const int64_t tiles_m = (Mp + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "conv_nhwc: grid too large");
+    const bool hok = halo_ok(ks, px, H, W, Cin, N);
+    EGG_CHECK_ARG(kernel != 2 || hok, "conv_nhwc: the halo kernel needs ks 3, px 1, H %% 16 == 0, W %% 32 == 0 "
+                  "(Cout 128) or W %% 16 == 0 and N %% 256 == 0");
+    hipStream_t st = as_stream(stream);
+    if (hok && kernel != 1) {
+        if (act == 0) launch_halo<0, false>(x, w_packed, bias, B, H, W, Cin, N, y, 0.0f, nullptr, nullptr, nullptr, st);
+        else launch_halo<1, false>(x, w_packed, bias, B, H, W, Cin, N, y, 0.0f, nullptr, nullptr, nullptr, st);
+        EGG_CHECK_LAUNCH("conv_nhwc");
+        return EGGROLL_OK;
+    }
     int lcpt = 0;
     while ((64ll << lcpt) < Cin) ++lcpt;
     const dim3 grid((unsigned)(tiles_m * tiles_n));
-    hipStream_t st = as_stream(stream);
 #define EGG_CONV(PX_, ACT_, KS_, WMW_)                                                                          \
     hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, ACT_, false, KS_, WMW_>), grid, dim3(512), 0, st,                  \
                        (const unsigned short*)x, (const unsigned short*)w_packed, (const unsigned short*)bias, \
@@ -1839,6 +2156,15 @@ int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, 
 int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
                                  int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
                                  const void* norm_b, const void* res, void* y, void* stream) {
+    return eggroll_conv3x3_rmsnorm_nhwc_sel(x, w_packed, bias, B, H, W, Cin, N, px, eps, norm_w, norm_b, res, y, 0,
+                                            stream);
+}
+
+int eggroll_conv3x3_rmsnorm_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
+                                     int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
+                                     const void* norm_b, const void* res, void* y, int32_t kernel, void* stream) {
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 2,
+                  "conv3x3_rmsnorm_nhwc: kernel must be 0 (auto), 1 (tap-staged) or 2 (halo)");
     EGG_CHECK_ARG(px == 1 || px == 2, "conv3x3_rmsnorm_nhwc: px must be 1 or 2 (got %d)", px);
     EGG_CHECK_ARG(N == 256 || (N == 128 && px == 1),
                   "conv3x3_rmsnorm_nhwc: N = px * Cout must be 256, or 128 at px 1 (got %lld, px %d)", (long long)N, px);
@@ -1852,10 +2178,18 @@ int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void
                   "conv3x3_rmsnorm_nhwc: sizes exceed the kernel's 32-bit offsets");
     EGG_CHECK_ARG(x && w_packed && y && norm_w && res, "conv3x3_rmsnorm_nhwc: NULL pointer");
     EGG_CHECK_ARG(res != y && x != y, "conv3x3_rmsnorm_nhwc: y may not alias x or res");
+    const bool hok = halo_ok(3, px, H, W, Cin, N);
+    EGG_CHECK_ARG(kernel != 2 || hok, "conv3x3_rmsnorm_nhwc: the halo kernel needs px 1, H %% 16 == 0 and W %% 32 == 0 "
+                  "(Cout 128) or W %% 16 == 0 (Cout 256)");
+    hipStream_t st = as_stream(stream);
+    if (hok && kernel != 1) {
+        launch_halo<0, true>(x, w_packed, bias, B, H, W, Cin, N, y, eps, norm_w, norm_b, res, st);
+        EGG_CHECK_LAUNCH("conv3x3_rmsnorm_nhwc");
+        return EGGROLL_OK;
+    }
     int lcpt = 0;
     while ((64ll << lcpt) < Cin) ++lcpt;
     const dim3 grid((unsigned)((Mp + BM - 1) / BM));
-    hipStream_t st = as_stream(stream);
 #define EGG_CONVN(PX_, WMW_)                                                                                    \
     hipLaunchKernelGGL((k_conv3x3_gemm8<PX_, 0, true, 3, WMW_>), grid, dim3(512), 0, st, (const unsigned short*)x, \
                        (const unsigned short*)w_packed, (const unsigned short*)bias, (int)H, (int)W, (int)Cin, lcpt, \

@@ -595,8 +595,9 @@ def pack_conv3x3_weight(w: torch.Tensor, px: int) -> torch.Tensor:
 
 
 def conv_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], ks: int, px: int = 1,
-              act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """ks x ks conv (ks 2 or 3), zero pad 1, of x [B,H,W,Cin] NHWC bf16 -> [B, H+3-ks, W+3-ks, N/px]."""
+              act: Optional[str] = None, out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
+    """ks x ks conv (ks 2 or 3), zero pad 1, of x [B,H,W,Cin] NHWC bf16 -> [B, H+3-ks, W+3-ks, N/px].
+    kernel: 0 auto, 1 tap-staged implicit GEMM, 2 halo-staged (eggroll_conv_nhwc_sel)."""
     _dev(x, "conv(x)", torch.bfloat16)
     _dev(w_packed, "conv(w)", torch.bfloat16)
     x = x.contiguous()
@@ -612,15 +613,15 @@ def conv_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tens
     if out is None:
         out = torch.empty((B, Ho, Wo, Cout), dtype=torch.bfloat16, device=x.device)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_conv_nhwc", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, ks, px, ACT[act],
-              out.data_ptr(), _stream(x.device))
+    _lib.call("eggroll_conv_nhwc_sel", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, ks, px,
+              ACT[act], out.data_ptr(), int(kernel), _stream(x.device))
     OpTimer.end(e0, f"conv{ks}x{ks}", 2.0 * (x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout} px{px}",
                 flops=2.0 * B * Ho * Wo * Cout * ks * ks * Cin)
     return out
 
 
 def conv3x3_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], px: int,
-                 act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 act: Optional[str] = None, out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
     """3x3 conv (stride 1, pad 1) of x [B,H,W,Cin] NHWC bf16 with a pack_conv3x3_weight operand;
     bias [px*Cout] (the conv bias repeated px times) or None; act None / 'silu'.  -> [B,H,W,Cout]."""
     _dev(x, "conv3x3(x)", torch.bfloat16)
@@ -638,15 +639,16 @@ def conv3x3_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.T
     if out is None:
         out = torch.empty((B, H, W, Cout), dtype=torch.bfloat16, device=x.device)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_conv3x3_nhwc", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, px,
-              ACT[act], out.data_ptr(), _stream(x.device))
+    _lib.call("eggroll_conv_nhwc_sel", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, 3, px,
+              ACT[act], out.data_ptr(), int(kernel), _stream(x.device))
     OpTimer.end(e0, "conv3x3", 2.0 * (x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout} px{px}",
                 flops=2.0 * B * H * W * Cout * 9 * Cin)
     return out
 
 
 def conv3x3_rmsnorm_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], px: int, eps: float,
-                         norm_w: torch.Tensor, norm_b: Optional[torch.Tensor], res: torch.Tensor) -> torch.Tensor:
+                         norm_w: torch.Tensor, norm_b: Optional[torch.Tensor], res: torch.Tensor,
+                         kernel: int = 0) -> torch.Tensor:
     """conv3x3_nhwc followed by RMSNorm over channels (* norm_w + norm_b) + res, in one launch
     (the DC-AE ResBlock tail); px * Cout must be 256, or Cout = 128 at px 1 (512 x 128 tile)."""
     _dev(x, "conv3x3_rmsnorm(x)", torch.bfloat16)
@@ -665,8 +667,9 @@ def conv3x3_rmsnorm_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional
             _dev(t, f"conv3x3_rmsnorm({nm})", torch.bfloat16)
     out = torch.empty_like(res)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_conv3x3_rmsnorm_nhwc", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, px,
-              float(eps), norm_w.data_ptr(), _p(norm_b), res.data_ptr(), out.data_ptr(), _stream(x.device))
+    _lib.call("eggroll_conv3x3_rmsnorm_nhwc_sel", x.data_ptr(), w_packed.data_ptr(), _p(bias), B, H, W, Cin, N, px,
+              float(eps), norm_w.data_ptr(), _p(norm_b), res.data_ptr(), out.data_ptr(), int(kernel),
+              _stream(x.device))
     OpTimer.end(e0, "conv3x3", 2.0 * (x.numel() + 2 * out.numel()), f"{tuple(x.shape)}->{N // px} px{px} +norm",
                 flops=2.0 * B * H * W * (N // px) * 9 * Cin)
     return out

@@ -247,13 +247,23 @@ int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, 
  * phase conv of the DC-AE up-blocks (see eggroll_subpixel_shortcut).                          */
 int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
                       int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, void* stream);
+/* Kernel choice per call: 0 auto, 1 the tap-staged implicit GEMM (any shape above), 2 the halo-
+ * staged kernel (ks 3, px 1, H % 16 == 0, and W % 32 == 0 with N == 128 or W % 16 == 0 with
+ * N % 256 == 0: the input halo of a 16-row tile is staged once per 32-channel slice instead of once
+ * per tap).  Auto picks 2 whenever the shape allows it.  Results agree to fp32 summation order.  */
+int eggroll_conv_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
+                          int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, int32_t kernel,
+                          void* stream);
 /* The same conv with the ResBlock tail fused into its epilogue (conv2 -> RMSNorm -> + residual):
  *   y[p, c] = bf16(z[p, c] / sqrt(mean_c z[p, :]^2 + eps) * norm_w[c] (+ norm_b[c]) + res[p, c])
  * with z the fp32 conv output (+ bias); requires N = px * Cout = 256 (whole pixels per tile:
- * Cout 128 with px 2, Cout 256 with px 1).  res [B,H,W,Cout] bf16 (may not alias y).         */
+ * Cout 128 with px 2, Cout 256 with px 1), or Cout 128 at px 1.  res [B,H,W,Cout] bf16 (may not alias y).         */
 int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
                                  int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
                                  const void* norm_b, const void* res, void* y, void* stream);
+int eggroll_conv3x3_rmsnorm_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
+                                     int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
+                                     const void* norm_b, const void* res, void* y, int32_t kernel, void* stream);
 
 /* ReLU linear attention with head dim 32 (diffusers SanaLinearAttnProcessor2_0 and DC-AE
  * SanaMultiscaleLinearAttention): for every image b and head h over its N tokens,

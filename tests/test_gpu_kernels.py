@@ -578,6 +578,63 @@ def test_conv3x3_rmsnorm_nhwc_vs_torch(dev, B, H, W, Cin, px, Cout):
     assert bool((err <= tol).all()), f"max err {err.max().item():.3e}"
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,bias,act", [
+    (2, 16, 32, 128, 128, True, "silu"),     # 16 x 32 tile (512 x 128), halo = the whole image + pad
+    (1, 48, 96, 128, 128, False, None),      # 3 x 3 tiles: interior tiles see real halo pixels
+    (2, 32, 64, 64, 128, True, None),        # Cin 64: two 32-channel slices (no middle slice)
+    (1, 32, 64, 256, 128, True, "silu"),     # Cin 256 -> 128
+    (1, 32, 32, 256, 256, True, None),       # 16 x 16 tile (256 x 256)
+    (2, 16, 48, 64, 256, False, "silu"),     # Cin 64 -> 256
+    (1, 16, 32, 512, 512, True, None),       # N = 512: two column tiles share each pixel tile
+])
+def test_conv3x3_halo_vs_torch(dev, B, H, W, Cin, Cout, bias, act):
+    """Halo-staged conv (kernel 2) vs torch fp32 on the same bf16 inputs (same bound as the
+    tap-staged kernel), and vs the tap-staged kernel (1): both round an fp32 sum once."""
+    g = torch.Generator().manual_seed(B * 100 + H + Cin)
+    x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)
+    b = (torch.randn(Cout, generator=g) * 0.5).to(dev, torch.bfloat16) if bias else None
+    wp = K.pack_conv3x3_weight(w, 1)
+    y = K.conv3x3_nhwc(x, wp, b, 1, act, kernel=2)
+    y1 = K.conv3x3_nhwc(x, wp, b, 1, act, kernel=1)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), b.float() if bias else None, padding=1)
+    if act == "silu":
+        ref = torch.nn.functional.silu(ref)
+    ref = ref.permute(0, 2, 3, 1)
+    err = (y.float() - ref).abs()
+    tol = 2.0 ** -8 * ref.abs() + 1e-3 * ref.abs().max()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.3e} (ref max {ref.abs().max().item():.3e})"
+    d = (y.float() - y1.float()).abs()
+    assert bool((d <= 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()).all())
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 32, 128, 128), (1, 32, 64, 64, 128), (1, 32, 32, 256, 256)])
+def test_conv3x3_rmsnorm_halo_vs_torch(dev, B, H, W, Cin, Cout):
+    """conv -> RMSNorm -> + res on the halo kernel (2-D tile rows mapped to NHWC pixels)."""
+    g = torch.Generator().manual_seed(3 + W)
+    x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)
+    nw = (1 + 0.2 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
+    nb = (0.2 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
+    res = torch.randn(B, H, W, Cout, generator=g).to(dev, torch.bfloat16)
+    bias = (0.3 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
+    y = K.conv3x3_rmsnorm_nhwc(x, K.pack_conv3x3_weight(w, 1), bias, 1, 1e-5, nw, nb, res, kernel=2).float()
+    z = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), bias.float(), padding=1)
+    z = z.permute(0, 2, 3, 1)
+    ref = z * torch.rsqrt(z.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float() + nb.float() + res.float()
+    err = (y - ref).abs()
+    tol = 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.3e}"
+
+
+def test_conv3x3_halo_rejects_ragged(dev):
+    x = torch.zeros(1, 8, 8, 64, device=dev, dtype=torch.bfloat16)   # H % 16 != 0
+    w = K.pack_conv3x3_weight(torch.zeros(128, 64, 3, 3, device=dev, dtype=torch.bfloat16), 1)
+    with pytest.raises(RuntimeError):
+        K.conv3x3_nhwc(x, w, None, 1, kernel=2)
+    K.conv3x3_nhwc(x, w, None, 1, kernel=0)   # auto falls back to the tap-staged kernel
+
+
 @pytest.mark.parametrize("B,H,W,Cin,N", [(2, 6, 5, 64, 128), (1, 16, 16, 128, 512), (3, 9, 4, 256, 64)])
 def test_conv2x2_pad1_nhwc_vs_torch(dev, B, H, W, Cin, N):
     """ks = 2 implicit-GEMM conv (the up-blocks' sub-pixel phase conv, output (H+1) x (W+1)) vs torch."""

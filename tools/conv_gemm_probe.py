@@ -43,6 +43,11 @@ for B, C, hw, pxs in [(8, 128, 1024, (2, 1)), (8, 256, 512, (1, 2)), (8, 512, 25
     for px in pxs:
         wp = K.pack_conv3x3_weight(w, px)
         out = torch.empty_like(x)
+        if px == 1:  # tap-staged (1) vs halo-staged (2) kernel
+            for kern in (1, 2):
+                ms_k = t(lambda: K.conv3x3_nhwc(x, wp, None, px, None, out=out, kernel=kern))
+                row[f"k{kern}_ms"] = round(ms_k, 3)
+                row[f"k{kern}_tflops"] = round(fl / ms_k / 1e9, 1)
         ms = t(lambda: K.conv3x3_nhwc(x, wp, None, px, None, out=out))
         ms_f = t(lambda: K.conv3x3_nhwc(x, wp, b.repeat(px), px, "silu", out=out))
         ref = F.conv2d(xn.float()[:1], w.float(), None, padding=1).permute(0, 2, 3, 1)
@@ -55,6 +60,8 @@ for B, C, hw, pxs in [(8, 128, 1024, (2, 1)), (8, 256, 512, (1, 2)), (8, 512, 25
         if wp.shape[0] == 256 or (px == 1 and C == 128):  # conv2 + RMSNorm + residual fused
             nw = torch.ones(C, device=dev, dtype=torch.bfloat16)
             row[f"px{px}_norm_ms"] = round(t(lambda: K.conv3x3_rmsnorm_nhwc(x, wp, None, px, 1e-5, nw, nw, x)), 3)
+            if px == 1:
+                row["k1_norm_ms"] = round(t(lambda: K.conv3x3_rmsnorm_nhwc(x, wp, None, px, 1e-5, nw, nw, x, kernel=1)), 3)
             row["rownorm_ms"] = round(t(lambda: K.rownorm(out, 1e-5, layer=False, w=nw, b=nw, res=x)), 3)
     print(json.dumps(row), flush=True)
     del x, y, out
