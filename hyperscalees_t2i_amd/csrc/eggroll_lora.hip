@@ -1473,12 +1473,12 @@ __device__ __forceinline__ void store_tile_t_act(f32x4 (&acc)[8][4], char* smem,
 // column lanes, then a [BM rows][WNW waves] LDS table for the WPP = COUT / 64 waves that share a
 // pixel, summed in a fixed order.
 // RowOf(tile row) -> the row of res (and of the output) that tile row holds.
-template <int PX, int WMW, class RowOf>
+template <int PX, int WMW, int WNW = 8 / WMW, class RowOf>
 __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float* red, int wm, int wn, int lane,
                                                       RowOf row_of, float eps, const unsigned short* __restrict__ nw,
                                                       const unsigned short* __restrict__ nb,
                                                       const unsigned short* __restrict__ res) {
-    constexpr int WNW = 8 / WMW, BN = WNW * 64, COUT = BN / PX, WPP = COUT / 64;
+    constexpr int BN = WNW * 64, COUT = BN / PX, WPP = COUT / 64;
     static_assert(WPP == 2 || WPP == 4, "a pixel spans 2 or 4 waves");
     const int rl = lane & 15, cg = lane >> 4;
     float ss[8];
@@ -1676,29 +1676,30 @@ __device__ __forceinline__ void wait_vmn() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WMW>
+template <int WMW, int WNW = 8 / WMW>
 struct HC {
-    static constexpr int WNW = 8 / WMW, BM = WMW * 128, BN = WNW * 64;
+    static constexpr int WM_ = WMW, WN_ = WNW;
+    static constexpr int NW = WMW * WNW, BM = WMW * 128, BN = WNW * 64;  // waves, tile
     static constexpr int TH = 16, TWD = BM / TH;                 // output pixels of a tile
     static constexpr int HW2 = TWD + 2, HP = (TH + 2) * HW2;     // halo pixels
-    static constexpr int NPW = (HP + 127) / 128;                 // halo pieces (16 px x 64 B) per wave
-    static constexpr int HALO = NPW * 8 * 1024;
-    static constexpr int NBW = BN / 128;                          // weight pieces per wave per K-step
+    static constexpr int NPW = (HP + 16 * NW - 1) / (16 * NW);  // halo pieces (16 px x 64 B) per wave
+    static constexpr int HALO = NPW * NW * 1024;
+    static constexpr int NBW = BN / (16 * NW);                    // weight pieces per wave per K-step
     static constexpr int BSLOT = BN * 64;
     static constexpr int D = 3, NBUF = D + 1;                     // weight prefetch distance / ring slots
     static constexpr int RB = 2 * HALO, LDS = 2 * HALO + NBUF * BSLOT;
     // the halo of slice s+1 (taps 0..NPW-1 of slice s) is older than the weights of K-step (s+1, 0)
     // (issued at tap 9-D of slice s), so the weight wait also retires the halo
     static_assert(NPW <= 9 - D, "halo pieces must precede the next slice's first weight DMA");
-    static_assert(LDS <= 160 * 1024, "LDS");
+    static constexpr int CSTAGE = NW * 128 * 64 * 2;               // epilogue C staging (one 128x64 tile per wave)
+    static_assert(NBW >= 1 && BN % (16 * NW) == 0, "weight pieces");
 };
 
 __device__ __forceinline__ uint32_t hc_swz(uint32_t L) { return L ^ ((L >> 3) & 32u); }
 
 // DMAs younger than K-step k+1's weights when step k (tap T) retires them in its second phase
-template <int WMW, int T, bool NEXT, bool LAST>
+template <class G, int T, bool NEXT, bool LAST>
 constexpr int hc_wait_n() {
-    using G = HC<WMW>;
     int n = 0;
     for (int i = 2; i <= G::D; ++i)
         if (!LAST || T + i < 9) n += G::NBW;
@@ -1716,10 +1717,9 @@ __device__ __forceinline__ void hc_static_for(F&& f) {
     }
 }
 
-template <int WMW, bool NORM>
+template <class G, bool NORM>
 constexpr int halo_smem_bytes() {
-    using G = HC<WMW>;
-    constexpr int need = G8<WMW>::CSTAGE + (NORM ? G::BM * G::WNW * 4 : 0);
+    constexpr int need = G::CSTAGE + (NORM ? G::BM * G::WN_ * 4 : 0);
     return G::LDS > need ? G::LDS : need;
 }
 
@@ -1761,18 +1761,22 @@ __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, 
     }
 }
 
-template <int ACT, bool NORM, int WMW>
-__global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* __restrict__ X,
+// WMW x WNW waves: (4, 2) 512 x 128 and (2, 4) 256 x 256 tiles run one 8-wave workgroup per CU
+// with the two wave groups staggered by a barrier (as the p8 kernels); (2, 2) 256 x 128 runs two
+// 4-wave workgroups per CU (80 KiB LDS each), which overlap each other's prologue and epilogue.
+template <int ACT, bool NORM, int WMW, int WNW>
+__global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_halo(const unsigned short* __restrict__ X,
                                                          const unsigned short* __restrict__ Wt,
                                                          const unsigned short* __restrict__ bias, int H, int W,
                                                          int Cin, int N, int tiles_n, unsigned short* __restrict__ Y,
                                                          float eps = 0.0f, const unsigned short* __restrict__ nw = nullptr,
                                                          const unsigned short* __restrict__ nb = nullptr,
                                                          const unsigned short* __restrict__ res = nullptr) {
-    using G = HC<WMW>;
-    __shared__ __attribute__((aligned(16))) char smem[halo_smem_bytes<WMW, NORM>()];
+    using G = HC<WMW, WNW>;
+    static_assert(halo_smem_bytes<G, NORM>() * (8 / G::NW) <= 160 * 1024, "LDS per CU");
+    __shared__ __attribute__((aligned(16))) char smem[halo_smem_bytes<G, NORM>()];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave / G::WNW, wn = wave % G::WNW;
+    const int wm = wave / WNW, wn = wave % WNW;
     const int grp8 = wave >> 2;
     // XCD-contiguous tile ranges (neighbouring tiles share halo rows and all share the weights);
     // the N-tiles of one pixel tile are adjacent
@@ -1793,7 +1797,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* _
     uint32_t hoff[G::NPW];
 #pragma unroll
     for (int i = 0; i < G::NPW; ++i) {
-        const int hp = (i * 8 + wave) * 16 + (lane >> 2);
+        const int hp = (i * G::NW + wave) * 16 + (lane >> 2);
         const int c = (lane & 3) ^ (((hp >> 2) & 1) << 1);
         const int hy = hp / G::HW2, hx = hp - hy * G::HW2;
         const int y = y0 - 1 + hy, x = x0 - 1 + hx;
@@ -1803,7 +1807,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* _
     uint32_t boff[G::NBW];
 #pragma unroll
     for (int i = 0; i < G::NBW; ++i) {
-        const int n = (i * 8 + wave) * 16 + (lane >> 2);
+        const int n = (i * G::NW + wave) * 16 + (lane >> 2);
         const int c = (lane & 3) ^ (((n >> 2) & 1) << 1);
         boff[i] = (uint32_t)(((n0 + n) * K + c * 8) * 2);
     }
@@ -1831,13 +1835,13 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* _
 #pragma unroll
         for (int i = 0; i < G::NBW; ++i) {
             const uint32_t v = boff[i];
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(dst + (i * 8 + wave) * 1024), 16, v, so, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(dst + (i * G::NW + wave) * 1024), 16, v, so, 0, 0);
         }
     };
     auto issue_h = [&](auto I, int sl) {
         constexpr int i = decltype(I)::value;
         const uint32_t v = hoff[i];
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(smem + (sl & 1) * G::HALO + (i * 8 + wave) * 1024),
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(smem + (sl & 1) * G::HALO + (i * G::NW + wave) * 1024),
                                                  16, v, sl * 64, 0, 0);
     };
 
@@ -1854,7 +1858,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* _
     wait_vmn<(G::D - 1) * G::NBW>();  // halo 0 + weights of K-step 0
     P8_BAR();
     EGG_STAMP(1);
-    if (grp8 == 1) P8_BAR();
+    if (G::NW == 8 && grp8 == 1) P8_BAR();
 
     auto slice = [&](int s, auto NEXT_, auto LAST_) {
         constexpr bool NEXT = decltype(NEXT_)::value, LAST = decltype(LAST_)::value;
@@ -1886,7 +1890,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* _
 #pragma unroll
             for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[4 + u] + delta));
             if constexpr (NEXT && T < G::NPW) issue_h(std::integral_constant<int, T>{}, s + 1);
-            if constexpr (!(LAST && T == 8)) wait_vmn<hc_wait_n<WMW, T, NEXT, LAST>()>();
+            if constexpr (!(LAST && T == 8)) wait_vmn<hc_wait_n<G, T, NEXT, LAST>()>();
             P8_LGKM0_;
             P8_BAR();
             __builtin_amdgcn_s_setprio(1);
@@ -1901,7 +1905,7 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* _
     };
     for (int s = 0; s < S - 1; ++s) slice(s, std::true_type{}, std::false_type{});
     slice(S - 1, std::false_type{}, std::true_type{});
-    if (grp8 == 0) P8_BAR();
+    if (G::NW == 8 && grp8 == 0) P8_BAR();
     EGG_STAMP(2);
     P8_VM0();
     __syncthreads();
@@ -1911,8 +1915,8 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_halo(const unsigned short* _
     if (bias)
         lora_mfma_addend<0>(acc, lane, 0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, 1 << 30, N);
     if constexpr (NORM) {
-        conv_rmsnorm_epilogue<1, WMW>(acc, reinterpret_cast<float*>(smem + G8<WMW>::CSTAGE), wm, wn, lane, row_of, eps,
-                                      nw, nb, res);
+        conv_rmsnorm_epilogue<1, WMW, WNW>(acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane, row_of, eps,
+                                           nw, nb, res);
         EGG_STAMP(4);
         store_tile_rows<0>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of);
     } else {
@@ -2057,30 +2061,35 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
 }  // extern "C"
 
 // The halo-staged kernel takes 3x3 px-1 convs whose tiles are all full: H % 16 == 0, W % TWD == 0
-// (TWD = 32 for Cout 128, else 16), N % BN == 0.
-static bool halo_ok(int64_t ks, int64_t px, int64_t H, int64_t W, int64_t Cin, int64_t N) {
+// (TWD = 32 for the 512 x 128 tile, 16 for 256 x 256 and 256 x 128), N % BN == 0.  Variant v:
+// 2 = 512 x 128 (N == 128) or 256 x 256 (N % 256 == 0), one 8-wave workgroup per CU;
+// 3 = 256 x 128 (N % 128 == 0), two 4-wave workgroups per CU.
+static bool halo_ok(int v, int64_t ks, int64_t px, int64_t H, int64_t W, int64_t Cin, int64_t N) {
     if (ks != 3 || px != 1 || H % 16 || 18 * (W + 2) * Cin * 2 >= (1ll << 31)) return false;  // 32-bit halo offsets
+    if (v == 3) return N % 128 == 0 && W % HC<2, 2>::TWD == 0;
     if (N == 128) return W % HC<4>::TWD == 0;
     return N % 256 == 0 && W % HC<2>::TWD == 0;
 }
 
+template <int ACT, bool NORM, int WMW, int WNW>
+static void launch_halo_t(const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W, int64_t Cin,
+                          int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
+                          hipStream_t st) {
+    using G = HC<WMW, WNW>;
+    const int64_t tiles = B * (H / 16) * (W / G::TWD), tn = N / G::BN;
+    hipLaunchKernelGGL((k_conv3x3_halo<ACT, NORM, WMW, WNW>), dim3((unsigned)(tiles * tn)), dim3(64 * G::NW), 0, st,
+                       (const unsigned short*)x, (const unsigned short*)w, (const unsigned short*)bias, (int)H, (int)W,
+                       (int)Cin, (int)N, (int)tn, (unsigned short*)y, eps, (const unsigned short*)nw,
+                       (const unsigned short*)nb, (const unsigned short*)res);
+}
+
 template <int ACT, bool NORM>
-static void launch_halo(const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W, int64_t Cin,
-                        int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
+static void launch_halo(int v, const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W,
+                        int64_t Cin, int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
                         hipStream_t st) {
-    if (N == 128) {
-        const int64_t tiles = B * (H / 16) * (W / HC<4>::TWD);
-        hipLaunchKernelGGL((k_conv3x3_halo<ACT, NORM, 4>), dim3((unsigned)tiles), dim3(512), 0, st,
-                           (const unsigned short*)x, (const unsigned short*)w, (const unsigned short*)bias, (int)H,
-                           (int)W, (int)Cin, (int)N, 1, (unsigned short*)y, eps, (const unsigned short*)nw,
-                           (const unsigned short*)nb, (const unsigned short*)res);
-    } else {
-        const int64_t tiles = B * (H / 16) * (W / HC<2>::TWD), tn = N / HC<2>::BN;
-        hipLaunchKernelGGL((k_conv3x3_halo<ACT, NORM, 2>), dim3((unsigned)(tiles * tn)), dim3(512), 0, st,
-                           (const unsigned short*)x, (const unsigned short*)w, (const unsigned short*)bias, (int)H,
-                           (int)W, (int)Cin, (int)N, (int)tn, (unsigned short*)y, eps, (const unsigned short*)nw,
-                           (const unsigned short*)nb, (const unsigned short*)res);
-    }
+    if (v == 3) launch_halo_t<ACT, NORM, 2, 2>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+    else if (N == 128) launch_halo_t<ACT, NORM, 4, 2>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+    else launch_halo_t<ACT, NORM, 2, 4>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
 }
 
 extern "C" {
@@ -2094,7 +2103,7 @@ int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int
 int eggroll_conv_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
                           int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, int32_t kernel,
                           void* stream) {
-    EGG_CHECK_ARG(kernel >= 0 && kernel <= 2, "conv_nhwc: kernel must be 0 (auto), 1 (tap-staged) or 2 (halo)");
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 3, "conv_nhwc: kernel must be 0 (auto), 1 (tap-staged), 2 or 3 (halo)");
     EGG_CHECK_ARG(ks == 2 || ks == 3, "conv_nhwc: ks must be 2 or 3 (got %d)", ks);
     EGG_CHECK_ARG(px == 1 || px == 2, "conv_nhwc: px must be 1 or 2 (got %d)", px);
     EGG_CHECK_ARG(ks == 3 || px == 1, "conv_nhwc: px 2 needs ks 3");
@@ -2115,13 +2124,14 @@ int eggroll_conv_nhwc_sel(const void* x, const void* w_packed, const void* bias,
     EGG_CHECK_ARG(x && w_packed && y, "conv_nhwc: NULL pointer");
     const int64_t tiles_m = (Mp + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "conv_nhwc: grid too large");
-    const bool hok = halo_ok(ks, px, H, W, Cin, N);
-    EGG_CHECK_ARG(kernel != 2 || hok, "conv_nhwc: the halo kernel needs ks 3, px 1, H %% 16 == 0, W %% 32 == 0 "
-                  "(Cout 128) or W %% 16 == 0 and N %% 256 == 0");
+    const int hv = kernel == 0 ? 2 : kernel;
+    const bool hok = halo_ok(hv, ks, px, H, W, Cin, N);
+    EGG_CHECK_ARG(kernel < 2 || hok, "conv_nhwc: halo kernel %d needs ks 3, px 1, H %% 16 == 0 and W, N multiples of "
+                  "the tile (see include/eggroll.h)", kernel);
     hipStream_t st = as_stream(stream);
     if (hok && kernel != 1) {
-        if (act == 0) launch_halo<0, false>(x, w_packed, bias, B, H, W, Cin, N, y, 0.0f, nullptr, nullptr, nullptr, st);
-        else launch_halo<1, false>(x, w_packed, bias, B, H, W, Cin, N, y, 0.0f, nullptr, nullptr, nullptr, st);
+        if (act == 0) launch_halo<0, false>(hv, x, w_packed, bias, B, H, W, Cin, N, y, 0.0f, nullptr, nullptr, nullptr, st);
+        else launch_halo<1, false>(hv, x, w_packed, bias, B, H, W, Cin, N, y, 0.0f, nullptr, nullptr, nullptr, st);
         EGG_CHECK_LAUNCH("conv_nhwc");
         return EGGROLL_OK;
     }
@@ -2163,8 +2173,8 @@ int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void
 int eggroll_conv3x3_rmsnorm_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
                                      int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
                                      const void* norm_b, const void* res, void* y, int32_t kernel, void* stream) {
-    EGG_CHECK_ARG(kernel >= 0 && kernel <= 2,
-                  "conv3x3_rmsnorm_nhwc: kernel must be 0 (auto), 1 (tap-staged) or 2 (halo)");
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 3,
+                  "conv3x3_rmsnorm_nhwc: kernel must be 0 (auto), 1 (tap-staged), 2 or 3 (halo)");
     EGG_CHECK_ARG(px == 1 || px == 2, "conv3x3_rmsnorm_nhwc: px must be 1 or 2 (got %d)", px);
     EGG_CHECK_ARG(N == 256 || (N == 128 && px == 1),
                   "conv3x3_rmsnorm_nhwc: N = px * Cout must be 256, or 128 at px 1 (got %lld, px %d)", (long long)N, px);
@@ -2177,13 +2187,15 @@ int eggroll_conv3x3_rmsnorm_nhwc_sel(const void* x, const void* w_packed, const 
     EGG_CHECK_ARG(Mp < (1ll << 31) && (BM * (px + 1) + 2 * W + 8) * Cin * 2 < (1ll << 30),
                   "conv3x3_rmsnorm_nhwc: sizes exceed the kernel's 32-bit offsets");
     EGG_CHECK_ARG(x && w_packed && y && norm_w && res, "conv3x3_rmsnorm_nhwc: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)res & 7) == 0, "conv3x3_rmsnorm_nhwc: res must be 8-byte aligned");
     EGG_CHECK_ARG(res != y && x != y, "conv3x3_rmsnorm_nhwc: y may not alias x or res");
-    const bool hok = halo_ok(3, px, H, W, Cin, N);
-    EGG_CHECK_ARG(kernel != 2 || hok, "conv3x3_rmsnorm_nhwc: the halo kernel needs px 1, H %% 16 == 0 and W %% 32 == 0 "
-                  "(Cout 128) or W %% 16 == 0 (Cout 256)");
+    const int hv = kernel == 0 ? 2 : kernel;
+    const bool hok = halo_ok(hv, 3, px, H, W, Cin, N) && (hv == 2 || N == 128);  // whole pixels per tile
+    EGG_CHECK_ARG(kernel < 2 || hok, "conv3x3_rmsnorm_nhwc: halo kernel %d needs px 1, H %% 16 == 0 and W a multiple "
+                  "of the tile width (see include/eggroll.h)", kernel);
     hipStream_t st = as_stream(stream);
     if (hok && kernel != 1) {
-        launch_halo<0, true>(x, w_packed, bias, B, H, W, Cin, N, y, eps, norm_w, norm_b, res, st);
+        launch_halo<0, true>(hv, x, w_packed, bias, B, H, W, Cin, N, y, eps, norm_w, norm_b, res, st);
         EGG_CHECK_LAUNCH("conv3x3_rmsnorm_nhwc");
         return EGGROLL_OK;
     }

@@ -13,6 +13,8 @@
 namespace eggroll {
 
 typedef __attribute__((ext_vector_type(8))) unsigned short u16x8m;
+typedef __attribute__((ext_vector_type(8))) __bf16 la_bf16x8;  // MFMA 16x16x32 operand fragment
+typedef __attribute__((ext_vector_type(4))) float la_f32x4;     // MFMA 16x16 accumulator fragment
 
 __device__ __forceinline__ float b2f(unsigned short h) { return __uint_as_float(((uint32_t)h) << 16); }
 __device__ __forceinline__ unsigned short f2b(float f) {
@@ -38,12 +40,18 @@ constexpr int DW_TH = 8;   // output rows per block
 
 typedef __attribute__((ext_vector_type(4))) unsigned short u16x4m;
 
-template <int KS, bool PRE_SILU, bool GLU>
+// PW: the DC-AE multi-scale branch's grouped 1x1 conv (groups of DW_CS = 32 channels, the block's
+// channel slice) fused behind the depthwise conv: the block's bf16-rounded conv tile [256 px][32 ch]
+// goes to LDS and every wave multiplies its 64 pixels by pw[slice] [32 out][32 in] on MFMA (8 x
+// 16x16x32), fp32 accumulate, one bf16 rounding — the torch.bmm it replaces rounds the same way.
+template <int KS, bool PRE_SILU, bool GLU, bool PW = false>
 __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __restrict__ in,
                                                      const unsigned short* __restrict__ wt,   // [KS*KS][Cin]
                                                      const unsigned short* __restrict__ bias, // [Cin] or null
                                                      int H, int W, int Cin, int xtiles, int bands, int cslices,
-                                                     unsigned short* __restrict__ out) {
+                                                     unsigned short* __restrict__ out,
+                                                     const unsigned short* __restrict__ pw = nullptr) {
+    static_assert(!PW || (!GLU && DW_CS == 32 && DW_TH * DW_TW == 256), "PW: one 32-channel group per block");
     constexpr int PLANES = GLU ? 2 : 1;
     constexpr int HALO = KS / 2;
     constexpr int TR = DW_TH + KS - 1, TC = DW_TW + KS - 1;
@@ -149,7 +157,7 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
                         win[1][dx][i] = win[2][dx][i];
                     }
             }
-            if (pl == 0 && GLU) {
+            if ((pl == 0 && GLU) || PW) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) res[oy][i] = acc[i];
             } else {
@@ -159,6 +167,43 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 #pragma unroll
                     for (int i = 0; i < 4; ++i) o[i] = f2b(GLU ? res[oy][i] * silu(acc[i]) : acc[i]);
                     *reinterpret_cast<u16x4m*>(out + (((int64_t)b * H + y) * W + x) * Cout + cq) = o;
+                }
+            }
+        }
+    }
+    if constexpr (PW) {
+        // conv tile -> LDS [pixel oy*32+x][32 ch], 64-B rows with slot ^= 2*((pixel >> 2) & 1): the
+        // 16x16x32 fragment reads (16 consecutive pixels, 4 chunks) are then bank-conflict-free
+        auto swz = [](uint32_t L) { return L ^ ((L >> 3) & 32u); };
+        __syncthreads();  // every thread is done with the staged input
+#pragma unroll
+        for (int oy = 0; oy < DW_TH; ++oy) {
+            u16x4m o;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = f2b(res[oy][i]);
+            *reinterpret_cast<u16x4m*>(lds + swz((uint32_t)((oy * DW_TW + xs) * 64 + q * 8))) = o;
+        }
+        __syncthreads();
+        const int lane = tid & 63, wv = tid >> 6, r16 = lane & 15, g4 = lane >> 4;
+        const unsigned short* pg = pw + (int64_t)cs * (DW_CS * DW_CS);  // [o][c] of this channel group
+        la_bf16x8 bo[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            bo[j] = *reinterpret_cast<const la_bf16x8*>(pg + (16 * j + r16) * DW_CS + 8 * g4);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int p = wv * 64 + 16 * f + r16;  // tile pixel of this lane's fragment row
+            const la_bf16x8 a = *reinterpret_cast<const la_bf16x8*>(lds + swz((uint32_t)(p * 64 + g4 * 16)));
+            const int y = y0 + (p >> 5), xx = x0 + (p & 31);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                // transposed product: lane holds pixel p, outputs 16j + 4 g4 .. +3
+                const la_f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bo[j], a, la_f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                if (y < H && xx < W) {
+                    u16x4m o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = f2b(d[e]);
+                    *reinterpret_cast<u16x4m*>(out + (((int64_t)b * H + y) * W + xx) * Cout + c0 + 16 * j + 4 * g4) = o;
                 }
             }
         }
@@ -432,8 +477,6 @@ constexpr int LA_T = 256;                     // tokens per chunk
 // more MFMA with a row of ones as A.  Each wave covers 64 tokens (2 K-steps); the 4 waves' partials
 // are summed in a fixed order through LDS.  Products of bf16 inputs are exact in fp32, as in the VALU
 // form; only the accumulation order differs.
-typedef __attribute__((ext_vector_type(8))) __bf16 la_bf16x8;
-typedef __attribute__((ext_vector_type(4))) float la_f32x4;
 constexpr int LA_RS = LA_D + 8;  // bf16 LDS row stride (80 B: 8-B aligned rows for the transpose reads)
 typedef __attribute__((ext_vector_type(4))) short la_s4;
 typedef __attribute__((address_space(3))) la_s4 la_lds_s4;
@@ -838,6 +881,34 @@ extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* 
     else EGG_DW(5, false, false);
 #undef EGG_DW
     EGG_CHECK_LAUNCH("dwconv_nhwc");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_dwconv_pw_nhwc(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H, int64_t W,
+                                      int64_t C, int32_t ks, void* out, void* stream) {
+    EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && C > 0 && C % DW_CS == 0, "dwconv_pw: C must be a multiple of %d", DW_CS);
+    EGG_CHECK_ARG(ks == 3 || ks == 5, "dwconv_pw: ks=%d unsupported (3, 5)", ks);
+    EGG_CHECK_ARG(((uintptr_t)in & 15) == 0 && ((uintptr_t)w_t & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                      ((uintptr_t)pw & 15) == 0,
+                  "dwconv_pw: pointers must be 16-byte aligned");
+    EGG_CHECK_ARG(H * W * C < (1ll << 31), "dwconv_pw: image too large");
+    if (B == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(in && w_t && pw && out && out != in, "dwconv_pw: NULL or aliased pointer");
+    const int64_t bands = (H + DW_TH - 1) / DW_TH, xtiles = (W + DW_TW - 1) / DW_TW, cslices = C / DW_CS;
+    const int64_t nblk = B * bands * xtiles * cslices;
+    EGG_CHECK_ARG(nblk < (1ll << 31), "dwconv_pw: grid too large");
+    auto* i = (const unsigned short*)in;
+    auto* w = (const unsigned short*)w_t;
+    auto* o = (unsigned short*)out;
+    auto* p = (const unsigned short*)pw;
+    hipStream_t st = as_stream(stream);
+    if (ks == 5)
+        hipLaunchKernelGGL((k_dwconv_nhwc<5, false, false, true>), dim3((unsigned)nblk), dim3(256), 0, st, i, w, nullptr,
+                           (int)H, (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o, p);
+    else
+        hipLaunchKernelGGL((k_dwconv_nhwc<3, false, false, true>), dim3((unsigned)nblk), dim3(256), 0, st, i, w, nullptr,
+                           (int)H, (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o, p);
+    EGG_CHECK_LAUNCH("dwconv_pw_nhwc");
     return EGGROLL_OK;
 }
 

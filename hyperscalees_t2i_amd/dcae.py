@@ -155,13 +155,10 @@ class MultiscaleLinearAttention(nn.Module):
         o = torch.empty((B * H * W, inner * (1 + len(self.scales))), dtype=x.dtype, device=x.device)
         self._attend(qkv, o[:, :inner])
         for i, (ks, wdw, wpw) in enumerate(zip(self.scales, self.ms_dw, self.ms_pw)):
-            d = K.dwconv_nhwc(qkv, wdw, None, ks, pre_silu=False, glu=False)
-            g = d.view(B * H * W, 3 * self.heads, self.hd).transpose(0, 1)       # [G, n, 32]
-            pg = torch.bmm(g, wpw.transpose(1, 2))                                 # [G, n, 32], G = 3h + {q,k,v}
-            # attention reads the group-major bmm output in place (row stride 32, head stride 3 groups)
-            # instead of a transpose copy back to [n, G*32]
-            K.linear_attention(pg[0], pg[1], pg[2], B, H * W, self.heads, 3 * pg.stride(0), relu_qk=True,
-                               out=o[:, (i + 1) * inner:(i + 2) * inner])
+            # depthwise ks x ks + grouped 1x1 (G = 3h + {q,k,v} groups of 32) in one kernel, output in
+            # the qkv layout, which the attention reads like the first branch
+            pg = K.dwconv_pw_nhwc(qkv, wdw, wpw, ks).view(B * H * W, 3 * inner)
+            self._attend(pg.view(B, H, W, 3 * inner), o[:, (i + 1) * inner:(i + 2) * inner])
         y = F.linear(o.view(B, H, W, -1), self.w_out)
         return self.norm_out(y, res=x)
 

@@ -443,6 +443,26 @@ def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor]
     return out
 
 
+def dwconv_pw_nhwc(x: torch.Tensor, w_t: torch.Tensor, pw: torch.Tensor, ks: int,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Depthwise ks x ks conv (no bias) then grouped 1x1 conv (groups of 32): x [B,H,W,C] bf16,
+    w_t [ks*ks, C], pw [C/32, 32, 32] ([group][out][in]) -> [B,H,W,C] (eggroll_dwconv_pw_nhwc)."""
+    _dev(x, "dwconv_pw(x)", torch.bfloat16)
+    _dev(w_t, "dwconv_pw(w_t)", torch.bfloat16)
+    _dev(pw, "dwconv_pw(pw)", torch.bfloat16)
+    x, pw = x.contiguous(), pw.contiguous()
+    B, H, W, C = x.shape
+    if w_t.shape != (ks * ks, C) or pw.shape != (C // 32, 32, 32) or C % 32:
+        raise ValueError(f"dwconv_pw: w_t {tuple(w_t.shape)} / pw {tuple(pw.shape)} do not match C={C}, ks={ks}")
+    if out is None:
+        out = torch.empty_like(x)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_dwconv_pw_nhwc", x.data_ptr(), w_t.data_ptr(), pw.data_ptr(), B, H, W, C, ks, out.data_ptr(),
+              _stream(x.device))
+    OpTimer.end(e0, f"dwconv_pw_nhwc<{ks}>", 4.0 * B * H * W * C, f"{B}x{H}x{W}x{C}")
+    return out
+
+
 def _row_ptr(t: Optional[torch.Tensor], what: str, C: int):
     """Pointer + row stride of a [groups, C]-shaped (possibly strided) bf16 view."""
     if t is None:

@@ -193,6 +193,12 @@ int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta
 int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
                         int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
                         void* stream);
+/* The DC-AE multi-scale aggregation (diffusers SanaMultiscaleAttentionProjection: depthwise ks x ks
+ * conv, no bias, then a grouped 1x1 conv with groups of 32 channels) in one pass:
+ *   d = bf16(dwconv(in, w_t)),  out[.., 32g + o] = bf16(sum_c pw[g][o][c] * d[.., 32g + c])
+ * in / out [B,H,W,C] bf16 (C % 32 == 0, out may not alias in), pw [C/32][32][32] bf16.          */
+int eggroll_dwconv_pw_nhwc(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H,
+                           int64_t W, int64_t C, int32_t ks, void* out, void* stream);
 
 /* Model-side fused row normalisation of x [rows, C] bf16 (C % 8 == 0, C <= 4096):
  *   y = (x - mean·layer) * rsqrt(var + eps) [* w] [* (1 + mscale[g])] [+ mshift[g]] [+ b];

@@ -462,6 +462,25 @@ def test_linear_attention_interleaved_relu(dev):
     assert rel < 8e-3, rel
 
 
+@pytest.mark.parametrize("B,H,W,C,ks", [(2, 9, 13, 96, 5), (1, 64, 64, 384, 5), (2, 20, 40, 64, 3)])
+def test_dwconv_pw_vs_torch(dev, B, H, W, C, ks):
+    """Fused depthwise conv + grouped 1x1 (groups of 32) vs torch: conv2d(groups=C) in fp32 rounded to
+    bf16 (the intermediate the unfused path stores), then the grouped product in fp32."""
+    g = torch.Generator().manual_seed(C + ks)
+    x = torch.randn(B, H, W, C, generator=g).to(dev, torch.bfloat16)
+    wt = (torch.randn(ks * ks, C, generator=g) * 0.2).to(dev, torch.bfloat16)
+    pw = (torch.randn(C // 32, 32, 32, generator=g) / math.sqrt(32)).to(dev, torch.bfloat16)
+    got = K.dwconv_pw_nhwc(x, wt, pw, ks).float()
+    wc = wt.float().t().reshape(C, 1, ks, ks)
+    d = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), wc, padding=ks // 2, groups=C)
+    d = d.permute(0, 2, 3, 1).to(torch.bfloat16).float()
+    ref = torch.einsum("ngc,goc->ngo", d.reshape(-1, C // 32, 32), pw.float()).reshape(B, H, W, C)
+    err = (got - ref).abs()
+    # bf16 rounding of the intermediate can flip one ulp between the two fp32 sums; output rounded once
+    tol = 2.0 ** -7 * ref.abs() + 2e-3 * ref.abs().max()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.3e}"
+
+
 def test_multiscale_linear_attention_vs_literal(dev):
     """DC-AE SanaMultiscaleLinearAttention (both branches written into column slices of one buffer)
     vs the literal fp32 restatement: qkv proj -> [qkv, grouped-1x1(dw5x5(qkv))] -> ReLU linear
@@ -587,15 +606,17 @@ def test_conv3x3_rmsnorm_nhwc_vs_torch(dev, B, H, W, Cin, px, Cout):
     (2, 16, 48, 64, 256, False, "silu"),     # Cin 64 -> 256
     (1, 16, 32, 512, 512, True, None),       # N = 512: two column tiles share each pixel tile
 ])
-def test_conv3x3_halo_vs_torch(dev, B, H, W, Cin, Cout, bias, act):
-    """Halo-staged conv (kernel 2) vs torch fp32 on the same bf16 inputs (same bound as the
-    tap-staged kernel), and vs the tap-staged kernel (1): both round an fp32 sum once."""
+@pytest.mark.parametrize("kern", [2, 3])
+def test_conv3x3_halo_vs_torch(dev, B, H, W, Cin, Cout, bias, act, kern):
+    """Halo-staged conv (kernel 2: 512x128 / 256x256 tiles, one 8-wave workgroup per CU; kernel 3:
+    256x128 tiles, two 4-wave workgroups per CU) vs torch fp32 on the same bf16 inputs (same bound
+    as the tap-staged kernel), and vs the tap-staged kernel (1): both round an fp32 sum once."""
     g = torch.Generator().manual_seed(B * 100 + H + Cin)
     x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
     w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)
     b = (torch.randn(Cout, generator=g) * 0.5).to(dev, torch.bfloat16) if bias else None
     wp = K.pack_conv3x3_weight(w, 1)
-    y = K.conv3x3_nhwc(x, wp, b, 1, act, kernel=2)
+    y = K.conv3x3_nhwc(x, wp, b, 1, act, kernel=kern)
     y1 = K.conv3x3_nhwc(x, wp, b, 1, act, kernel=1)
     ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), b.float() if bias else None, padding=1)
     if act == "silu":
@@ -608,8 +629,10 @@ def test_conv3x3_halo_vs_torch(dev, B, H, W, Cin, Cout, bias, act):
     assert bool((d <= 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()).all())
 
 
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 32, 128, 128), (1, 32, 64, 64, 128), (1, 32, 32, 256, 256)])
-def test_conv3x3_rmsnorm_halo_vs_torch(dev, B, H, W, Cin, Cout):
+@pytest.mark.parametrize("B,H,W,Cin,Cout,kern", [(2, 16, 32, 128, 128, 2), (1, 32, 64, 64, 128, 2),
+                                                  (1, 32, 32, 256, 256, 2), (2, 16, 32, 128, 128, 3),
+                                                  (1, 32, 48, 256, 128, 3)])
+def test_conv3x3_rmsnorm_halo_vs_torch(dev, B, H, W, Cin, Cout, kern):
     """conv -> RMSNorm -> + res on the halo kernel (2-D tile rows mapped to NHWC pixels)."""
     g = torch.Generator().manual_seed(3 + W)
     x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
@@ -618,7 +641,7 @@ def test_conv3x3_rmsnorm_halo_vs_torch(dev, B, H, W, Cin, Cout):
     nb = (0.2 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
     res = torch.randn(B, H, W, Cout, generator=g).to(dev, torch.bfloat16)
     bias = (0.3 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
-    y = K.conv3x3_rmsnorm_nhwc(x, K.pack_conv3x3_weight(w, 1), bias, 1, 1e-5, nw, nb, res, kernel=2).float()
+    y = K.conv3x3_rmsnorm_nhwc(x, K.pack_conv3x3_weight(w, 1), bias, 1, 1e-5, nw, nb, res, kernel=kern).float()
     z = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), bias.float(), padding=1)
     z = z.permute(0, 2, 3, 1)
     ref = z * torch.rsqrt(z.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float() + nb.float() + res.float()

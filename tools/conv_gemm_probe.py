@@ -44,7 +44,7 @@ for B, C, hw, pxs in [(8, 128, 1024, (2, 1)), (8, 256, 512, (1, 2)), (8, 512, 25
         wp = K.pack_conv3x3_weight(w, px)
         out = torch.empty_like(x)
         if px == 1:  # tap-staged (1) vs halo-staged (2) kernel
-            for kern in (1, 2):
+            for kern in (1, 2, 3):
                 ms_k = t(lambda: K.conv3x3_nhwc(x, wp, None, px, None, out=out, kernel=kern))
                 row[f"k{kern}_ms"] = round(ms_k, 3)
                 row[f"k{kern}_tflops"] = round(fl / ms_k / 1e9, 1)
@@ -61,7 +61,9 @@ for B, C, hw, pxs in [(8, 128, 1024, (2, 1)), (8, 256, 512, (1, 2)), (8, 512, 25
             nw = torch.ones(C, device=dev, dtype=torch.bfloat16)
             row[f"px{px}_norm_ms"] = round(t(lambda: K.conv3x3_rmsnorm_nhwc(x, wp, None, px, 1e-5, nw, nw, x)), 3)
             if px == 1:
-                row["k1_norm_ms"] = round(t(lambda: K.conv3x3_rmsnorm_nhwc(x, wp, None, px, 1e-5, nw, nw, x, kernel=1)), 3)
+                for kern in (1, 3) if C == 128 else (1,):
+                    row[f"k{kern}_norm_ms"] = round(t(lambda: K.conv3x3_rmsnorm_nhwc(x, wp, None, px, 1e-5, nw, nw, x,
+                                                                                      kernel=kern)), 3)
             row["rownorm_ms"] = round(t(lambda: K.rownorm(out, 1e-5, layer=False, w=nw, b=nw, res=x)), 3)
     print(json.dumps(row), flush=True)
     del x, y, out
