@@ -68,7 +68,12 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--small", action="store_true", help="tiny architecture (smoke only; not a valid metric)")
     p.add_argument("--aux-out", type=str, default="", help="write per-phase / per-kernel details here")
-    return p.parse_args()
+    p.add_argument("--workload", choices=("sana", "var_d16"), default="sana",
+                   help="var_d16: BASELINE configs[0] (VAR-d16, LoRA r 4, 4 classes x 4 batches) on the GPU path")
+    a = p.parse_args()
+    if a.workload == "var_d16" and a.pop_per_gpu == 8 and "--pop-per-gpu" not in sys.argv:
+        a.pop_per_gpu = 4           # configs[0]: pop_size 4
+    return a
 
 
 def dist_setup(args):
@@ -105,7 +110,34 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def build_var(args, world, rank, device):
+    """BASELINE configs[0]: VAR-d16 class-conditional, LoRA r 4 / alpha 16 on the reference targets,
+    pop 4 antithetic, 4 classes x 4 batches per member (16 images at 256 px), cfg 4, top-k 900 / top-p 0.95."""
+    from hyperscalees_t2i_amd.backend import VarBackend, VarConfig
+    from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params
+    from hyperscalees_t2i_amd.es_step import DistInfo, ESConfig, ESEngine
+    from hyperscalees_t2i_amd.rewards import RewardModels
+    from hyperscalees_t2i_amd.var import VARArch
+
+    cfg = VarConfig(classes_per_gen=4, batches_per_gen=4)
+    if args.small:
+        cfg.arch = VARArch(depth=2, vae_ch=32)
+    backend = VarBackend(device=str(device), cfg=cfg)
+    backend.init_and_attach_lora()
+    params, shapes = backend.collect_lora_params()
+    theta = flatten_params(params).to(device=device, dtype=torch.float32)
+    noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=1, use_antithetic=True)
+    rewards = RewardModels.build(device, tiny=args.small)
+    pop = args.pop_per_gpu * world
+    es_cfg = ESConfig(pop_size=pop, sigma=1e-2, lr_scale=1e-1, egg_rank=1, use_antithetic=True, promptnorm=True,
+                      theta_max_norm=40.0, max_step_norm=0.0)
+    engine = ESEngine(backend, rewards, noiser, es_cfg, device, DistInfo(rank, world, None))
+    return backend, engine, noiser, theta, pop
+
+
 def build(args, world, rank, device):
+    if args.workload == "var_d16":
+        return build_var(args, world, rank, device)
     from hyperscalees_t2i_amd.backend import SanaBackend, SanaConfig
     from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params
     from hyperscalees_t2i_amd.es_step import DistInfo, ESConfig, ESEngine
@@ -211,7 +243,7 @@ def main():
     # the same kernels at one GPU's share of configs[2] (pop 64 over 8 GPUs: noise and update over
     # all 32 base samples, perturb of this GPU's 8 members) — the sizes the node-level metric runs
     aux64 = None
-    if pop != 64 and not args.small:
+    if pop != 64 and not args.small and args.workload == "sana":
         aux64 = aux_kernel_rooflines(noiser.layout, 64, 0, args.pop_per_gpu, device, theta=theta)
 
     value = pop * args.steps / elapsed
@@ -234,11 +266,31 @@ def main():
             aux["lora_project"] = {"us": v["avg_us"], "bytes": v["bytes"] / v["launches"], "GBps": v["GBps"],
                                    "frac": v["GBps"] / HBM_PEAK_GBPS, "launches": v["launches"]}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "sana":
         from oracle import cpu_baseline
         cpu = cpu_baseline.run()
         log(f"cpu baseline: {cpu['value']:.4g} member-evals/s on {cpu['cores']} threads ({cpu.pop('wall_s'):.1f}s)")
-    if rank == 0:
+    if rank == 0 and args.workload == "var_d16":
+        c = backend.cfg
+        line = {
+            "metric": "ES member-evals/sec VAR-d16 class-conditional 256px pop=4 (BASELINE configs[0] on the GPU path)",
+            "value": value, "unit": "member-evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init VAR-d16 / VQVAE ch160 / CLIP weights; no checkpoint offline)",
+            "config": {"workload": "tiny-arch smoke (INVALID as metric)" if args.small else "var_d16_256px_es_epoch",
+                       "pop_per_gpu": args.pop_per_gpu, "pop_total": pop,
+                       "images_per_member": c.classes_per_gen * c.batches_per_gen, "classes_per_gen": c.classes_per_gen,
+                       "batches_per_gen": c.batches_per_gen, "cfg": c.guidance_scale, "top_k": c.top_k, "top_p": c.top_p,
+                       "egg_rank": 1, "lora_r": c.lora_r, "lora_alpha": c.lora_alpha, "theta_D": noiser.num_params,
+                       "parallelism": f"member-shard x{world} (S all-gather)"},
+            "roofline": roofline, "cpu_baseline": None, "phases_ms": phases, "aux_kernels": aux,
+            "model_kernels": model_kernels,
+        }
+        print(json.dumps(line), flush=True)
+        if args.aux_out:
+            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
+    elif rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "member-evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,

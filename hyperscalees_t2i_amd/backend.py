@@ -12,14 +12,15 @@ from __future__ import annotations
 import json
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
 
-from .es import get_trainable_params_and_shapes, repeat_batches, sample_indices_unique
+from .es import get_trainable_params_and_shapes, repeat_batches, sample_classes_unique, sample_indices_unique
 from .lora import lora_modules
 from .pipeline import SanaOneStep
 from .sana import SANA_LORA_TARGETS, SANA_SPRINT_1_6B, SanaArch, attach_lora
+from .var import VAR_LORA_TARGETS, VARArch, VARClassGenerator, quantize_uint8_var
 
 
 class ESBackend:
@@ -226,3 +227,135 @@ class SanaBackend(ESBackend):
         pe, am = self._gather(flat_ids)
         return self.es_model.generate_population(pe, am, theta_pop, seed, guidance_scale, self.cfg.width_latent,
                                                  self.cfg.height_latent)
+
+
+# ---------------------------------------------------------------------------------------
+# VAR backend (es_backend.py:299-450) — BASELINE configs[0]
+# ---------------------------------------------------------------------------------------
+
+
+def _save_adapter(model: torch.nn.Module, save_dir: Path, cfg_dict: Dict[str, Any]) -> None:
+    from safetensors.torch import save_file
+    save_dir = Path(save_dir)
+    save_dir.mkdir(parents=True, exist_ok=True)
+    tensors = {f"base_model.model.{n}": p.detach().float().cpu().contiguous()
+               for n, p in model.named_parameters() if p.requires_grad}
+    save_file(tensors, str(save_dir / "adapter_model.safetensors"))
+    (save_dir / "adapter_config.json").write_text(json.dumps(cfg_dict, indent=2))
+
+
+def imagenet_prompt_text(class_id: int, labels_path: Union[str, Path] = "imagenet_classes.txt") -> str:
+    """utills.py:216-273 without the download: "a photo of <label>" from a local labels file
+    (one name per line); without one, the reference's own out-of-range fallback name class_<id>."""
+    p = Path(labels_path)
+    labels = [l.strip() for l in p.read_text(encoding="utf-8").splitlines() if l.strip()] if p.is_file() else []
+    name = labels[class_id] if 0 <= class_id < len(labels) else f"class_{class_id}"
+    return f"a photo of {name}"
+
+
+@dataclass
+class VarConfig:
+    """es_backend.py:299-317 (+ build knobs).  Reference CLI defaults: unifed_es.py:396-406."""
+
+    model_depth: int = 16
+    ckpt_dir: str = "checkpoints_var"
+    download_if_missing: bool = False
+    guidance_scale: float = 4.0
+    allowed_classes: Union[str, Sequence[int]] = "all"
+    classes_per_gen: int = 2
+    batches_per_gen: int = 4
+    max_log_batches: int = 1
+    torch_compile: bool = False
+    compile_mode: str = "max-autotune"
+    compile_fullgraph: bool = False
+    lora_r: int = 4
+    lora_alpha: int = 16
+    lora_dropout: float = 0.0
+    lora_target_modules: List[str] = field(default_factory=lambda: list(VAR_LORA_TARGETS))
+    # build-specific
+    arch: Optional[VARArch] = None          # None: VAR-d{model_depth} with the reference's VQVAE
+    top_k: int = 900                        # models/VAR.py:276-277 generate() defaults
+    top_p: float = 0.95
+    labels_path: str = "imagenet_classes.txt"
+    synthetic_if_missing: bool = True       # no checkpoint offline: seeded synthetic weights
+    weight_seed: int = 0
+    lora_seed: int = 1234
+    lora_b_std: float = 0.02
+    vae_chunk: int = 16
+
+
+class VarBackend(ESBackend):
+    """es_backend.py:319-450."""
+
+    def __init__(self, device: str, cfg: VarConfig):
+        self.name = "var_class"
+        self.device = device
+        self.cfg = cfg
+        self.es_model: Optional[VARClassGenerator] = None
+        self.image_to_uint8 = quantize_uint8_var
+
+    def init_and_attach_lora(self):
+        c = self.cfg
+        self.es_model = VARClassGenerator(model_depth=c.model_depth, device=self.device, arch=c.arch,
+                                          weight_seed=c.weight_seed, vae_chunk=c.vae_chunk)
+        d = Path(c.ckpt_dir)
+        vae_ckpt, var_ckpt = d / "vae_ch160v4096z32.pth", d / f"var_d{self.es_model.model_depth}.pth"
+        if vae_ckpt.is_file() and var_ckpt.is_file():
+            self.es_model.load_reference_state(torch.load(var_ckpt, map_location="cpu", weights_only=True),
+                                               torch.load(vae_ckpt, map_location="cpu", weights_only=True))
+        elif not c.synthetic_if_missing:
+            raise FileNotFoundError(f"Missing VAR checkpoints in {d} (no download offline)")
+        n = attach_lora(self.es_model.transformer, c.lora_r, c.lora_alpha, c.lora_target_modules)
+        if n == 0:
+            raise RuntimeError("no LoRA target module matched")
+        g = torch.Generator(device=self.device).manual_seed(c.lora_seed)
+        for m in lora_modules(self.es_model.transformer):
+            m.reset_lora(g, b_std=c.lora_b_std)
+        self.es_model.transformer.eval()
+
+    def collect_lora_params(self):
+        return get_trainable_params_and_shapes(self.es_model.transformer)
+
+    def save_lora(self, save_dir: Path) -> None:
+        c = self.cfg
+        _save_adapter(self.es_model.transformer, Path(save_dir),
+                      {"peft_type": "LORA", "r": c.lora_r, "lora_alpha": c.lora_alpha, "lora_dropout": c.lora_dropout,
+                       "target_modules": list(c.lora_target_modules),
+                       "base_model_name_or_path": f"FoundationVision/var (depth={self.es_model.model_depth})",
+                       "bias": "none", "task_type": None})
+
+    def _sample_classes_unique(self, seed: int, num_classes_total: int = 1000) -> List[int]:
+        return sample_classes_unique(seed, self.cfg.allowed_classes, self.cfg.classes_per_gen, num_classes_total)
+
+    def step_sampling_info(self, seed: int) -> Dict[str, Any]:
+        """es_backend.py:398-423."""
+        unique_ids = self._sample_classes_unique(seed=seed, num_classes_total=1000)
+        flat_ids = repeat_batches(unique_ids, repeats=self.cfg.batches_per_gen)
+        m = len(unique_ids)
+        txt = (lambda cid: imagenet_prompt_text(int(cid), self.cfg.labels_path))
+        log_batches = int(max(0, min(self.cfg.max_log_batches, self.cfg.batches_per_gen)))
+        return dict(unique_ids=unique_ids, flat_ids=flat_ids, unique_texts=[txt(c) for c in unique_ids],
+                    flat_texts=[txt(c) for c in flat_ids], pid_to_j={cid: j for j, cid in enumerate(unique_ids)},
+                    m=m, total_imgs_per_indiv=len(flat_ids), total_imgs_for_logging=log_batches * m,
+                    log_batches=log_batches)
+
+    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                      flat_seeds: Optional[List[int]] = None) -> List[Any]:
+        """es_backend.py:425-450: regroup flat_ids as [repeats][m], one generate call, flatten."""
+        if flat_seeds is not None:
+            raise NotImplementedError("VAR generation is seeded per call (g_seed), not per image")
+        m, r = self.cfg.classes_per_gen, self.cfg.batches_per_gen
+        if len(flat_ids) != m * r:
+            raise RuntimeError(f"VAR expected flat_ids length {m*r}, got {len(flat_ids)}")
+        grouped = [[int(flat_ids[b * m + j]) for j in range(m)] for b in range(r)]
+        imgs, _ = self.es_model.generate(seed=seed, guidance_scale=guidance_scale, class_ids=grouped,
+                                         return_grouped=True, top_k=self.cfg.top_k, top_p=self.cfg.top_p)
+        return [imgs[b][j] for b in range(r) for j in range(m)]
+
+    def generate_population(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                            theta_pop: torch.Tensor) -> torch.Tensor:
+        """The grouped [repeats][m] class ids flatten back to flat_ids (models/VAR.py:206-242), so the
+        label batch is flat_ids itself."""
+        label = torch.as_tensor([int(c) for c in flat_ids], device=self.device, dtype=torch.long)
+        return self.es_model.generate_population(label, theta_pop, seed, guidance_scale, self.cfg.top_k,
+                                                 self.cfg.top_p)

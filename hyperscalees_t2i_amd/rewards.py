@@ -202,14 +202,16 @@ class RewardModels:
         return {"clip_aes": t_clip[0], "clip_neg": t_clip[1], "clip_prompt": t_clip[2:], "pick_prompt": t_pick}
 
     @torch.no_grad()
-    def score(self, images: torch.Tensor, prompt_index: torch.Tensor, feats: Dict[str, torch.Tensor]
-              ) -> Dict[str, torch.Tensor]:
-        """images: VAE outputs [n,3,H,W] in [-1,1]; prompt_index [n] into feats' prompt rows.
-        Returns per-image fp32 tensors with the compute_all_rewards keys."""
+    def score(self, images: torch.Tensor, prompt_index: torch.Tensor, feats: Dict[str, torch.Tensor],
+              to_uint8=postprocess_uint8) -> Dict[str, torch.Tensor]:
+        """images: VAE outputs [n,3,H,W] in [-1,1]; prompt_index [n] into feats' prompt rows;
+        to_uint8: the backend's image -> PIL pixel conversion (Sana: PixArt postprocess, rounding;
+        VAR: models/VAR.py:245-259, truncation).  Returns per-image fp32 tensors with the
+        compute_all_rewards keys."""
         n = images.shape[0]
         e_clip, e_pick = [], []
         for s in range(0, n, self.image_batch):
-            px = clip_preprocess(postprocess_uint8(images[s:s + self.image_batch]))
+            px = clip_preprocess(to_uint8(images[s:s + self.image_batch]))
             e_clip.append(_image_features(self.clip, px))
             e_pick.append(_image_features(self.pick, px))
         ic = torch.cat(e_clip)

@@ -391,6 +391,97 @@ def gen_var():
     return len(recs)
 
 
+def gen_var_model():
+    """g11: VAR model-level parity (BASELINE configs[0] path at a tiny size): the reference's own
+    VAR_models (depth 2 -> width 128, 2 heads; VQVAE ch 32; V 4096, Cvae 32, the 10 default scales)
+    with deterministic synthetic weights (tests/var_weights.py, applied by parameter name) and the
+    PEFT LoRA formula y += (alpha/r) (x A^T) B^T hooked onto every target linear (r 4, alpha 16,
+    es_backend.py:334-341) from a seeded theta (the mat_qkv hook never fires: basic_var.py:93 calls
+    F.linear on mat_qkv.weight, which under PEFT is the base weight — the reference's own semantics).  One autoregressive_infer_cfg(B=2, cfg 4, top_k 900,
+    top_p 0.95, g_seed 5) on CPU fp32 records: the sampled token maps of every scale, the CFG logits
+    fed to the sampler (exact fp32 for scales 0-3 -> sampler replay; fp16 at <= 8 token positions per
+    scale for all scales -> teacher-forced logits check), f_hat and the [0, 1] image."""
+    sys.path.insert(0, str(REF))
+    sys.path.insert(0, str(OUT.parent))
+    import torch.nn as nn
+    import torch.nn.functional as F
+    import VAR_models.var as var_mod
+    from VAR_models import build_vae_var
+    from var_weights import TARGETS, TINY, synth_state, synth_theta
+    torch.manual_seed(0)
+    vae, var = build_vae_var(device="cpu", V=4096, Cvae=32, ch=TINY["vae_ch"], share_quant_resi=4,
+                             depth=TINY["depth"], shared_aln=False, attn_l2_norm=True,
+                             flash_if_available=False, fused_if_available=False)
+    var.eval(), vae.eval()
+    dec_keys = [(n, tuple(p.shape)) for n, p in vae.named_parameters()
+                if not n.startswith(("encoder.", "quant_conv."))]
+    var_keys = [(n, tuple(p.shape)) for n, p in var.named_parameters()]
+    with torch.no_grad():
+        for mod, keys in ((var, var_keys), (vae, dec_keys)):
+            st = synth_state(keys)
+            own = dict(mod.named_parameters())
+            for n, t in st.items():
+                own[n].copy_(t)
+    targets = [(n, m) for n, m in var.named_modules()
+               if isinstance(m, nn.Linear) and any(n == t or n.endswith("." + t) for t in TARGETS)]
+    r, s = TINY["lora_r"], TINY["lora_alpha"] / TINY["lora_r"]
+    shapes = []
+    for n, m in targets:
+        shapes += [(r, m.in_features), (m.out_features, r)]
+    theta = synth_theta(shapes)
+    off, hooks = 0, []
+    for n, m in targets:
+        A = theta[off:off + r * m.in_features].view(r, m.in_features)
+        off += r * m.in_features
+        Bm = theta[off:off + m.out_features * r].view(m.out_features, r)
+        off += m.out_features * r
+        hooks.append(m.register_forward_hook(
+            lambda mod, inp, out, A=A, Bm=Bm: out + s * F.linear(F.linear(inp[0], A), Bm)))
+    assert off == theta.numel()
+    rec = {"idx": [], "logits": []}
+    orig = var_mod.sample_with_top_k_top_p_
+
+    def spy(logits_BlV, **kw):
+        rec["logits"].append(logits_BlV.detach().clone())
+        idx = orig(logits_BlV, **kw)
+        rec["idx"].append(idx[:, :, 0].clone())
+        return idx
+
+    cap = {}
+    orig_f2i = vae.fhat_to_img
+
+    def f2i(f_hat):
+        cap["f_hat"] = f_hat.detach().clone()
+        return orig_f2i(f_hat)
+
+    var_mod.sample_with_top_k_top_p_ = spy
+    vae.fhat_to_img = f2i
+    labels = torch.tensor([3, 980])
+    try:
+        with torch.no_grad():
+            img = var.autoregressive_infer_cfg(B=2, label_B=labels, cfg=4.0, top_k=900, top_p=0.95, g_seed=5,
+                                               more_smooth=False)
+    finally:
+        var_mod.sample_with_top_k_top_p_ = orig
+        for h in hooks:
+            h.remove()
+    out = {"labels": labels.numpy(), "theta": theta.numpy(), "lora_shapes": np.array(shapes, np.int64),
+           "var_keys": np.array("\x1f".join(f"{n}:{'x'.join(map(str, sh))}" for n, sh in var_keys)),
+           "dec_keys": np.array("\x1f".join(f"{n}:{'x'.join(map(str, sh))}" for n, sh in dec_keys)),
+           "meta": np.array([4.0, 900, 0.95, 5], np.float64), "f_hat": cap["f_hat"].numpy(),
+           "image": img.to(torch.float16).numpy()}
+    for si, (lg, idx) in enumerate(zip(rec["logits"], rec["idx"])):
+        out[f"idx{si}"] = idx.numpy().astype(np.int16)
+        l = lg.shape[1]
+        pos = torch.linspace(0, l - 1, min(8, l)).round().long()
+        out[f"pos{si}"] = pos.numpy()
+        out[f"logit_sub{si}"] = lg[:, pos].to(torch.float16).numpy()
+        if si <= 3:
+            out[f"logit_full{si}"] = lg.numpy()
+    np.savez_compressed(OUT / "g11_var_model.npz", **out)
+    return len(out)
+
+
 def gen_es_tail(u):
     """unifed_es.py:227-281 composed from the reference's own functions (unifed_es.py itself does
     not import here: wandb / lovely_tensors / peft are absent)."""
@@ -452,6 +543,9 @@ def gen_lora(u):
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["var_model"]:          # regenerate g11 only
+        print("gen_var_model", gen_var_model())
+        raise SystemExit(0)
     u = load_reference()
     torch.set_num_threads(1)
     for fn in (gen_eps, gen_fitness, gen_update, gen_indices, gen_sampling_info, gen_es_tail, gen_lora,
@@ -459,3 +553,4 @@ if __name__ == "__main__":
         print(fn.__name__, fn(u))
     print("gen_s_aggregation", gen_s_aggregation())
     print("gen_var", gen_var())
+    print("gen_var_model", gen_var_model())

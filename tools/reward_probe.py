@@ -1,0 +1,53 @@
+"""Where the reward phase's time goes (bench N=1: 128 images of 1024^2 per epoch).
+
+    python tools/reward_probe.py [--n 128] [--iters 5]
+Times, with HIP events on the current stream: uint8 conversion + CLIP preprocessing (bit-exact
+Pillow bicubic), the CLIP-B/32 and CLIP-H/14 vision towers, and the whole RewardModels.score.
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    from hyperscalees_t2i_amd.rewards import (RewardModels, _image_features, clip_preprocess, postprocess_uint8)
+    dev = torch.device("cuda:0")
+    rm = RewardModels.build(dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    imgs = (torch.rand((a.n, 3, 1024, 1024), generator=g, device=dev) * 2.2 - 1.1).to(torch.bfloat16)
+    feats = rm.prompt_features(["a", "b", "c", "d"])
+    idx = torch.arange(a.n, device=dev) % 4
+    px = clip_preprocess(postprocess_uint8(imgs[:rm.image_batch]))
+    res = {
+        "preprocess_ms_per_batch64": timeit(lambda: clip_preprocess(postprocess_uint8(imgs[:rm.image_batch])), a.iters),
+        "clip_b32_ms_per_batch64": timeit(lambda: _image_features(rm.clip, px), a.iters),
+        "clip_h14_ms_per_batch64": timeit(lambda: _image_features(rm.pick, px), a.iters),
+        "score_ms_total": timeit(lambda: rm.score(imgs, idx, feats), a.iters),
+        "n_images": a.n,
+    }
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
