@@ -20,7 +20,7 @@ from .es import get_trainable_params_and_shapes, repeat_batches, sample_classes_
 from .lora import lora_modules
 from .pipeline import SanaOneStep
 from .sana import SANA_LORA_TARGETS, SANA_SPRINT_1_6B, SanaArch, attach_lora
-from .var import VAR_LORA_TARGETS, VARArch, VARClassGenerator, quantize_uint8_var
+from .var import VAR_LORA_TARGETS, VARArch, VARClassGenerator
 
 
 class ESBackend:
@@ -224,9 +224,14 @@ class SanaBackend(ESBackend):
 
     def generate_population(self, flat_ids: List[int], seed: int, guidance_scale: float,
                             theta_pop: torch.Tensor) -> torch.Tensor:
-        pe, am = self._gather(flat_ids)
+        """flat_ids repeats each sampled prompt batches_per_gen times (repeat_batches): the distinct
+        prompts are gathered once and every image points at its prompt's row, so the caption path
+        (caption projection, to_k / to_v of every block) runs on m instead of m*R captions per member."""
+        uniq = list(dict.fromkeys(int(f) for f in flat_ids))
+        idx = torch.tensor([uniq.index(int(f)) for f in flat_ids], device=self.device)
+        pe, am = self._gather(uniq)
         return self.es_model.generate_population(pe, am, theta_pop, seed, guidance_scale, self.cfg.width_latent,
-                                                 self.cfg.height_latent)
+                                                 self.cfg.height_latent, prompt_index=idx)
 
 
 # ---------------------------------------------------------------------------------------
@@ -292,7 +297,7 @@ class VarBackend(ESBackend):
         self.device = device
         self.cfg = cfg
         self.es_model: Optional[VARClassGenerator] = None
-        self.image_to_uint8 = quantize_uint8_var
+        self.image_pil_mode = 1          # rewards: the VAR PIL conversion (models/VAR.py:245-259)
 
     def init_and_attach_lora(self):
         c = self.cfg

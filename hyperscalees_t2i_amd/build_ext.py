@@ -39,15 +39,18 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     if not force and not _stale():
         return LIB
     BUILD.mkdir(parents=True, exist_ok=True)
-    objs = []
-    for s in SOURCES:
+    objs, procs = [], []
+    for s in SOURCES:   # the translation units compile in parallel (one hipcc each)
         obj = BUILD / (Path(s).stem + ".o")
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
                "-Wall", "-Wno-unused-function", f"-I{ROOT / 'include'}", str(CSRC / s), "-o", str(obj)]
         if verbose:
             print("[build]", " ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        procs.append((s, subprocess.Popen(cmd)))
         objs.append(str(obj))
+    failed = [s for s, pr in procs if pr.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, f"hipcc {failed}")
     tmp = LIB.with_suffix(".so.tmp")
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)]
     if verbose:

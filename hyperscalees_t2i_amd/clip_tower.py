@@ -1,0 +1,92 @@
+"""CLIP vision tower for the batched reward path (rewards.py:66-158 of the reference runs
+transformers' CLIPModel.get_image_features once per image).
+
+Same weights and the same arithmetic as transformers' CLIPVisionModel + visual_projection
+(patch conv -> [CLS] + positions -> pre-LN -> pre-norm encoder layers -> post-LN of [CLS] ->
+projection), restated for throughput on every image of every local member at once:
+  * q / k / v projections fused into one GEMM per layer ([3C, C] weight, concatenated biases);
+  * the patch-embedding conv (stride = kernel) as a patch reshape + GEMM;
+  * the LAST layer runs its attention output, MLP and residuals on the [CLS] rows only — the only
+    rows get_image_features reads (its keys / values still come from every token);
+  * one batch for all images (no per-image or per-chunk model calls).
+Numerics follow the module in bf16 (the towers are built in bf16, rewards.py:150-155).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn.functional as F
+
+ACT = {"gelu": lambda x: F.gelu(x), "quick_gelu": lambda x: x * torch.sigmoid(1.702 * x),
+       "gelu_new": lambda x: F.gelu(x, approximate="tanh")}
+
+
+class CLIPVisionTower:
+    def __init__(self, model, pad_head_dim: bool = False):
+        vm = model.vision_model
+        self.pad_head_dim = pad_head_dim
+        cfg = model.config.vision_config
+        self.C, self.heads = cfg.hidden_size, cfg.num_attention_heads
+        self.hd = self.C // self.heads
+        self.patch = cfg.patch_size
+        self.act = ACT[cfg.hidden_act]
+        emb = vm.embeddings
+        self.patch_w = emb.patch_embedding.weight.detach().reshape(self.C, -1).contiguous()     # [C, 3 p p]
+        self.cls = emb.class_embedding.detach()
+        self.pos = emb.position_embedding.weight.detach()
+        self.pre = vm.pre_layrnorm
+        self.post = vm.post_layernorm
+        self.proj = model.visual_projection.weight.detach()
+        self.layers: List[dict] = []
+        for L in vm.encoder.layers:
+            a = L.self_attn
+            self.layers.append(dict(
+                ln1=L.layer_norm1, ln2=L.layer_norm2,
+                wqkv=torch.cat([a.q_proj.weight, a.k_proj.weight, a.v_proj.weight]).detach().contiguous(),
+                bqkv=torch.cat([a.q_proj.bias, a.k_proj.bias, a.v_proj.bias]).detach().contiguous(),
+                wo=a.out_proj.weight.detach(), bo=a.out_proj.bias.detach(), scale=a.scale,
+                w1=L.mlp.fc1.weight.detach(), b1=L.mlp.fc1.bias.detach(),
+                w2=L.mlp.fc2.weight.detach(), b2=L.mlp.fc2.bias.detach()))
+
+    @staticmethod
+    def _ln(mod, x):
+        return F.layer_norm(x, mod.normalized_shape, mod.weight, mod.bias, mod.eps)
+
+    @torch.no_grad()
+    def __call__(self, pixels: torch.Tensor) -> torch.Tensor:
+        """pixels [n, 3, S, S] (normalised fp32) -> projected image embeddings [n, proj] fp32."""
+        n = pixels.shape[0]
+        p, C, H, hd = self.patch, self.C, self.heads, self.hd
+        x = pixels.to(self.patch_w.dtype)
+        g = x.shape[-1] // p                                                    # non-overlapping patches:
+        cols = x.view(n, 3, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(n, g * g, 3 * p * p)  # (c, ky, kx)
+        P = cols.shape[1]
+        tok = torch.empty((n, P + 1, C), dtype=x.dtype, device=x.device)
+        tok[:, 0] = self.cls
+        tok[:, 1:] = cols @ self.patch_w.t()
+        tok += self.pos[None, :P + 1]
+        h = self._ln(self.pre, tok)
+        T = P + 1
+        last = len(self.layers) - 1
+        for i, L in enumerate(self.layers):
+            y = self._ln(L["ln1"], h)
+            qkv = F.linear(y, L["wqkv"], L["bqkv"]).view(n, T, 3, H, hd)
+            k, v = qkv[:, :, 1].transpose(1, 2), qkv[:, :, 2].transpose(1, 2)
+            if i == last:           # only the [CLS] row is read by get_image_features
+                q = qkv[:, :1, 0].transpose(1, 2)
+                h = h[:, :1]
+            else:
+                q = qkv[:, :, 0].transpose(1, 2)
+            pad = (-hd) % 64 if self.pad_head_dim else 0
+            if pad:   # zero-padded head dims: exact (zeros in q.k, zero output columns); measured slower at 80
+                q, k, v = (F.pad(t, (0, pad)) for t in (q, k, v))
+            o = F.scaled_dot_product_attention(q, k, v, scale=L["scale"])
+            if pad:
+                o = o[..., :hd]
+            o = o.transpose(1, 2).reshape(n, -1, C)
+            h = h + F.linear(o, L["wo"], L["bo"])
+            y = self._ln(L["ln2"], h)
+            h = h + F.linear(self.act(F.linear(y, L["w1"], L["b1"])), L["w2"], L["b2"])
+        pooled = self._ln(self.post, h[:, 0])
+        return F.linear(pooled, self.proj).float()

@@ -802,6 +802,87 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
 
 using namespace eggroll;
 
+// ------------------------------------------------------------------------------------
+// CLIP image preprocessing, bit-exact with transformers' CLIPImageProcessor (PIL backend) on the
+// PIL image the reference would build from the decoder output (rewards.py:86-90, 133-147):
+//   u8 = PixArt postprocess (mode 0: rint((x/2 + 0.5).clamp(0,1) * 255), Sana) or the VAR PIL
+//        path (mode 1: fp16 ((x+1)*0.5).clamp(0,1) * 255 truncated, models/VAR.py:190, 245-259);
+//   Pillow BICUBIC resize in 8-bit fixed point (Resample.c: int32 taps of 22 fractional bits,
+//   horizontal pass first, each pass rounded + clipped to 8 bits), center crop, then
+//   (u8 / 255 - mean[c]) / std[c] in fp32 (IEEE division, as torch).
+// Tap tables (host-built from Pillow's precompute_coeffs): int32 [out][1 + KT] = {first input
+// index, KT weights (zero beyond the filter's support)}.  Pass 1 writes the horizontally resized
+// rows of the crop's columns as uint8 [n][3][H][OW]; pass 2 the normalised [n][3][OH][OW] fp32.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int clip_u8_of(float x, int mode) {
+    if (mode == 0) {
+        float v = fminf(fmaxf(x * 0.5f + 0.5f, 0.0f), 1.0f);
+        return (int)rintf(v * 255.0f);
+    }
+    // fp16 arithmetic of the reference's autocast output: every op rounded to half
+    _Float16 h = (_Float16)x;
+    h = (_Float16)(h + (_Float16)1.0f);
+    h = (_Float16)(h * (_Float16)0.5f);
+    h = h < (_Float16)0.0f ? (_Float16)0.0f : (h > (_Float16)1.0f ? (_Float16)1.0f : h);
+    h = (_Float16)(h * (_Float16)255.0f);
+    return (int)(float)h;  // .to(torch.uint8) truncates toward zero
+}
+
+__device__ __forceinline__ int pil_clip8(int ss) {
+    ss >>= 22;  // arithmetic shift: floor, as Resample.c's clip8
+    return ss < 0 ? 0 : (ss > 255 ? 255 : ss);
+}
+
+// Pass 1: one block per input row (image n, row y): the row's 3 x W pixels are converted to uint8
+// once into LDS (coalesced loads), then the 3 x OW horizontal taps are summed from LDS.
+constexpr int CLIP_MAXW = 4096;
+__global__ __launch_bounds__(256) void k_clip_resize_h(const unsigned short* __restrict__ img, int64_t sn, int64_t sc,
+                                                       int64_t sh, int64_t sw, int H, int W, int OW, int left,
+                                                       int mode, const int* __restrict__ tab, int KT,
+                                                       unsigned char* __restrict__ tmp) {
+    __shared__ unsigned char row[3 * CLIP_MAXW];
+    const int64_t n = blockIdx.x / H;
+    const int y = (int)(blockIdx.x - n * H);
+    const unsigned short* src = img + n * sn + (int64_t)y * sh;
+    for (int t = threadIdx.x; t < 3 * W; t += 256) {
+        const int x = t / 3, c = t - 3 * x;
+        row[c * W + x] = (unsigned char)clip_u8_of(b2f(src[c * sc + (int64_t)x * sw]), mode);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < 3 * OW; o += 256) {
+        const int c = o / OW, xo = o - c * OW;
+        const int* t = tab + (int64_t)(left + xo) * (KT + 1);
+        const unsigned char* r = row + c * W + t[0];
+        int ss = 1 << 21;
+        for (int k = 0; k < KT; ++k) ss += (int)r[k] * t[1 + k];
+        tmp[((n * 3 + c) * H + y) * OW + xo] = (unsigned char)pil_clip8(ss);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_clip_resize_v(const unsigned char* __restrict__ tmp, int H, int OW, int OH,
+                                                       int top, const int* __restrict__ tab, int KT, float m0,
+                                                       float m1, float m2, float s0, float s1, float s2,
+                                                       int64_t total, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int xo = (int)(i % OW);
+    int64_t r = i / OW;                    // (n, c, yo)
+    const int yo = (int)(r % OH);
+    const int64_t nc = r / OH;
+    const int c = (int)(nc % 3);
+    const int* t = tab + (int64_t)(top + yo) * (KT + 1);
+    const int y0 = t[0];
+    const unsigned char* col = tmp + nc * H * OW + xo;
+    int ss = 1 << 21;
+    for (int k = 0; k < KT; ++k) {
+        const int w = t[1 + k];
+        if (w != 0) ss += (int)col[(int64_t)(y0 + k) * OW] * w;
+    }
+    const float v = (float)pil_clip8(ss) / 255.0f;
+    const float m = c == 0 ? m0 : (c == 1 ? m1 : m2), sd = c == 0 ? s0 : (c == 1 ? s1 : s2);
+    out[i] = (v - m) / sd;
+}
+
 template <int SEG, int NCH>
 static void launch_rownorm(const void* x, int64_t rows, int C, float eps, int layer, const void* w, const void* b,
                            const void* ms, const void* mh, int64_t mstride, int64_t rpg, int act, const void* res,
@@ -1024,5 +1105,34 @@ extern "C" int eggroll_dcae_head(const void* x, int64_t B, int64_t H, int64_t W,
                        (const unsigned short*)conv_w, (const unsigned short*)conv_b, (int)xtiles, (int)bands,
                        (unsigned short*)y);
     EGG_CHECK_LAUNCH("dcae_head");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, int64_t W, int64_t sn, int64_t sc,
+                                       int64_t sh, int64_t sw, int32_t mode, const int32_t* tab_w, const int32_t* tab_h,
+                                       int32_t ktw, int32_t kth, int64_t RW, int64_t RH, int64_t out_size,
+                                       const float* mean, const float* stdv, void* tmp, void* out, void* stream) {
+    EGG_CHECK_ARG(n >= 0 && H > 0 && W > 0 && out_size > 0 && RW >= out_size && RH >= out_size, "clip_preprocess: bad sizes");
+    EGG_CHECK_ARG(mode == 0 || mode == 1, "clip_preprocess: mode %d (0 PixArt round, 1 VAR fp16 trunc)", mode);
+    EGG_CHECK_ARG(ktw > 0 && kth > 0 && ktw <= 64 && kth <= 64, "clip_preprocess: tap counts out of range");
+    if (n == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(img && tab_w && tab_h && mean && stdv && tmp && out, "clip_preprocess: NULL pointer");
+    const int left = (int)((RW - out_size) / 2), top = (int)((RH - out_size) / 2);
+    const int64_t t2 = n * 3 * out_size * out_size;
+    EGG_CHECK_ARG((t2 + 255) / 256 < (1ll << 31), "clip_preprocess: grid too large");
+    hipStream_t st = as_stream(stream);
+    EGG_CHECK_ARG(W <= CLIP_MAXW && n * H < (1ll << 31), "clip_preprocess: W=%lld > %d or too many rows",
+                  (long long)W, CLIP_MAXW);
+    hipLaunchKernelGGL(k_clip_resize_h, dim3((unsigned)(n * H)), dim3(256), 0, st, (const unsigned short*)img,
+                       sn, sc, sh, sw, (int)H, (int)W, (int)out_size, left, (int)mode, tab_w, (int)ktw,
+                       (unsigned char*)tmp);
+    EGG_CHECK_LAUNCH("clip_resize_h");
+    float m[3], sd[3];
+    // mean / std are host pointers (3 floats each): passed by value to the kernel
+    for (int k = 0; k < 3; ++k) { m[k] = mean[k]; sd[k] = stdv[k]; }
+    hipLaunchKernelGGL(k_clip_resize_v, dim3((unsigned)((t2 + 255) / 256)), dim3(256), 0, st, (const unsigned char*)tmp,
+                       (int)H, (int)out_size, (int)out_size, top, tab_h, (int)kth, m[0], m[1], m[2], sd[0], sd[1], sd[2],
+                       t2, (float*)out);
+    EGG_CHECK_LAUNCH("clip_resize_v");
     return EGGROLL_OK;
 }

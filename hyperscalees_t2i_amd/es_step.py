@@ -176,9 +176,7 @@ class ESEngine:
         mark("generate")
         feats = self.rewards.prompt_features(info["unique_texts"])
         j_of_img = torch.tensor([info["pid_to_j"][p] for p in flat_ids], device=self.device).repeat(nl)
-        to_u8 = getattr(self.backend, "image_to_uint8", None)
-        rew = (self.rewards.score(imgs, j_of_img, feats) if to_u8 is None else
-               self.rewards.score(imgs, j_of_img, feats, to_uint8=to_u8))
+        rew = self.rewards.score(imgs, j_of_img, feats, pil_mode=getattr(self.backend, "image_pil_mode", 0))
         S_local, raw_local = aggregate_member_rewards(rew, flat_ids, info["pid_to_j"], nl, m)
         if keep_images:
             n_log = self.log_imgs(info)

@@ -66,7 +66,10 @@ class SanaOneStep(ESBaseModel):
         return lat * self.sigma_data
 
     @torch.no_grad()
-    def _one_step(self, latents, prompt_embeds, prompt_attention_mask, guidance_scale, reps: int):
+    def _one_step(self, latents, prompt_embeds, prompt_attention_mask, guidance_scale, reps: int,
+                  prompt_index: Optional[torch.Tensor] = None):
+        """prompt_index (optional): [b] image -> row of prompt_embeds / mask, which then hold the
+        distinct prompts only (the images of one prompt share its caption k / v, see sana.py)."""
         b = latents.shape[0]
         lmi = latents / self.sigma_data
         t = torch.tensor(1.571, device=self.device, dtype=torch.float32)
@@ -79,8 +82,12 @@ class SanaOneStep(ESBaseModel):
         def rep(x):
             return x if reps == 1 else x.repeat(reps, *([1] * (x.ndim - 1)))  # member-major stacking
 
+        enc_index = None
+        if prompt_index is not None:
+            u = prompt_embeds.shape[0]
+            enc_index = (torch.arange(reps, device=self.device)[:, None] * u + prompt_index.to(self.device)[None, :]).reshape(-1)
         eps = self.transformer(rep(lmi.float()), rep(scm.float()), rep(prompt_embeds), rep(prompt_attention_mask),
-                               rep(guidance.float()))
+                               rep(guidance.float()), enc_index=enc_index)
         eps = torch.nan_to_num(eps.float(), nan=0.0, posinf=0.0, neginf=0.0)
         # dtype semantics of models/SanaSprint.py:138-153: eps rounded to the latent dtype (fp16) before
         # the SCM combine, which promotes to fp32 through the fp32 scm tensor; 0.267 * latents is an fp16
@@ -110,14 +117,18 @@ class SanaOneStep(ESBaseModel):
     # ---- engine API -----------------------------------------------------------------
     @torch.no_grad()
     def generate_population(self, prompt_embeds, prompt_attention_mask, theta_pop: torch.Tensor, seed: int,
-                            guidance_scale: float, width_latent: int, height_latent: int) -> torch.Tensor:
-        """All members of theta_pop [n, D] at once: returns VAE images [n*b, 3, H, W] (member-major)."""
+                            guidance_scale: float, width_latent: int, height_latent: int,
+                            prompt_index: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """All members of theta_pop [n, D] at once: returns VAE images [n*b, 3, H, W] (member-major).
+        prompt_index: [b] image -> distinct-prompt row (prompt_embeds then holds the distinct prompts)."""
         n = theta_pop.shape[0]
         self.ctx.theta_pop, self.ctx.n_members = theta_pop, n
         set_population(self.transformer, self.ctx)
         try:
-            latents = self._latents(prompt_embeds.shape[0], seed, height_latent, width_latent)
-            imgs, _ = self._one_step(latents, prompt_embeds, prompt_attention_mask, guidance_scale, reps=n)
+            b = prompt_embeds.shape[0] if prompt_index is None else prompt_index.numel()
+            latents = self._latents(b, seed, height_latent, width_latent)
+            imgs, _ = self._one_step(latents, prompt_embeds, prompt_attention_mask, guidance_scale, reps=n,
+                                     prompt_index=prompt_index)
         finally:
             set_population(self.transformer, None)
             self.ctx.theta_pop = None

@@ -22,6 +22,7 @@ the reward *contract* (dict keys, per-image scalars, combination, S aggregation)
 """
 from __future__ import annotations
 
+import ctypes
 import zlib
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -147,6 +148,54 @@ def clip_preprocess(u8: torch.Tensor, size: int = 224) -> torch.Tensor:
     return (x - mean) / std
 
 
+_TAP_CACHE: Dict[tuple, Tuple[torch.Tensor, int]] = {}
+
+
+def pil_tap_table(in_size: int, out_size: int, device) -> Tuple[torch.Tensor, int]:
+    """Pillow's bicubic 8-bit taps as the int32 table eggroll_clip_preprocess reads: [out][1 + KT] =
+    {first input index, KT taps} (identity taps when the size is unchanged: Pillow skips that pass)."""
+    key = (in_size, out_size, str(device))
+    if key not in _TAP_CACHE:
+        mat = (np.eye(in_size) * float(1 << _PIL_PRECISION_BITS) if in_size == out_size
+               else _pil_bicubic_coeffs(in_size, out_size))
+        nz = [np.nonzero(r)[0] for r in mat]
+        KT = max(int(z[-1] - z[0] + 1) for z in nz)
+        tab = np.zeros((out_size, 1 + KT), np.int64)
+        for o, z in enumerate(nz):
+            first = int(min(z[0], in_size - KT))          # keep every tap index inside the row
+            tab[o, 0] = first
+            tab[o, 1 + z[0] - first: 1 + z[-1] - first + 1] = mat[o, z[0]:z[-1] + 1]
+        _TAP_CACHE[key] = (torch.from_numpy(tab.astype(np.int32)).to(device), KT)
+    return _TAP_CACHE[key]
+
+
+def clip_pixels(images: torch.Tensor, pil_mode: int = 0, size: int = 224) -> torch.Tensor:
+    """Decoder images [n,3,H,W] (bf16, any strides) -> CLIP pixel values [n,3,size,size] fp32 on the
+    HIP path (eggroll_clip_preprocess): the uint8 PIL conversion of the backend (pil_mode 0: PixArt
+    postprocess, rounding; 1: the VAR PIL path, fp16 + truncation), Pillow's bicubic resize of the
+    short edge, center crop, CLIP normalisation — bitwise equal to
+    clip_preprocess(postprocess_uint8(images)) / clip_preprocess(quantize_uint8_var(images))."""
+    from . import _lib
+    from .kernels import _stream
+    if images.device.type != "cuda" or images.dtype != torch.bfloat16:
+        raise _lib.EggrollError("clip_pixels: expected a bf16 ROCm tensor (no CPU fallback)")
+    n, c, h, w = images.shape
+    if c != 3:
+        raise ValueError(f"clip_pixels: expected 3 channels, got {c}")
+    nh, nw = (size, int(size * w / h)) if h <= w else (int(size * h / w), size)
+    tw, ktw = pil_tap_table(w, nw, images.device)
+    th, kth = pil_tap_table(h, nh, images.device)
+    out = torch.empty((n, 3, size, size), dtype=torch.float32, device=images.device)
+    tmp = torch.empty((max(n * 3 * h * size, 1),), dtype=torch.uint8, device=images.device)
+    mean = (ctypes.c_float * 3)(*CLIP_MEAN)
+    std = (ctypes.c_float * 3)(*CLIP_STD)
+    sn, sc, sh, sw = images.stride()
+    _lib.call("eggroll_clip_preprocess", images.data_ptr(), n, h, w, sn, sc, sh, sw, int(pil_mode), tw.data_ptr(),
+              th.data_ptr(), ktw, kth, nw, nh, size, ctypes.cast(mean, ctypes.c_void_p),
+              ctypes.cast(std, ctypes.c_void_p), tmp.data_ptr(), out.data_ptr(), _stream(images.device))
+    return out
+
+
 def build_clip(cfg: dict, device, seed: int, dtype=torch.bfloat16):
     from transformers import CLIPConfig, CLIPModel
     torch.manual_seed(seed)
@@ -180,7 +229,14 @@ class RewardModels:
     clip: object
     pick: object
     mix_weights: Tuple[float, ...] = (0.0, 0.0, 0.0, 1.0)  # unifed_es.py:360-363 defaults (length 3 or 4)
-    image_batch: int = 64
+    image_batch: int = 256
+    _towers: Optional[tuple] = None
+
+    def towers(self):
+        if self._towers is None:
+            from .clip_tower import CLIPVisionTower
+            self._towers = (CLIPVisionTower(self.clip), CLIPVisionTower(self.pick))
+        return self._towers
 
     @classmethod
     def build(cls, device, mix_weights=(0.0, 0.0, 0.0, 1.0), tiny: bool = False, seed: int = 7):
@@ -203,17 +259,18 @@ class RewardModels:
 
     @torch.no_grad()
     def score(self, images: torch.Tensor, prompt_index: torch.Tensor, feats: Dict[str, torch.Tensor],
-              to_uint8=postprocess_uint8) -> Dict[str, torch.Tensor]:
-        """images: VAE outputs [n,3,H,W] in [-1,1]; prompt_index [n] into feats' prompt rows;
-        to_uint8: the backend's image -> PIL pixel conversion (Sana: PixArt postprocess, rounding;
-        VAR: models/VAR.py:245-259, truncation).  Returns per-image fp32 tensors with the
+              pil_mode: int = 0) -> Dict[str, torch.Tensor]:
+        """images: decoder outputs [n,3,H,W] in [-1,1] (bf16); prompt_index [n] into feats' prompt
+        rows; pil_mode: the backend's image -> PIL conversion (0 Sana: PixArt postprocess, rounding;
+        1 VAR: models/VAR.py:245-259, fp16 + truncation).  Returns per-image fp32 tensors with the
         compute_all_rewards keys."""
         n = images.shape[0]
+        t_clip, t_pick = self.towers()
         e_clip, e_pick = [], []
         for s in range(0, n, self.image_batch):
-            px = clip_preprocess(to_uint8(images[s:s + self.image_batch]))
-            e_clip.append(_image_features(self.clip, px))
-            e_pick.append(_image_features(self.pick, px))
+            px = clip_pixels(images[s:s + self.image_batch].to(torch.bfloat16), pil_mode)
+            e_clip.append(t_clip(px))
+            e_pick.append(t_pick(px))
         ic = torch.cat(e_clip)
         ic = ic / ic.norm(dim=-1, keepdim=True).clamp_min(1e-6)  # rewards.py:99
         ip = torch.cat(e_pick)

@@ -149,19 +149,24 @@ class CrossAttention(nn.Module):
         self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
         self.pad_head_dim = True   # pad the SDPA head dim to a multiple of 64 (exact, see forward)
 
-    def forward(self, x, enc, mask_bias):  # x [B,N,D], enc [B,L,D], mask_bias [B,1,1,L]
+    def forward(self, x, enc, mask_bias, enc_index=None):
+        """x [B,N,D]; enc [U,L,D] caption rows; mask_bias [B,1,1,L]; enc_index [B] (image -> caption
+        row, None: U == B).  Images that share a caption share its k / v rows, so to_k / to_v (and the
+        caption projection before them) run once per distinct caption and the rows are gathered."""
         B, N, _ = x.shape
-        L = enc.shape[1]
+        U, L = enc.shape[0], enc.shape[1]
         hd = self.head_dim
         q = self.norm_q(self.to_q(x)).view(B, N, self.heads, hd)
-        k = self.norm_k(self.to_k(enc)).view(B, L, self.heads, hd)
-        v = self.to_v(enc).view(B, L, self.heads, hd)
+        k = self.norm_k(self.to_k(enc)).view(U, L, self.heads, hd)
+        v = self.to_v(enc).view(U, L, self.heads, hd)
         pad = (-hd) % 64 if self.pad_head_dim else 0
         if pad:
             # SDPA at head dim 112 runs ~2.7x slower than at 128 on gfx950; zero-padded dims add exact
             # zeros to q.k and give zero output columns, so with the 1/sqrt(112) scale passed explicitly
             # the result is bit-identical (tools/xattn_pad_probe.py, tests/test_gpu_engine.py)
             q, k, v = (F.pad(t, (0, pad)) for t in (q, k, v))
+        if enc_index is not None:
+            k, v = k.index_select(0, enc_index), v.index_select(0, enc_index)
         o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
                                            attn_mask=mask_bias, scale=hd ** -0.5)
         if pad:
@@ -198,13 +203,13 @@ class SanaBlock(nn.Module):
         self.ff = GLUMBConv(D, int(a.mlp_ratio * D))
         self.scale_shift_table = nn.Parameter(torch.randn(6, D).div(D ** 0.5).to(torch.bfloat16), requires_grad=False)
 
-    def forward(self, x, enc, mask_bias, timestep, H, W):
+    def forward(self, x, enc, mask_bias, timestep, H, W, enc_index=None):
         B, N, D = x.shape
         # [B, 6, D]: shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
         mods = (self.scale_shift_table[None] + timestep.view(B, 6, -1)).contiguous()
         n = K.rownorm(x, self.eps, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=N)
         K.gated_residual_(x, self.attn1(n), mods[:, 2], rows_per_group=N)
-        x = x + self.attn2(x, enc, mask_bias)
+        x = x + self.attn2(x, enc, mask_bias, enc_index)
         n = K.rownorm(x, self.eps, layer=True, mscale=mods[:, 4], mshift=mods[:, 3], rows_per_group=N)
         K.gated_residual_(x, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
         return x
@@ -250,7 +255,12 @@ class SanaTransformer2DModel(nn.Module):
             else:
                 p.zero_()
 
-    def forward(self, hidden_states, timestep, encoder_hidden_states, encoder_attention_mask, guidance):
+    def forward(self, hidden_states, timestep, encoder_hidden_states, encoder_attention_mask, guidance,
+                enc_index=None):
+        """enc_index (optional, build-specific): [B] image -> row of encoder_hidden_states /
+        encoder_attention_mask, which then hold only the DISTINCT captions (the caption projection,
+        caption norm and every block's to_k / to_v run once per distinct caption).  None: one caption
+        row per image, as diffusers' SanaTransformer2DModel."""
         B, C, H, W = hidden_states.shape
         a = self.config
         x = hidden_states.to(torch.bfloat16).permute(0, 2, 3, 1).reshape(B, H * W, C)
@@ -269,9 +279,12 @@ class SanaTransformer2DModel(nn.Module):
                 encoder_attention_mask = encoder_attention_mask[:, :L_eff]
         enc = self.caption_projection(encoder_hidden_states.to(torch.bfloat16))
         enc = self.caption_norm(enc)
-        mask_bias = ((1.0 - encoder_attention_mask.to(torch.bfloat16)) * -10000.0).view(B, 1, 1, -1)
+        mask_bias = (1.0 - encoder_attention_mask.to(torch.bfloat16)) * -10000.0
+        if enc_index is not None:
+            mask_bias = mask_bias.index_select(0, enc_index)
+        mask_bias = mask_bias.view(B, 1, 1, -1)
         for blk in self.transformer_blocks:
-            x = blk(x, enc, mask_bias, timestep6, H, W)
+            x = blk(x, enc, mask_bias, timestep6, H, W, enc_index)
         mods = (self.scale_shift_table[None] + emb_t[:, None]).contiguous()     # [B, 2, D]: shift, scale
         x = K.rownorm(x, a.norm_eps, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=H * W)
         x = self.proj_out(x)

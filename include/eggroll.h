@@ -282,6 +282,20 @@ int eggroll_linear_attention(const void* q, const void* k, const void* v, int64_
                              int64_t B, int64_t N, int64_t heads, int32_t relu_qk, void* out, int64_t ldo,
                              void* workspace, void* stream);
 
+/* CLIP image preprocessing of decoder outputs for the reward towers, bit-exact with transformers'
+ * CLIPImageProcessor (PIL backend) on the PIL image the reference builds (rewards.py:86-90,133-147):
+ *   u8 = mode 0: rint((x/2 + 0.5).clamp(0,1) * 255)    (PixArtImageProcessor.postprocess, Sana)
+ *        mode 1: fp16 ((x+1)*0.5).clamp(0,1) * 255, truncated  (models/VAR.py:190, 245-259)
+ *   Pillow BICUBIC 8-bit fixed-point resize to RH x RW (horizontal pass first, clip8 per pass),
+ *   center crop out_size^2, out = (u8/255 - mean[c]) / std[c]  fp32 [n, 3, out, out].
+ * img: bf16, element (i, c, y, x) at img[i*sn + c*sc + y*sh + x*sw]; tab_w [RW][1+ktw] / tab_h
+ * [RH][1+kth] int32 device tables {first input index, taps}; mean / std: 3 floats (host);
+ * tmp: device scratch of n*3*H*out_size bytes.                                                  */
+int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, int64_t W, int64_t sn, int64_t sc, int64_t sh,
+                            int64_t sw, int32_t mode, const int32_t* tab_w, const int32_t* tab_h, int32_t ktw,
+                            int32_t kth, int64_t RW, int64_t RH, int64_t out_size, const float* mean,
+                            const float* stdv, void* tmp, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -108,3 +108,39 @@ def test_clip_preprocess_on_device_1024(dev):
     ours = clip_preprocess(postprocess_uint8(x.to(dev))).cpu().numpy()
     ref = CLIPImageProcessorPil()(images=pils, return_tensors="pt")["pixel_values"].numpy()
     assert np.abs(ours - ref).max() <= 2e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W", [(1024, 1024), (256, 256), (224, 336), (300, 200), (97, 301)])
+def test_clip_pixels_hip_bitexact(dev, H, W):
+    """eggroll_clip_preprocess (one HIP pass per resize direction, int32 Pillow taps, fused uint8
+    conversion and normalisation) == the torch restatement on the CPU, which
+    test_clip_preprocess_matches_transformers_processor pins to transformers bit for bit; both PIL
+    conversions (0: PixArt rounding, Sana; 1: fp16 + truncation, VAR); NHWC-strided input."""
+    from hyperscalees_t2i_amd.rewards import clip_pixels
+    from hyperscalees_t2i_amd.var import quantize_uint8_var
+    x = _images(3, H, W, H * 3 + W).to(torch.bfloat16)
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last)
+    for mode, to_u8 in ((0, lambda t: postprocess_uint8(t)), (1, quantize_uint8_var)):
+        ref = clip_preprocess(to_u8(x)).numpy()
+        ours = clip_pixels(xd, mode).cpu().numpy()
+        assert ours.shape == ref.shape == (3, 3, 224, 224)
+        assert np.array_equal(ours, ref), (mode, float(np.abs(ours - ref).max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["tiny", "b32", "h14"])
+def test_clip_vision_tower_matches_transformers(dev, which):
+    """The fused reward tower (one qkv GEMM, unfold patch GEMM, [CLS]-only last layer, padded SDPA
+    head dim) vs transformers' CLIPModel.get_image_features on the same bf16 weights and pixels."""
+    from hyperscalees_t2i_amd.clip_tower import CLIPVisionTower
+    from hyperscalees_t2i_amd.rewards import CLIP_B32, CLIP_H14, CLIP_TINY, _image_features, build_clip
+    model = build_clip({"tiny": CLIP_TINY, "b32": CLIP_B32, "h14": CLIP_H14}[which], dev, seed=5)
+    g = torch.Generator(device=dev).manual_seed(1)
+    px = torch.randn((6, 3, 224, 224), generator=g, device=dev)
+    ref = _image_features(model, px)
+    ours = CLIPVisionTower(model)(px)
+    rel = float((ours - ref).norm() / ref.norm())
+    cos = float(torch.nn.functional.cosine_similarity(ours, ref, dim=-1).min())
+    print(f"[clip tower {which}] rel {rel:.2e} min cos {cos:.6f}")
+    assert rel < 2e-2 and cos > 0.9995

@@ -132,7 +132,12 @@ def test_member_eval_bf16_vs_fp32_with_reference_noise(stack, dev, golden, case)
         for li, (a, b) in enumerate(zip(lin_out, rec)):
             a2 = a.reshape(-1, a.shape[-1])
             a2 = a2.view(pop, -1, a2.shape[-1])[k]
-            e = rel(a2, b.reshape(-1, b.shape[-1]))
+            b2 = b.reshape(-1, b.shape[-1])
+            if a2.shape[0] * (B // m) == b2.shape[0]:
+                # caption path (caption projection, attn2 to_k / to_v): the build evaluates the m distinct
+                # prompts once per member; flat = repeat_batches(unique, R) puts them first, in order
+                b2 = b2[: a2.shape[0]]
+            e = rel(a2, b2)
             per_lin[li] = max(per_lin.get(li, 0.0), e)
             worst["lora_rel"] = max(worst["lora_rel"], e)
         worst["eps_rel"] = max(worst["eps_rel"], rel(tr_out[0][k * B:(k + 1) * B], eps32))
