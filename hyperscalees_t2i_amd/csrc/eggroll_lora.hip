@@ -645,9 +645,53 @@ __device__ __forceinline__ void lora_epilogue(f32x4 (&acc)[WTM / 16][WTN / 16], 
 // Store of a transposed (TR) 128x64 wave tile: acc[i][j][e] = Y[rbase + 16 i + (l & 15)]
 // [cbase + 16 j + 4 (l >> 4) + e]; 4 columns -> one ds_write_b64 into the wave's swizzled LDS
 // staging tile, then 16-B global stores of whole 128-B row segments.
+// Epilogue ops applied to the bf16-rounded GEMM output y (one rounding per torch op it replaces):
+//   EPI_SILU  : out = bf16(silu(y))                        (GLUMBConv: 1x1 conv -> SiLU)
+//   EPI_RES   : out = bf16(res + y)                        (x = x + attn2(...))
+//   EPI_GATED : out = bf16(res + gate[row / rpg] * y)      (x += gate * attn1(...), k_gated_residual)
+// res may alias Y (each element is read and written by the same lane).
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3 };
+struct EpiArgs {
+    const unsigned short* res;
+    int64_t ldr;
+    const unsigned short* gate;
+    int64_t gstride;
+    int64_t rpg;
+};
+__device__ __forceinline__ float epi_silu(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
+
+template <int EPI>
+__device__ __forceinline__ u16x8 epi_apply(u16x8 v, int row, int col, const EpiArgs& ea) {
+    if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(epi_silu(bf16_to_f32(v[u])));
+    } else if constexpr (EPI == EPI_RES || EPI == EPI_GATED) {
+        const u16x8 r = *reinterpret_cast<const u16x8*>(ea.res + (int64_t)row * ea.ldr + col);
+        if constexpr (EPI == EPI_RES) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(bf16_to_f32(r[u]) + bf16_to_f32(v[u]));
+        } else {
+            const u16x8 g = *reinterpret_cast<const u16x8*>(ea.gate + (row / ea.rpg) * ea.gstride + col);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(bf16_to_f32(r[u]) + bf16_to_f32(g[u]) * bf16_to_f32(v[u]));
+        }
+    }
+    return v;
+}
+template <int EPI>
+__device__ __forceinline__ unsigned short epi_apply1(unsigned short v, int row, int col, const EpiArgs& ea) {
+    if constexpr (EPI == EPI_SILU) return f32_to_bf16(epi_silu(bf16_to_f32(v)));
+    if constexpr (EPI == EPI_RES) return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) + bf16_to_f32(v));
+    if constexpr (EPI == EPI_GATED)
+        return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) +
+                           bf16_to_f32(ea.gate[(row / ea.rpg) * ea.gstride + col]) * bf16_to_f32(v));
+    return v;
+}
+
+template <int EPI = EPI_NONE>
 __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int m0, int n0,
                                              int rbase, int cbase, int M, int N, unsigned short* __restrict__ Y,
-                                             int64_t ldy) {
+                                             int64_t ldy, const EpiArgs& ea = EpiArgs{}) {
     constexpr int ROWB = 128, SLOTS = 8;
     char* ctile = smem + wave * (128 * ROWB);
     const int r_l = lane & 15, c_l = (lane >> 4) * 4;
@@ -666,14 +710,22 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
     const bool full = m0 + rbase + 128 <= M && n0 + cbase + 64 <= N && (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0;
-    if (full) {  // interior wave tile: all 16 row reads in flight, then 16 unconditional 16-B stores
+    const bool epi_vec = EPI == EPI_NONE || EPI == EPI_SILU ||
+                         ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
+                          (EPI != EPI_GATED || ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0)));
+    if (full && epi_vec) {  // interior wave tile: all 16 row reads in flight, then 16 unconditional 16-B stores
         u16x8 v[16];
 #pragma unroll
         for (int it = 0; it < 16; ++it) {
             const int rr = it * 8 + (lane >> 3), sl = lane & 7;
             v[it] = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
         }
-        unsigned short* dst = Y + (int64_t)(m0 + rbase + (lane >> 3)) * ldy + n0 + cbase + (lane & 7) * 8;
+        const int row0 = m0 + rbase + (lane >> 3), col0 = n0 + cbase + (lane & 7) * 8;
+        if constexpr (EPI != EPI_NONE) {
+#pragma unroll
+            for (int it = 0; it < 16; ++it) v[it] = epi_apply<EPI>(v[it], row0 + it * 8, col0, ea);
+        }
+        unsigned short* dst = Y + (int64_t)row0 * ldy + col0;
 #pragma unroll
         for (int it = 0; it < 16; ++it) *reinterpret_cast<u16x8*>(dst + (int64_t)it * 8 * ldy) = v[it];
         return;
@@ -684,12 +736,13 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
         const int row = m0 + rbase + rr;
         const int col = n0 + cbase + sl * 8;
         if (row >= M || col >= N) continue;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+        u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
         unsigned short* dst = Y + (int64_t)row * ldy + col;
-        if (col + 8 <= N && (((uintptr_t)dst) & 15) == 0) {
+        if (col + 8 <= N && (((uintptr_t)dst) & 15) == 0 && epi_vec) {
+            if constexpr (EPI != EPI_NONE) v = epi_apply<EPI>(v, row, col, ea);
             *reinterpret_cast<u16x8*>(dst) = v;
         } else {
-            for (int u = 0; u < 8 && col + u < N; ++u) dst[u] = v[u];
+            for (int u = 0; u < 8 && col + u < N; ++u) dst[u] = epi_apply1<EPI>(v[u], row, col + u, ea);
         }
     }
 }
@@ -858,12 +911,13 @@ __device__ __forceinline__ void lora_mfma_addend_lds(f32x4 (&acc)[8][4], int lan
     }
 }
 
-template <int R, bool MF>
+template <int R, bool MF, int EPI = EPI_NONE>
 __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
     const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
     const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
     int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int M, int N, int64_t K, int tiles_n,
-    unsigned short* __restrict__ Y, int64_t ldy) {
+    unsigned short* __restrict__ Y, int64_t ldy, EpiArgs ea = EpiArgs{}) {
+    static_assert(EPI == EPI_NONE || MF, "epilogue ops ride the MFMA-addend path");
     __shared__ __attribute__((aligned(16))) char smem[p8::LDS + (MF ? epi::BYTES : 0)];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
@@ -952,7 +1006,7 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
         lora_mfma_addend_lds<(MF ? R : 0)>(acc, lane, m0, wm * 128, wn * 64, smem + p8::LDS, bias != nullptr, scale,
                                            rows_per_member, M);
         EGG_STAMP(4);
-        store_tile_t(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, M, N, Y, ldy);
+        store_tile_t<EPI>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 64, M, N, Y, ldy, ea);
         EGG_STAMP_DRAIN();
         EGG_STAMP(5);
         EGG_STAMP_RT(7);
@@ -1288,6 +1342,35 @@ static int launch_gemm8(const void* X, int64_t ldx, const void* W, int64_t ldw, 
     }
 #undef EGG_GEMM8
     EGG_CHECK_LAUNCH("lora_gemm8");
+    return EGGROLL_OK;
+}
+
+// The MFMA-addend 8-phase kernel with an epilogue op (r <= 2; any grid size).
+static int launch_gemm8_epi(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                            const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                            int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, int32_t epi,
+                            const EpiArgs& ea, hipStream_t st) {
+    const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_gemm: grid too large");
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+#define EGG_GEMM8E(RV, EV)                                                                                         \
+    hipLaunchKernelGGL((k_lora_gemm8<RV, true, EV>), grid, dim3(512), 0, st, (const unsigned short*)X, ldx,         \
+                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T, theta_pop, ld_theta, offB,  \
+                       scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy, ea)
+#define EGG_GEMM8E_R(EV)                       \
+    switch (r) {                               \
+        case 0: EGG_GEMM8E(0, EV); break;      \
+        case 1: EGG_GEMM8E(1, EV); break;      \
+        default: EGG_GEMM8E(2, EV); break;     \
+    }
+    switch (epi) {
+        case EPI_SILU: EGG_GEMM8E_R(EPI_SILU); break;
+        case EPI_RES: EGG_GEMM8E_R(EPI_RES); break;
+        default: EGG_GEMM8E_R(EPI_GATED); break;
+    }
+#undef EGG_GEMM8E_R
+#undef EGG_GEMM8E
+    EGG_CHECK_LAUNCH("lora_gemm8_epi");
     return EGGROLL_OK;
 }
 
@@ -2048,6 +2131,35 @@ int eggroll_lora_linear_pop_sel(const void* X, int64_t ldx, const void* W, int64
     }
     return lora_gemm_impl(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
                           ldy, kernel == 12 ? 8 : kernel, stream);
+}
+
+int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                                const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                                float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                                int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr, const void* gate,
+                                int64_t gstride, int64_t rows_per_group, void* stream) {
+    if (epi == EPI_NONE)
+        return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
+                                           rows_per_member, M, N, K, Y, ldy, T_ws, 0, stream);
+    EGG_CHECK_ARG(epi == EPI_SILU || epi == EPI_RES || epi == EPI_GATED, "lora_linear_pop_epi: epi=%d unknown", epi);
+    EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
+    EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
+    EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "lora_linear_pop_epi: need K %% 64 == 0");
+    EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop_epi: bad strides");
+    EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_linear_pop_epi: M/N too large");
+    EGG_CHECK_ARG(epi == EPI_SILU || (res && ldr >= N), "lora_linear_pop_epi: res NULL or ldr < N");
+    EGG_CHECK_ARG(epi != EPI_GATED || (gate && gstride >= N && rows_per_group > 0), "lora_linear_pop_epi: bad gate");
+    if (M == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(X && W && Y, "lora_linear_pop_epi: NULL pointer");
+    EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_linear_pop_epi: operand > 2 GiB");
+    if (r > 0) {
+        EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop_epi: theta_pop / T_ws NULL with r > 0");
+        int rc = eggroll_lora_project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T_ws, stream);
+        if (rc) return rc;
+    }
+    const EpiArgs ea{(const unsigned short*)res, ldr, (const unsigned short*)gate, gstride, rows_per_group};
+    return launch_gemm8_epi(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale,
+                            r ? rows_per_member : (M > 0 ? M : 1), M, N, K, Y, ldy, epi, ea, as_stream(stream));
 }
 
 int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,

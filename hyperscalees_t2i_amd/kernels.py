@@ -301,6 +301,41 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
     return out
 
 
+EPI = {None: 0, "silu": 1, "res": 2, "gated": 3}
+
+
+def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], theta_pop: Optional[torch.Tensor],
+                        offA: int, offB: int, r: int, scale: float, rows_per_member: int, epi: str,
+                        res: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
+                        rows_per_group: int = 1, out: Optional[torch.Tensor] = None,
+                        T_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """lora_linear_pop with an epilogue op on the bf16 output y (eggroll_lora_linear_pop_epi):
+    "silu": silu(y); "res": res + y; "gated": res + gate[row // rows_per_group] * y.  With res given and
+    out None the result is written into res (in place, as the residual adds it replaces)."""
+    _dev(x, "lora_linear_pop_epi(x)", torch.bfloat16)
+    _dev(W, "lora_linear_pop_epi(W)", torch.bfloat16)
+    M, Kd = x.shape
+    N = W.shape[0]
+    code = EPI[epi]
+    if res is not None:
+        _dev(res, "lora_linear_pop_epi(res)", torch.bfloat16)
+        if res.shape[-1] != N or res.numel() != M * N:
+            raise ValueError(f"res {tuple(res.shape)} does not match [{M}, {N}]")
+    if out is None:
+        out = res if res is not None and code in (2, 3) else torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    pg, gst = _row_ptr(gate, "lora_linear_pop_epi(gate)", N) if gate is not None else (None, 0)
+    if r > 0:
+        _dev(theta_pop, "lora_linear_pop_epi(theta_pop)", torch.float32)
+        need = lora_workspace_numel(M, Kd, r, rows_per_member)
+        if T_ws is None or T_ws.numel() < need:
+            T_ws = torch.empty(need, dtype=torch.float32, device=x.device)
+    _lib.call("eggroll_lora_linear_pop_epi", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
+              _p(theta_pop) if r > 0 else None, theta_pop.stride(0) if r > 0 else 0, offA, offB, r, float(scale),
+              rows_per_member, M, N, Kd, out.data_ptr(), N, _p(T_ws) if r > 0 else None, code,
+              _p(res), N if res is not None else 0, pg, gst or N, int(rows_per_group), _stream(x.device))
+    return out
+
+
 def lora_workspace_numel(M: int, K: int, r: int, rows_per_member: int) -> int:
     """fp32 elements of the eggroll_lora_linear_pop workspace (T, or the fused path's A_k images)."""
     nbytes = int(_lib.load().eggroll_lora_workspace_bytes(M, K, r, rows_per_member))

@@ -28,6 +28,13 @@ from torch import nn
 from . import kernels as K
 
 
+# Elementwise ops fused into GEMM epilogues (residual adds, gated residuals, the GLUMBConv SiLU).
+# The fused and unfused forms run the same kernels and are bit-identical
+# (tests/test_gpu_engine.py::test_fused_epilogues_bit_identical); False keeps every GEMM output
+# materialised (per-linear captures in the fp32 drift test).
+FUSE_EPILOGUES = True
+
+
 @dataclass
 class PopulationContext:
     theta_pop: Optional[torch.Tensor] = None  # [n_members, ld] fp32 (perturbed theta per member)
@@ -123,7 +130,11 @@ class LoRALinear(nn.Module):
             else:
                 self.lora_B.weight.zero_()
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, epi: Optional[str] = None, res: Optional[torch.Tensor] = None,
+                gate: Optional[torch.Tensor] = None, rows_per_group: int = 1) -> torch.Tensor:
+        """epi (optional): an elementwise op on the output, fused into the GEMM epilogue on the
+        population path (kernels.lora_linear_pop_epi): "res" -> res + y, "gated" -> res + gate[g] * y,
+        both written into `res` in place and returned."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if x2.dtype != torch.bfloat16:
@@ -131,6 +142,25 @@ class LoRALinear(nn.Module):
         x2 = x2.contiguous()
         M = x2.shape[0]
         ctx = self.ctx
+        if epi is not None:
+            res2 = res.view(M, self.out_features)
+            if (FUSE_EPILOGUES and self.r and ctx is not None and ctx.theta_pop is not None and self.r <= 2
+                    and not GemmTimer.active
+                    and M % ctx.n_members == 0 and M // ctx.n_members >= 256 and self.in_features % 64 == 0):
+                rpm = M // ctx.n_members
+                ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device)
+                K.lora_linear_pop_epi(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
+                                      self.r, self.scale, rpm, epi, res=res2, gate=gate, rows_per_group=rows_per_group,
+                                      T_ws=ws)
+                return res
+            y = self.forward(x).view(M, self.out_features)   # the same ops, unfused
+            if epi == "res":
+                res2.add_(y)
+            elif epi == "gated":
+                K.gated_residual_(res2, y, gate, rows_per_group=rows_per_group)
+            else:
+                raise ValueError(f"LoRALinear: epi {epi!r} unsupported")
+            return res
         if self.r and ctx is not None and ctx.theta_pop is not None:
             if M % ctx.n_members:
                 raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")

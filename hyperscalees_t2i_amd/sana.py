@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import kernels as K
+from . import lora
 from .lora import LoRALinear, bind_theta_layout
 
 
@@ -125,12 +126,16 @@ class LinearSelfAttention(nn.Module):
         self.to_v = LoRALinear(dim, inner, bias=False, lora=False)
         self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
 
-    def forward(self, x):  # x [B, N, D]
+    def forward(self, x, res=None, gate=None):  # x [B, N, D]
+        """With res / gate: returns res += gate[image] * attn1(x), the gated residual fused into
+        to_out's GEMM epilogue (the block's `x + gate_msa * attn_output`)."""
         B, N, D = x.shape
         q = self.norm_q(self.to_q(x), act="relu").view(B * N, -1)   # RMS norm + ReLU fused
         k = self.norm_k(self.to_k(x), act="relu").view(B * N, -1)
         v = self.to_v(x).view(B * N, -1)
         o = K.linear_attention(q, k, v, B, N, self.heads, self.head_dim, relu_qk=False)
+        if res is not None:
+            return self.to_out[0](o.view(B, N, -1), epi="gated", res=res, gate=gate, rows_per_group=N)
         return self.to_out[0](o.view(B, N, -1))
 
 
@@ -149,7 +154,7 @@ class CrossAttention(nn.Module):
         self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
         self.pad_head_dim = True   # pad the SDPA head dim to a multiple of 64 (exact, see forward)
 
-    def forward(self, x, enc, mask_bias, enc_index=None):
+    def forward(self, x, enc, mask_bias, enc_index=None, res=None):
         """x [B,N,D]; enc [U,L,D] caption rows; mask_bias [B,1,1,L]; enc_index [B] (image -> caption
         row, None: U == B).  Images that share a caption share its k / v rows, so to_k / to_v (and the
         caption projection before them) run once per distinct caption and the rows are gathered."""
@@ -171,7 +176,10 @@ class CrossAttention(nn.Module):
                                            attn_mask=mask_bias, scale=hd ** -0.5)
         if pad:
             o = o[..., :hd]
-        return self.to_out[0](o.transpose(1, 2).reshape(B, N, -1))
+        o = o.transpose(1, 2).reshape(B, N, -1)
+        if res is not None:   # res += to_out(o): the block's residual add fused into the GEMM epilogue
+            return self.to_out[0](o, epi="res", res=res)
+        return self.to_out[0](o)
 
 
 class GLUMBConv(nn.Module):
@@ -187,9 +195,15 @@ class GLUMBConv(nn.Module):
         self.w_point = nn.Parameter(torch.empty(dim, hidden, dtype=torch.bfloat16), requires_grad=False)
 
     def forward(self, x, H: int, W: int):  # x [B, N, D]
-        B, N, _ = x.shape
-        h = F.linear(x, self.w_inv, self.b_inv).view(B, H, W, -1)           # pre-activation [B,H,W,2h]
-        g = K.dwconv_nhwc(h, self.w_dw, self.b_dw, 3, pre_silu=True, glu=True)  # silu->dw3x3->GLU fused
+        B, N, D = x.shape
+        # 1x1 conv + SiLU on the 8-phase GEMM (SiLU of the bf16-rounded output in its epilogue), then
+        # dw3x3 -> GLU fused; the same values as F.linear -> dwconv(pre_silu=True)
+        if lora.FUSE_EPILOGUES:
+            h = K.lora_linear_pop_epi(x.reshape(B * N, D), self.w_inv, self.b_inv, None, 0, 0, 0, 0.0, B * N, "silu")
+            g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=False, glu=True)
+        else:
+            h = K.lora_linear_pop(x.reshape(B * N, D), self.w_inv, self.b_inv, None, 0, 0, 0, 0.0, B * N)
+            g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=True, glu=True)
         return F.linear(g.view(B, N, -1), self.w_point)
 
 
@@ -208,8 +222,12 @@ class SanaBlock(nn.Module):
         # [B, 6, D]: shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
         mods = (self.scale_shift_table[None] + timestep.view(B, 6, -1)).contiguous()
         n = K.rownorm(x, self.eps, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=N)
-        K.gated_residual_(x, self.attn1(n), mods[:, 2], rows_per_group=N)
-        x = x + self.attn2(x, enc, mask_bias, enc_index)
+        if lora.FUSE_EPILOGUES:
+            self.attn1(n, res=x, gate=mods[:, 2])             # x += gate_msa * attn1(n), in to_out's epilogue
+            self.attn2(x, enc, mask_bias, enc_index, res=x)   # x = x + attn2(x): in to_out's epilogue
+        else:                                                 # the same ops unfused (bit-identical)
+            K.gated_residual_(x, self.attn1(n), mods[:, 2], rows_per_group=N)
+            x = x + self.attn2(x, enc, mask_bias, enc_index)
         n = K.rownorm(x, self.eps, layer=True, mscale=mods[:, 4], mshift=mods[:, 3], rows_per_group=N)
         K.gated_residual_(x, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
         return x

@@ -136,6 +136,19 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
                    int64_t D, int32_t rank, float lr, float max_step_norm, float theta_max_norm,
                    void* workspace, float* theta_out, void* stream);
 
+
+/* eggroll_lora_linear_pop with one elementwise op fused into the GEMM epilogue, applied to the
+ * bf16-rounded output y exactly as the separate torch / libeggroll op it replaces would:
+ *   epi 1: Y = bf16(silu(y))                       GLUMBConv 1x1 conv -> SiLU (sana.py, dcae.py)
+ *   epi 2: Y = bf16(res + y)                       x = x + attn2(...) (Sana block)
+ *   epi 3: Y = bf16(res + gate[row/rpg, :] * y)    x += gate_msa * attn1(...) (eggroll_gated_residual)
+ * res [M, ldr] bf16 may alias Y; gate rows gstride apart.  Requires r <= 2 (and rows_per_member >=
+ * 256 when r > 0) and K % 64 == 0: always the MFMA-addend 8-phase kernel.  epi 0 = linear_pop.    */
+int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                                const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                                float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                                int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr, const void* gate,
+                                int64_t gstride, int64_t rows_per_group, void* stream);
 /* (2) Population-batched perturbed LoRA linear — replaces per-member
  * `unflatten_to_params` + PEFT lora.Linear.forward (peft: y = base(x) + B(A x) * alpha/r),
  * members evaluated sequentially in the reference (unifed_es.py:159-163).

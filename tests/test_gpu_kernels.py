@@ -704,3 +704,42 @@ def test_full_size_sana_layout_properties(dev, pop):
     ref, _ = O.ref_es_tail(S.cpu().numpy(), eps.cpu().numpy(), theta.cpu().numpy(), promptnorm=True, lr_scale=0.1,
                            sigma=0.01, max_step_norm=0.0, theta_max_norm=40.0)
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("epi,r,M,N,Kd,rpm", [("silu", 0, 16384, 2304, 512, 16384), ("res", 2, 4 * 4096, 2240, 2240, 4096),
+                                             ("gated", 2, 4 * 4096, 2240, 2240, 4096), ("gated", 1, 3 * 1000 + 200, 384, 256, 1000),
+                                             ("res", 0, 777, 200, 128, 777)])
+def test_lora_linear_pop_epilogue_bitexact(dev, epi, r, M, N, Kd, rpm):
+    """eggroll_lora_linear_pop_epi == the same 8-phase GEMM (kernel 8) followed by the separate op it
+    fuses (SiLU of the bf16 output / residual add / eggroll_gated_residual), bit for bit; ragged M, N."""
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    x = torch.randn((M, Kd), generator=g, device=dev).to(torch.bfloat16)
+    W = (torch.randn((N, Kd), generator=g, device=dev) / Kd ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=dev).to(torch.bfloat16)
+    nm = -(-M // rpm)
+    tp = torch.randn((nm, Kd * r + N * r + 8), generator=g, device=dev) * 0.05 if r else None
+    offA, offB = 0, Kd * r
+    y = K.lora_gemm(x, W, bias, K.lora_project(x, tp, offA, r, rpm) if r else None, tp, offB, r, 2.0, rpm, kernel=8) \
+        if r else K.lora_linear_pop(x, W, bias, None, 0, 0, 0, 0.0, M, kernel=8)
+    res = torch.randn((M, N), generator=g, device=dev).to(torch.bfloat16)
+    rpg = 512
+    gate = torch.randn((-(-M // rpg), 3 * N), generator=g, device=dev).to(torch.bfloat16)[:, N:2 * N]
+    if epi == "silu":
+        ref = (y.float() * torch.reciprocal(1.0 + torch.exp(-y.float()))).to(torch.bfloat16)
+        out = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, "silu")
+        # the device SiLU uses the hardware reciprocal / exp (as the dwconv's): within 1 bf16 ulp of torch,
+        # and bitwise equal to the dwconv's own pre-SiLU of the same values
+        assert float((out.float() - ref.float()).abs().max()) <= float(ref.float().abs().max()) * 2 ** -7
+        w_id = torch.zeros((9, N), device=dev, dtype=torch.bfloat16)
+        w_id[4] = 1.0
+        pre = K.dwconv_nhwc(y.view(1, 1, M, N), w_id, None, 3, pre_silu=True, glu=False).view(M, N)
+        assert torch.equal(out, pre)
+        return
+    if epi == "res":
+        ref = (res.float() + y.float()).to(torch.bfloat16)
+        out = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, "res", res=res.clone())
+    else:
+        ref = K.gated_residual_(res.clone(), y, gate, rows_per_group=rpg)
+        out = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, "gated", res=res.clone(), gate=gate,
+                                    rows_per_group=rpg)
+    assert torch.equal(out, ref)

@@ -1,0 +1,48 @@
+"""Same-process interleaved A/B of the GEMM-epilogue fusions on the bench epoch (N=1, pop 8).
+
+    python tools/fuse_ab.py [--rounds 4]
+Alternates lora.FUSE_EPILOGUES True / False, 2 timed epochs per arm per round (box-to-box spread is
++-3 %, so only same-process interleaved arms are compared)."""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=4)
+    a = ap.parse_args()
+    import bench
+    from hyperscalees_t2i_amd import lora
+    args = argparse.Namespace(latent=32, small=False, pop_per_gpu=8, workload="sana")
+    backend, engine, noiser, theta, pop = bench.build(args, 1, 0, torch.device("cuda:0"))
+    g = backend.cfg.guidance_scale
+    for w in range(2):
+        theta, _ = engine.step(theta, seed=w, guidance_scale=g)
+    res = {"fused": [], "unfused": []}
+    seed = 10
+    for r in range(a.rounds):
+        for arm in ("fused", "unfused"):
+            lora.FUSE_EPILOGUES = arm == "fused"
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(2):
+                theta, _ = engine.step(theta, seed=seed, guidance_scale=g)
+                seed += 1
+            torch.cuda.synchronize()
+            res[arm].append(1e3 * (time.perf_counter() - t0) / 2)
+            print(arm, round(res[arm][-1], 1), flush=True)
+    lora.FUSE_EPILOGUES = True
+    out = {k: sorted(v) for k, v in res.items()}
+    out["median_ms"] = {k: v[len(v) // 2] for k, v in out.items()}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
