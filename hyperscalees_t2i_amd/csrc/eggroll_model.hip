@@ -56,7 +56,13 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
     constexpr int HALO = KS / 2;
     constexpr int TR = DW_TH + KS - 1, TC = DW_TW + KS - 1;
     constexpr int PIXB = DW_CS * 2;  // bytes per staged pixel per plane
-    __shared__ __attribute__((aligned(16))) char lds[PLANES * TR * TC * PIXB];
+    constexpr int IN_BYTES = PLANES * TR * TC * PIXB;
+    // PW: the conv tile [256 px][32 ch] bf16 gets its own region, written row by row as the band is
+    // computed (no 8 x 4 result registers held to the end: 284 -> ~170 VGPRs, 1 -> 3 waves per SIMD)
+    constexpr int PW_BYTES = PW ? DW_TH * DW_TW * 64 : 0;
+    __shared__ __attribute__((aligned(16))) char lds[IN_BYTES + PW_BYTES];
+    char* const pwt = lds + IN_BYTES;
+    auto swz = [](uint32_t L) { return L ^ ((L >> 3) & 32u); };
     const int Cout = GLU ? Cin / 2 : Cin;
     const int tid = threadIdx.x;
     int bid = xcd_remap(blockIdx.x, gridDim.x);  // adjacent channel slices share 128-B lines: same L2
@@ -125,7 +131,10 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 #pragma unroll
                 for (int dx = 0; dx < 3; ++dx) rd(pl, r, xs + dx, win[r][dx]);
         }
-#pragma unroll
+        // KS = 5: one output row per iteration (not unrolled): the 25 taps' LDS reads of eight rows are not
+        // all hoisted into registers, which keeps the kernel at 3 waves per SIMD
+        constexpr int ROW_UNROLL = KS == 3 ? DW_TH : 1;
+#pragma unroll ROW_UNROLL
         for (int oy = 0; oy < DW_TH; ++oy) {
             if constexpr (KS == 3) {
 #pragma unroll
@@ -157,7 +166,14 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
                         win[1][dx][i] = win[2][dx][i];
                     }
             }
-            if ((pl == 0 && GLU) || PW) {
+            if constexpr (PW) {
+                // conv tile -> LDS [pixel oy*32+x][32 ch], 64-B rows with slot ^= 2*((pixel >> 2) & 1): the
+                // 16x16x32 fragment reads (16 consecutive pixels, 4 chunks) are then bank-conflict-free
+                u16x4m o;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[i] = f2b(acc[i]);
+                *reinterpret_cast<u16x4m*>(pwt + swz((uint32_t)((oy * DW_TW + xs) * 64 + q * 8))) = o;
+            } else if (pl == 0 && GLU) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) res[oy][i] = acc[i];
             } else {
@@ -172,18 +188,7 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
         }
     }
     if constexpr (PW) {
-        // conv tile -> LDS [pixel oy*32+x][32 ch], 64-B rows with slot ^= 2*((pixel >> 2) & 1): the
-        // 16x16x32 fragment reads (16 consecutive pixels, 4 chunks) are then bank-conflict-free
-        auto swz = [](uint32_t L) { return L ^ ((L >> 3) & 32u); };
-        __syncthreads();  // every thread is done with the staged input
-#pragma unroll
-        for (int oy = 0; oy < DW_TH; ++oy) {
-            u16x4m o;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[i] = f2b(res[oy][i]);
-            *reinterpret_cast<u16x4m*>(lds + swz((uint32_t)((oy * DW_TW + xs) * 64 + q * 8))) = o;
-        }
-        __syncthreads();
+        __syncthreads();  // the whole conv tile is in pwt
         const int lane = tid & 63, wv = tid >> 6, r16 = lane & 15, g4 = lane >> 4;
         const unsigned short* pg = pw + (int64_t)cs * (DW_CS * DW_CS);  // [o][c] of this channel group
         la_bf16x8 bo[2];
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
             const int p = wv * 64 + 16 * f + r16;  // tile pixel of this lane's fragment row
-            const la_bf16x8 a = *reinterpret_cast<const la_bf16x8*>(lds + swz((uint32_t)(p * 64 + g4 * 16)));
+            const la_bf16x8 a = *reinterpret_cast<const la_bf16x8*>(pwt + swz((uint32_t)(p * 64 + g4 * 16)));
             const int y = y0 + (p >> 5), xx = x0 + (p & 31);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
