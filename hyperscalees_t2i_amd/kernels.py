@@ -741,3 +741,29 @@ def bias_act_(y: torch.Tensor, bias: torch.Tensor, act: Optional[str]) -> torch.
     _lib.call("eggroll_bias_act", y.data_ptr(), bias.data_ptr(), y.numel() // C, C, ACT[act], _stream(y.device))
     OpTimer.end(e0, "bias_act", 4.0 * y.numel(), f"{tuple(y.shape)}")
     return y
+
+
+def cross_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, N: int, heads: int, head_dim: int,
+                    L: int, scale: float, bias: Optional[torch.Tensor] = None, enc_index: Optional[torch.Tensor] = None,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sana attn2 softmax cross-attention on MFMA (eggroll_cross_attention).  q: [B*N, >= heads*hd] bf16
+    rows; k, v: [U*L, >= heads*hd] bf16 caption rows; bias [U, L] bf16 (additive mask) or None;
+    enc_index [B] int (image -> caption row) or None.  Returns [B*N, heads*hd] bf16."""
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        if t.device.type != "cuda" or t.dtype != torch.bfloat16 or t.stride(-1) != 1:
+            raise _lib.EggrollError(f"cross_attention({nm}): expected a bf16 device view with unit inner stride")
+    if k.stride(0) != v.stride(0):
+        raise ValueError("cross_attention: k / v must share a row stride")
+    if out is None:
+        out = torch.empty((B * N, heads * head_dim), dtype=torch.bfloat16, device=q.device)
+    if bias is not None:
+        _dev(bias, "cross_attention(bias)", torch.bfloat16)
+    ei = None
+    if enc_index is not None:
+        ei = enc_index.to(device=q.device, dtype=torch.int32).contiguous()
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_cross_attention", q.data_ptr(), q.stride(0), k.data_ptr(), v.data_ptr(), k.stride(0), _p(bias),
+              _p(ei), B, N, heads, head_dim, L, float(scale), out.data_ptr(), out.stride(0), _stream(q.device))
+    OpTimer.end(e0, "cross_attention", 2.0 * (2 * B * N * heads * head_dim + 2 * k.shape[0] * heads * head_dim),
+                f"B{B} N{N} L{L}")
+    return out

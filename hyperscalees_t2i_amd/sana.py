@@ -153,17 +153,30 @@ class CrossAttention(nn.Module):
         self.to_v = LoRALinear(dim, inner, bias=True, lora=False)
         self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
         self.pad_head_dim = True   # pad the SDPA head dim to a multiple of 64 (exact, see forward)
+        self.use_kernel = True     # eggroll_cross_attention where it applies (head dim 112, L <= 320)
 
     def forward(self, x, enc, mask_bias, enc_index=None, res=None):
-        """x [B,N,D]; enc [U,L,D] caption rows; mask_bias [B,1,1,L]; enc_index [B] (image -> caption
-        row, None: U == B).  Images that share a caption share its k / v rows, so to_k / to_v (and the
-        caption projection before them) run once per distinct caption and the rows are gathered."""
+        """x [B,N,D]; enc [U,L,D] caption rows; mask_bias [U, L] additive caption mask per caption row;
+        enc_index [B] (image -> caption row, None: U == B).  Images that share a caption share its k / v
+        rows, so to_k / to_v (and the caption projection before them) run once per distinct caption.
+        Head dim 112 with L <= 320 runs libeggroll's MFMA cross-attention (k / v read through
+        enc_index, q / o in the projection layout); otherwise SDPA on gathered k / v."""
         B, N, _ = x.shape
         U, L = enc.shape[0], enc.shape[1]
         hd = self.head_dim
+        if self.use_kernel and hd == 112 and L <= 320:
+            q = self.norm_q(self.to_q(x)).view(B * N, -1)
+            k = self.norm_k(self.to_k(enc)).view(U * L, -1)
+            v = self.to_v(enc).view(U * L, -1)
+            o = K.cross_attention(q, k, v, B, N, self.heads, hd, L, hd ** -0.5, bias=mask_bias.contiguous(),
+                                  enc_index=enc_index).view(B, N, -1)
+            if res is not None:   # res += to_out(o): the block's residual add fused into the GEMM epilogue
+                return self.to_out[0](o, epi="res", res=res)
+            return self.to_out[0](o)
         q = self.norm_q(self.to_q(x)).view(B, N, self.heads, hd)
         k = self.norm_k(self.to_k(enc)).view(U, L, self.heads, hd)
         v = self.to_v(enc).view(U, L, self.heads, hd)
+        mask_bias = (mask_bias if enc_index is None else mask_bias.index_select(0, enc_index)).view(B, 1, 1, L)
         pad = (-hd) % 64 if self.pad_head_dim else 0
         if pad:
             # SDPA at head dim 112 runs ~2.7x slower than at 128 on gfx950; zero-padded dims add exact
@@ -297,10 +310,7 @@ class SanaTransformer2DModel(nn.Module):
                 encoder_attention_mask = encoder_attention_mask[:, :L_eff]
         enc = self.caption_projection(encoder_hidden_states.to(torch.bfloat16))
         enc = self.caption_norm(enc)
-        mask_bias = (1.0 - encoder_attention_mask.to(torch.bfloat16)) * -10000.0
-        if enc_index is not None:
-            mask_bias = mask_bias.index_select(0, enc_index)
-        mask_bias = mask_bias.view(B, 1, 1, -1)
+        mask_bias = (1.0 - encoder_attention_mask.to(torch.bfloat16)) * -10000.0   # [U, L], per caption row
         for blk in self.transformer_blocks:
             x = blk(x, enc, mask_bias, timestep6, H, W, enc_index)
         mods = (self.scale_shift_table[None] + emb_t[:, None]).contiguous()     # [B, 2, D]: shift, scale

@@ -309,6 +309,15 @@ int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, int64_t W, in
                             int32_t kth, int64_t RW, int64_t RH, int64_t out_size, const float* mean,
                             const float* stdv, void* tmp, void* out, void* stream);
 
+/* Softmax cross-attention over a short key sequence (Sana attn2: diffusers SanaAttnProcessor2_0,
+ * F.scaled_dot_product_attention with the caption mask as an additive bias):
+ *   o[b,n,h,:] = softmax_j(scale * q[b,n,h,:] . k[u,j,h,:] + bias[u,j]) @ v[u,:,h,:],  u = enc_index[b]
+ * q / o bf16 rows b*N + n (head h at columns h*head_dim), k / v bf16 rows u*L + j; bias bf16 [U][L]
+ * or NULL; enc_index int32 [B] or NULL (u = b).  head_dim 112, L <= 320; MFMA, fp32 softmax.        */
+int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, const void* bias,
+                            const int32_t* enc_index, int64_t B, int64_t N, int64_t heads, int64_t head_dim,
+                            int64_t L, float scale, void* o, int64_t ldo, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

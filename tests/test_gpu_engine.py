@@ -235,3 +235,29 @@ def test_fused_epilogues_population_forward(dev):
     finally:
         lora.FUSE_EPILOGUES = True
     assert float((fused - plain).norm() / plain.norm()) < 3e-2   # measured 1.1 % (bf16 through 2 blocks + DC-AE)
+
+
+def test_cross_attention_kernel_in_population_forward(dev):
+    """Sana attn2 on eggroll_cross_attention (head dim 112, caption rows through enc_index, mask as
+    an additive bias) vs the SDPA path on gathered k / v, inside the population forward."""
+    arch = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=4,
+                    cross_attention_head_dim=112, caption_channels=2304)   # inner 448 = 7 x 64 (GEMM K)
+    cfg = SanaConfig(width_latent=4, height_latent=4, batches_per_gen=2, arch=arch,
+                     vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
+    be = SanaBackend(str(dev), cfg)
+    be.init_and_attach_lora()
+    params, shapes = be.collect_lora_params()
+    theta0 = flatten_params(params).to(dev)
+    noiser = EggRollNoiser(shapes, sigma=0.05, lr_scale=0.1, rank=1, use_antithetic=True)
+    tp = noiser.perturb(theta0, noiser.sample_factors(3, dev, seed=4), 3, 0, 3)
+    flat = be.step_sampling_info(2)["flat_ids"]
+    blocks = be.es_model.transformer.transformer_blocks
+    outs = []
+    for use in (True, False):
+        for blk in blocks:
+            blk.attn2.use_kernel = use
+        outs.append(be.generate_population(flat, 2, 4.5, tp).float())
+    for blk in blocks:
+        blk.attn2.use_kernel = True
+    rel = float((outs[0] - outs[1]).norm() / outs[1].norm())
+    assert rel < 2e-2, rel

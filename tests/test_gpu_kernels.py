@@ -743,3 +743,29 @@ def test_lora_linear_pop_epilogue_bitexact(dev, epi, r, M, N, Kd, rpm):
         out = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, "gated", res=res.clone(), gate=gate,
                                     rows_per_group=rpg)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("B,N,H,L,U", [(4, 64, 2, 37, 2), (3, 100, 3, 300, 3), (6, 17, 1, 320, 2), (16, 1024, 20, 300, 4)])
+def test_cross_attention_vs_sdpa(dev, B, N, H, L, U):
+    """eggroll_cross_attention (MFMA, caption rows through enc_index, additive mask) vs fp32 SDPA on the
+    gathered k / v; ragged N, L not a multiple of 16/32, fully-valid and heavily-masked captions."""
+    import torch.nn.functional as F
+    hd = 112
+    g = torch.Generator(device=dev).manual_seed(B * 131 + L)
+    q = torch.randn((B * N, H * hd), generator=g, device=dev).to(torch.bfloat16)
+    k = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
+    v = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
+    lens = [L] + [int(x) for x in torch.randint(1, L + 1, (U - 1,), generator=g, device=dev).tolist()]
+    bias = torch.zeros((U, L), device=dev, dtype=torch.bfloat16)
+    for u, n_valid in enumerate(lens):
+        bias[u, n_valid:] = -10000.0
+    enc_index = torch.arange(B, device=dev) % U
+    ours = K.cross_attention(q, k, v, B, N, H, hd, L, hd ** -0.5, bias=bias, enc_index=enc_index).float()
+    qq = q.view(B, N, H, hd).transpose(1, 2).float()
+    kk = k.view(U, L, H, hd)[enc_index].transpose(1, 2).float()
+    vv = v.view(U, L, H, hd)[enc_index].transpose(1, 2).float()
+    ref = F.scaled_dot_product_attention(qq, kk, vv, attn_mask=bias[enc_index].view(B, 1, 1, L).float(),
+                                         scale=hd ** -0.5).transpose(1, 2).reshape(B * N, H * hd)
+    rel = float((ours - ref).norm() / ref.norm())
+    assert rel < 1e-2, rel     # bf16 P (probabilities rounded before the PV MFMA) + bf16 output
+    assert float((ours - ref).abs().max()) < 3e-2 * float(ref.abs().max())

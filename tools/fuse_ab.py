@@ -1,8 +1,9 @@
-"""Same-process interleaved A/B of the GEMM-epilogue fusions on the bench epoch (N=1, pop 8).
+"""Same-process interleaved A/B of one build knob on the bench epoch (N=1, pop 8).
 
-    python tools/fuse_ab.py [--rounds 4]
-Alternates lora.FUSE_EPILOGUES True / False, 2 timed epochs per arm per round (box-to-box spread is
-+-3 %, so only same-process interleaved arms are compared)."""
+    python tools/fuse_ab.py [--rounds 4] [--knob fuse|xattn]
+fuse: lora.FUSE_EPILOGUES (GEMM-epilogue fusions); xattn: Sana attn2 on eggroll_cross_attention vs
+SDPA.  2 timed epochs per arm per round (box-to-box spread is +-3 %, so only same-process interleaved
+arms are compared)."""
 import argparse
 import json
 import sys
@@ -17,6 +18,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--knob", choices=("fuse", "xattn"), default="fuse")
     a = ap.parse_args()
     import bench
     from hyperscalees_t2i_amd import lora
@@ -27,9 +29,18 @@ def main():
         theta, _ = engine.step(theta, seed=w, guidance_scale=g)
     res = {"fused": [], "unfused": []}
     seed = 10
+    blocks = backend.es_model.transformer.transformer_blocks
+
+    def set_arm(on):
+        if a.knob == "fuse":
+            lora.FUSE_EPILOGUES = on
+        else:
+            for blk in blocks:
+                blk.attn2.use_kernel = on
+
     for r in range(a.rounds):
         for arm in ("fused", "unfused"):
-            lora.FUSE_EPILOGUES = arm == "fused"
+            set_arm(arm == "fused")
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(2):
@@ -38,9 +49,10 @@ def main():
             torch.cuda.synchronize()
             res[arm].append(1e3 * (time.perf_counter() - t0) / 2)
             print(arm, round(res[arm][-1], 1), flush=True)
-    lora.FUSE_EPILOGUES = True
+    set_arm(True)
     out = {k: sorted(v) for k, v in res.items()}
-    out["median_ms"] = {k: v[len(v) // 2] for k, v in out.items()}
+    out["knob"] = a.knob
+    out["median_ms"] = {k: v[len(v) // 2] for k, v in out.items() if k != "knob"}
     print(json.dumps(out))
 
 
