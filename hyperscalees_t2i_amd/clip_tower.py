@@ -23,9 +23,10 @@ ACT = {"gelu": lambda x: F.gelu(x), "quick_gelu": lambda x: x * torch.sigmoid(1.
 
 
 class CLIPVisionTower:
-    def __init__(self, model, pad_head_dim: bool = False):
+    def __init__(self, model, pad_head_dim: bool = False, use_kernel: bool = True):
         vm = model.vision_model
         self.pad_head_dim = pad_head_dim
+        self.use_kernel = use_kernel   # libeggroll's MFMA attention (eggroll_cross_attention, k = v = own tokens)
         cfg = model.config.vision_config
         self.C, self.heads = cfg.hidden_size, cfg.num_attention_heads
         self.hd = self.C // self.heads
@@ -71,6 +72,20 @@ class CLIPVisionTower:
         last = len(self.layers) - 1
         for i, L in enumerate(self.layers):
             y = self._ln(L["ln1"], h)
+            if self.use_kernel and hd in (64, 80, 112) and T <= 320:
+                from . import kernels as K
+                qkv = F.linear(y, L["wqkv"], L["bqkv"]).view(n * T, 3 * C)
+                last_i = i == len(self.layers) - 1
+                # self-attention as the caption-attention kernel with the image's own tokens as keys; on the
+                # last layer only the [CLS] query rows (row stride T) are attended
+                qv = qkv[::T] if last_i else qkv
+                o = K.cross_attention(qv, qkv[:, C:], qkv[:, 2 * C:], n, 1 if last_i else T, H, hd, T, L["scale"])
+                if last_i:
+                    h = h[:, :1]
+                h = h + F.linear(o.view(n, -1, C), L["wo"], L["bo"])
+                y = self._ln(L["ln2"], h)
+                h = h + F.linear(self.act(F.linear(y, L["w1"], L["b1"])), L["w2"], L["b2"])
+                continue
             qkv = F.linear(y, L["wqkv"], L["bqkv"]).view(n, T, 3, H, hd)
             k, v = qkv[:, :, 1].transpose(1, 2), qkv[:, :, 2].transpose(1, 2)
             if i == last:           # only the [CLS] row is read by get_image_features

@@ -906,21 +906,22 @@ __global__ __launch_bounds__(256) void k_clip_resize_v(const unsigned char* __re
 //   o = O / rowsum, written as 4 consecutive dims of one query per lane (8-B stores) in the q layout.
 // Keys past L are excluded (-inf); the additive bias is the reference's attention mask.
 // ------------------------------------------------------------------------------------
-constexpr int XA_D = 112, XA_LMAX = 320, XA_RS = XA_D + 8;  // LDS row stride 240 B (8-B aligned rows)
-constexpr int XA_KF = XA_LMAX / 16;                         // key fragments
+constexpr int XA_LMAX = 320;          // keys per (caption, head) staged in LDS
+constexpr int XA_KF = XA_LMAX / 16;   // key fragments
 
+template <int RS>
 __device__ __forceinline__ la_bf16x8 xa_tr8_perm(const unsigned short* base, int lane) {
     // rows base + 4g + {0..3} and base + 16 + 4g + {0..3} of the 16-lane group g (lane 4q+p: row q, columns 4p..)
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const unsigned short* r0 = base + (4 * g + q) * XA_RS + 4 * p;
+    const unsigned short* r0 = base + (4 * g + q) * RS + 4 * p;
     const la_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((la_lds_s4*)(r0));
-    const la_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((la_lds_s4*)(r0 + 16 * XA_RS));
+    const la_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((la_lds_s4*)(r0 + 16 * RS));
     typedef __attribute__((ext_vector_type(8))) short s8;
     const s8 f = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(la_bf16x8, f);
 }
 
-template <int NWAVE, int QF>
+template <int HD, int NWAVE, int QF>
 __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short* __restrict__ q, int64_t ldq,
                                                     const unsigned short* __restrict__ k,
                                                     const unsigned short* __restrict__ v, int64_t ldkv,
@@ -929,8 +930,10 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
                                                     float scale, unsigned short* __restrict__ o, int64_t ldo) {
     // NWAVE waves sweep the image's queries in blocks of 16 * QF (QF query fragments share every k / v
     // fragment read from LDS)
-    __shared__ __attribute__((aligned(16))) unsigned short sk[XA_LMAX * XA_RS];
-    __shared__ __attribute__((aligned(16))) unsigned short sv[XA_LMAX * XA_RS];
+    constexpr int RS = HD + 8, KSN = (HD + 31) / 32, DF = HD / 16;  // LDS row stride, Q.K k-steps, PV dim frags
+    static_assert(HD % 16 == 0 && HD <= 128, "head dim");
+    __shared__ __attribute__((aligned(16))) unsigned short sk[XA_LMAX * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short sv[XA_LMAX * RS];
     __shared__ float sb[XA_LMAX];
     constexpr int NT = 64 * NWAVE;
     const int bh = xcd_remap(blockIdx.x, gridDim.x);
@@ -938,17 +941,17 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     const int u = enc_index ? enc_index[b] : b;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
     // stage k / v rows of caption u, head h: 14 chunks of 16 B per row; rows >= L are zeros
-    constexpr int CH = XA_D / 8;
+    constexpr int CH = HD / 8;
     for (int c = tid; c < XA_LMAX * CH; c += NT) {
         const int r = c / CH, cc = c - r * CH;
         u16x8m kv = u16x8m{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
         if (r < L) {
-            const int64_t off = ((int64_t)u * L + r) * ldkv + (int64_t)h * XA_D + cc * 8;
+            const int64_t off = ((int64_t)u * L + r) * ldkv + (int64_t)h * HD + cc * 8;
             kv = *reinterpret_cast<const u16x8m*>(k + off);
             vv = *reinterpret_cast<const u16x8m*>(v + off);
         }
-        *reinterpret_cast<u16x8m*>(sk + r * XA_RS + cc * 8) = kv;
-        *reinterpret_cast<u16x8m*>(sv + r * XA_RS + cc * 8) = vv;
+        *reinterpret_cast<u16x8m*>(sk + r * RS + cc * 8) = kv;
+        *reinterpret_cast<u16x8m*>(sv + r * RS + cc * 8) = vv;
     }
     for (int r = tid; r < XA_LMAX; r += NT)
         sb[r] = r < L ? (bias ? b2f(bias[(int64_t)u * L + r]) : 0.0f) : -INFINITY;
@@ -957,16 +960,16 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     const int nqb = (N + 16 * QF - 1) / (16 * QF);
     for (int qb = w; qb < nqb; qb += NWAVE) {
         // B = Q^T fragments for the 4 k-steps (dims 32ks + 8g .. +7; dims >= 112 are zero)
-        la_bf16x8 bq[QF][4];
+        la_bf16x8 bq[QF][KSN];
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
             const int qrow = qb * 16 * QF + 16 * x + r16;
 #pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
+            for (int ks = 0; ks < KSN; ++ks) {
                 const int d0 = 32 * ks + 8 * g;
                 u16x8m t = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
-                if (d0 < XA_D && qrow < N)
-                    t = *reinterpret_cast<const u16x8m*>(q + ((int64_t)b * N + qrow) * ldq + (int64_t)h * XA_D + d0);
+                if (d0 < HD && qrow < N)
+                    t = *reinterpret_cast<const u16x8m*>(q + ((int64_t)b * N + qrow) * ldq + (int64_t)h * HD + d0);
                 bq[x][ks] = __builtin_bit_cast(la_bf16x8, t);
             }
         }
@@ -981,10 +984,10 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
             for (int x = 0; x < QF; ++x) sf[x][f] = la_f32x4{0.f, 0.f, 0.f, 0.f};
             if (f < nkf) {
 #pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
+                for (int ks = 0; ks < KSN; ++ks) {
                     const int d0 = 32 * ks + 8 * g;
                     la_bf16x8 a;
-                    if (d0 < XA_D) a = *reinterpret_cast<const la_bf16x8*>(sk + (16 * f + r16) * XA_RS + d0);
+                    if (d0 < HD) a = *reinterpret_cast<const la_bf16x8*>(sk + (16 * f + r16) * RS + d0);
                     else a = la_bf16x8{};
 #pragma unroll
                     for (int x = 0; x < QF; ++x) sf[x][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[x][ks], sf[x][f], 0, 0, 0);
@@ -1027,11 +1030,11 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
             sum[x] += __shfl_xor(sum[x], 32);
         }
         // O^T[dim][query] = sum_keys V^T[dim][key] P^T[key][query]
-        la_f32x4 oc[QF][7];
+        la_f32x4 oc[QF][DF];
 #pragma unroll
         for (int x = 0; x < QF; ++x)
 #pragma unroll
-            for (int d = 0; d < 7; ++d) oc[x][d] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int d = 0; d < DF; ++d) oc[x][d] = la_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < XA_KF / 2; ++j) {
             if (j < nkb) {
@@ -1044,8 +1047,8 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
                         bp[x][4 + e] = (__bf16)sf[x][2 * j + 1][e];
                     }
 #pragma unroll
-                for (int d = 0; d < 7; ++d) {
-                    const la_bf16x8 av = xa_tr8_perm(sv + (32 * j) * XA_RS + 16 * d, lane);
+                for (int d = 0; d < DF; ++d) {
+                    const la_bf16x8 av = xa_tr8_perm<RS>(sv + (32 * j) * RS + 16 * d, lane);
 #pragma unroll
                     for (int x = 0; x < QF; ++x) oc[x][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bp[x], oc[x][d], 0, 0, 0);
                 }
@@ -1056,9 +1059,9 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
             const int qrow = qb * 16 * QF + 16 * x + r16;
             if (qrow < N) {
                 const float inv = 1.0f / sum[x];
-                unsigned short* dst = o + ((int64_t)b * N + qrow) * ldo + (int64_t)h * XA_D + 4 * g;
+                unsigned short* dst = o + ((int64_t)b * N + qrow) * ldo + (int64_t)h * HD + 4 * g;
 #pragma unroll
-                for (int d = 0; d < 7; ++d) {
+                for (int d = 0; d < DF; ++d) {
                     u16x4m t;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) t[e] = f2b(oc[x][d][e] * inv);
@@ -1327,10 +1330,11 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
                                        const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
                                        int64_t heads, int64_t head_dim, int64_t L, float scale, void* o, int64_t ldo,
                                        void* stream) {
-    EGG_CHECK_ARG(head_dim == XA_D, "cross_attention: head_dim %lld unsupported (%d)", (long long)head_dim, XA_D);
+    EGG_CHECK_ARG(head_dim == 64 || head_dim == 80 || head_dim == 112, "cross_attention: head_dim %lld unsupported "
+                  "(64, 80, 112)", (long long)head_dim);
     EGG_CHECK_ARG(B >= 0 && N > 0 && heads > 0 && L > 0 && L <= XA_LMAX, "cross_attention: bad sizes (L <= %d)", XA_LMAX);
-    EGG_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldo % 4 == 0 && ldq >= heads * XA_D && ldkv >= heads * XA_D &&
-                  ldo >= heads * XA_D, "cross_attention: bad strides");
+    EGG_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldo % 4 == 0 && ldq >= heads * head_dim &&
+                  ldkv >= heads * head_dim && ldo >= heads * head_dim, "cross_attention: bad strides");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(q && k && v && o, "cross_attention: NULL pointer");
     EGG_CHECK_ARG(((uintptr_t)q & 15) == 0 && ((uintptr_t)k & 15) == 0 && ((uintptr_t)v & 15) == 0 && ((uintptr_t)o & 7) == 0,
@@ -1339,9 +1343,14 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
     // 8 waves x 16-query blocks (164 VGPRs, 2 waves per SIMD): measured 0.80 ms at the Sana attn2 shape
     // (B 128, N 1024, 20 heads, L 300) vs 0.94 for 4 waves x 32 queries and 1.27 for 4 x 16 (SDPA on
     // the gathered k / v with the mask: 1.53 ms)
-    hipLaunchKernelGGL((k_cross_attn<8, 1>), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream),
-                       (const unsigned short*)q, ldq, (const unsigned short*)k, (const unsigned short*)v, ldkv,
-                       (const unsigned short*)bias, enc_index, (int)heads, (int)N, (int)L, scale, (unsigned short*)o, ldo);
+#define EGG_XA(HD_)                                                                                              \
+    hipLaunchKernelGGL((k_cross_attn<HD_, 8, 1>), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream),  \
+                       (const unsigned short*)q, ldq, (const unsigned short*)k, (const unsigned short*)v, ldkv,    \
+                       (const unsigned short*)bias, enc_index, (int)heads, (int)N, (int)L, scale, (unsigned short*)o, ldo)
+    if (head_dim == 112) EGG_XA(112);
+    else if (head_dim == 80) EGG_XA(80);
+    else EGG_XA(64);
+#undef EGG_XA
     EGG_CHECK_LAUNCH("cross_attention");
     return EGGROLL_OK;
 }
