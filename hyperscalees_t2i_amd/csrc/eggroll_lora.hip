@@ -1599,9 +1599,14 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
         const int64_t row = row_of(rr);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const u16x4 r4 = *reinterpret_cast<const u16x4*>(res + row * BN + wn * 64 + 16 * j + 4 * cg);
+            if (res) {
+                const u16x4 r4 = *reinterpret_cast<const u16x4*>(res + row * BN + wn * 64 + 16 * j + 4 * cg);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][j][e] = acc[i][j][e] * rs * wv[j][e] + bv[j][e] + bf16_to_f32(r4[e]);
+                for (int e = 0; e < 4; ++e) acc[i][j][e] = acc[i][j][e] * rs * wv[j][e] + bv[j][e] + bf16_to_f32(r4[e]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i][j][e] = acc[i][j][e] * rs * wv[j][e] + bv[j][e];
+            }
         }
     }
 }
@@ -1807,9 +1812,10 @@ constexpr int halo_smem_bytes() {
 }
 
 // store_tile_t (fast path only: every conv tile is full) with tile row -> output row through row_of
-template <int ACT, class RowOf>
+template <int ACT, class RowOf, bool RES = false>
 __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int rbase,
-                                                int col0, unsigned short* __restrict__ Y, int64_t ldy, RowOf row_of) {
+                                                int col0, unsigned short* __restrict__ Y, int64_t ldy, RowOf row_of,
+                                                const unsigned short* __restrict__ res = nullptr) {
     constexpr int ROWB = 128, SLOTS = 8;
     char* ctile = smem + wave * (128 * ROWB);
     const int r_l = lane & 15, c_l = (lane >> 4) * 4;
@@ -1830,6 +1836,12 @@ __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, 
             *reinterpret_cast<u16x4*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) = o;
         }
     }
+    u16x8 rv[RES ? 16 : 1];
+    if constexpr (RES) {  // residual rows as coalesced 16-B loads, in flight while the tile goes through LDS
+#pragma unroll
+        for (int it = 0; it < 16; ++it)
+            rv[it] = *reinterpret_cast<const u16x8*>(res + row_of(rbase + it * 8 + (lane >> 3)) * ldy + col0 + (lane & 7) * 8);
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
     u16x8 v[16];
 #pragma unroll
@@ -1840,6 +1852,10 @@ __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, 
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int rr = it * 8 + (lane >> 3);
+        if constexpr (RES) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[it][u] = f32_to_bf16(bf16_to_f32(v[it][u]) + bf16_to_f32(rv[it][u]));
+        }
         *reinterpret_cast<u16x8*>(Y + row_of(rbase + rr) * ldy + col0 + (lane & 7) * 8) = v[it];
     }
 }
@@ -1998,10 +2014,12 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
     if (bias)
         lora_mfma_addend<0>(acc, lane, 0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, 1 << 30, N);
     if constexpr (NORM) {
+        // the residual joins in the store phase (coalesced 16-B rows, one more bf16 rounding of the
+        // normalised value: bf16(bf16(norm) + res), as the eager bf16 graph x + norm(conv(h)) rounds)
         conv_rmsnorm_epilogue<1, WMW, WNW>(acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane, row_of, eps,
-                                           nw, nb, res);
+                                           nw, nb, (const unsigned short*)nullptr);
         EGG_STAMP(4);
-        store_tile_rows<0>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of);
+        store_tile_rows<0, decltype(row_of), true>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of, res);
     } else {
         EGG_STAMP(4);
         store_tile_rows<ACT>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of);

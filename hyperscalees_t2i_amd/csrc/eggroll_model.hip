@@ -696,7 +696,10 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
 constexpr int HD_C = 128;                // input channels (the decoder's widths[0])
 constexpr int HD_TH = 8, HD_TW = 16;     // output tile
 constexpr int HD_TR = HD_TH + 2, HD_TC = HD_TW + 2;
-constexpr int HD_PSTR = HD_C * 2 + 16;   // LDS bytes per staged pixel (+16: spreads b128 banks)
+constexpr int HD_PSTR = HD_C * 2;        // LDS bytes per staged pixel: 16-B chunk c of pixel p sits at slot
+                                         // c ^ (p & 15) (conflict-free b128 reads of 16 pixels, no padding:
+                                         // 53 KB per block -> 3 blocks per CU instead of 2)
+__device__ __forceinline__ int hd_slot(int pix, int c) { return pix * HD_PSTR + ((c ^ (pix & 15)) << 4); }
 
 typedef __attribute__((ext_vector_type(8))) __bf16 hd_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float hd_f32x4;
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
                 o8[i] = f2b(t > 0.f ? t : 0.f);
             }
         }
-        if (u < UNITS) *reinterpret_cast<u16x8m*>(tile + (u >> 4) * HD_PSTR + (u & 15) * 16) = o8;
+        if (u < UNITS) *reinterpret_cast<u16x8m*>(tile + hd_slot(u >> 4, u & 15)) = o8;
     }
     __syncthreads();
     // conv: wave w computes output rows 2w, 2w+1 (one 16-pixel M-tile each)
@@ -783,8 +786,7 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const int oy = wave * 2 + r;
-            const hd_bf16x8 af = *reinterpret_cast<const hd_bf16x8*>(
-                tile + ((oy + dy) * HD_TC + n + dx) * HD_PSTR + (cq * 32 + g * 8) * 2);
+            const hd_bf16x8 af = *reinterpret_cast<const hd_bf16x8*>(tile + hd_slot((oy + dy) * HD_TC + n + dx, cq * 4 + g));
             acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[r], 0, 0, 0);
         }
     }

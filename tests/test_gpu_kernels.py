@@ -591,9 +591,12 @@ def test_conv3x3_rmsnorm_nhwc_vs_torch(dev, B, H, W, Cin, px, Cout):
     res = torch.randn(B, H, W, Cout, generator=g).to(dev, torch.bfloat16)
     y = K.conv3x3_rmsnorm_nhwc(x, K.pack_conv3x3_weight(w, px), None, px, 1e-5, nw, nb, res).float()
     z = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), None, padding=1).permute(0, 2, 3, 1)
-    ref = z * torch.rsqrt(z.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float() + nb.float() + res.float()
+    zn = z * torch.rsqrt(z.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float() + nb.float()
+    ref = zn + res.float()
     err = (y - ref).abs()
-    tol = 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    # auto picks the halo kernel where it applies (H % 16 == 0), which rounds the normalised value to
+    # bf16 before the residual add (see test_conv3x3_rmsnorm_halo_vs_torch)
+    tol = 2.0 ** -7 * (ref.abs() + zn.abs()) + 1e-3 * ref.abs().max()
     assert bool((err <= tol).all()), f"max err {err.max().item():.3e}"
 
 
@@ -644,9 +647,12 @@ def test_conv3x3_rmsnorm_halo_vs_torch(dev, B, H, W, Cin, Cout, kern):
     y = K.conv3x3_rmsnorm_nhwc(x, K.pack_conv3x3_weight(w, 1), bias, 1, 1e-5, nw, nb, res, kernel=kern).float()
     z = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), bias.float(), padding=1)
     z = z.permute(0, 2, 3, 1)
-    ref = z * torch.rsqrt(z.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float() + nb.float() + res.float()
+    zn = z * torch.rsqrt(z.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float() + nb.float()
+    ref = zn + res.float()
     err = (y - ref).abs()
-    tol = 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    # the halo kernel adds the residual to the bf16-rounded normalised value in its store phase (two
+    # roundings, as the eager bf16 graph x + norm(conv(h))): the bound covers a rounding of |zn| too
+    tol = 2.0 ** -7 * (ref.abs() + zn.abs()) + 1e-3 * ref.abs().max()
     assert bool((err <= tol).all()), f"max err {err.max().item():.3e}"
 
 

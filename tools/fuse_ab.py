@@ -2,7 +2,7 @@
 
     python tools/fuse_ab.py [--rounds 4] [--knob fuse|xattn]
 fuse: lora.FUSE_EPILOGUES (GEMM-epilogue fusions); xattn: Sana attn2 on eggroll_cross_attention vs
-SDPA.  2 timed epochs per arm per round (box-to-box spread is +-3 %, so only same-process interleaved
+SDPA; chunk: DC-AE decode chunk size ("fused" arm = the first of --chunks).  2 timed epochs per arm per round (box-to-box spread is +-3 %, so only same-process interleaved
 arms are compared)."""
 import argparse
 import json
@@ -18,7 +18,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=4)
-    ap.add_argument("--knob", choices=("fuse", "xattn"), default="fuse")
+    ap.add_argument("--knob", choices=("fuse", "xattn", "chunk"), default="fuse")
+    ap.add_argument("--chunks", type=str, default="8,16", help="knob chunk: the two DC-AE decode chunk sizes")
     a = ap.parse_args()
     import bench
     from hyperscalees_t2i_amd import lora
@@ -31,8 +32,12 @@ def main():
     seed = 10
     blocks = backend.es_model.transformer.transformer_blocks
 
+    ca, cb = (int(c) for c in a.chunks.split(","))
+
     def set_arm(on):
-        if a.knob == "fuse":
+        if a.knob == "chunk":
+            backend.es_model.vae_chunk = ca if on else cb
+        elif a.knob == "fuse":
             lora.FUSE_EPILOGUES = on
         else:
             for blk in blocks:
