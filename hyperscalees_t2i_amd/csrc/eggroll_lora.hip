@@ -1564,6 +1564,14 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
     constexpr int BN = WNW * 64, COUT = BN / PX, WPP = COUT / 64;
     static_assert(WPP == 2 || WPP == 4, "a pixel spans 2 or 4 waves");
     const int rl = lane & 15, cg = lane >> 4;
+    // norm weight / bias: 4 consecutive channels per load, issued ahead of the row-sum barrier
+    u16x4 wq[4], bq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c4 = (wn * 64 + 16 * j + 4 * cg) % COUT;
+        wq[j] = *reinterpret_cast<const u16x4*>(nw + c4);
+        bq[j] = nb ? *reinterpret_cast<const u16x4*>(nb + c4) : u16x4{0, 0, 0, 0};
+    }
     float ss[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1585,9 +1593,8 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
     for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int c = (wn * 64 + 16 * j + 4 * cg + e) % COUT;
-            wv[j][e] = bf16_to_f32(nw[c]);
-            bv[j][e] = nb ? bf16_to_f32(nb[c]) : 0.0f;
+            wv[j][e] = bf16_to_f32(wq[j][e]);
+            bv[j][e] = bf16_to_f32(bq[j][e]);
         }
     const int w0 = (wn / WPP) * WPP;  // first wave of this pixel
 #pragma unroll
@@ -1812,10 +1819,20 @@ constexpr int halo_smem_bytes() {
 }
 
 // store_tile_t (fast path only: every conv tile is full) with tile row -> output row through row_of
-template <int ACT, class RowOf, bool RES = false>
+// the residual rows of a wave's 128 x 64 tile as coalesced 16-B loads (store_tile_rows' order)
+template <int I0 = 0, int I1 = 16, class RowOf>
+__device__ __forceinline__ void load_res_rows(u16x8 (&rv)[16], const unsigned short* __restrict__ res, int lane,
+                                              int rbase, int col0, int64_t ldy, RowOf row_of) {
+#pragma unroll
+    for (int it = I0; it < I1; ++it)
+        rv[it] = *reinterpret_cast<const u16x8*>(res + row_of(rbase + it * 8 + (lane >> 3)) * ldy + col0 + (lane & 7) * 8);
+}
+
+template <int ACT, class RowOf, bool RES = false, bool PRE = false>
 __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int rbase,
                                                 int col0, unsigned short* __restrict__ Y, int64_t ldy, RowOf row_of,
-                                                const unsigned short* __restrict__ res = nullptr) {
+                                                const unsigned short* __restrict__ res = nullptr,
+                                                const u16x8* pre = nullptr) {
     constexpr int ROWB = 128, SLOTS = 8;
     char* ctile = smem + wave * (128 * ROWB);
     const int r_l = lane & 15, c_l = (lane >> 4) * 4;
@@ -1838,9 +1855,13 @@ __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, 
     }
     u16x8 rv[RES ? 16 : 1];
     if constexpr (RES) {  // residual rows as coalesced 16-B loads, in flight while the tile goes through LDS
+        if constexpr (PRE) {  // the first 8 rows were loaded by the caller
 #pragma unroll
-        for (int it = 0; it < 16; ++it)
-            rv[it] = *reinterpret_cast<const u16x8*>(res + row_of(rbase + it * 8 + (lane >> 3)) * ldy + col0 + (lane & 7) * 8);
+            for (int it = 0; it < 8; ++it) rv[it] = pre[it];
+            load_res_rows<8, 16>(rv, res, lane, rbase, col0, ldy, row_of);
+        } else {
+            load_res_rows(rv, res, lane, rbase, col0, ldy, row_of);
+        }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
     u16x8 v[16];
@@ -2016,10 +2037,15 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
     if constexpr (NORM) {
         // the residual joins in the store phase (coalesced 16-B rows, one more bf16 rounding of the
         // normalised value: bf16(bf16(norm) + res), as the eager bf16 graph x + norm(conv(h)) rounds)
+        // (half its loads are issued first, so their latency hides behind the row-sum barrier; all 16
+        // would spill)
+        u16x8 rv[16];
+        load_res_rows<0, 8>(rv, res, lane, wm * 128, n0 + wn * 64, N, row_of);
         conv_rmsnorm_epilogue<1, WMW, WNW>(acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane, row_of, eps,
                                            nw, nb, (const unsigned short*)nullptr);
         EGG_STAMP(4);
-        store_tile_rows<0, decltype(row_of), true>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of, res);
+        store_tile_rows<0, decltype(row_of), true, true>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of,
+                                                         res, rv);
     } else {
         EGG_STAMP(4);
         store_tile_rows<ACT>(acc, smem, wave, lane, wm * 128, n0 + wn * 64, Y, N, row_of);

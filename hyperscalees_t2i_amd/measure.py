@@ -84,6 +84,10 @@ def aux_kernel_rooflines(layout: ThetaLayout, pop: int, member_lo: int, member_h
     newt = torch.empty_like(theta)
     sec = _time(lambda: K.update(theta, fac, fit, layout, pop, antithetic, lr, 0.0, 40.0, out=newt, workspace=ws), it)
     out["update"] = _entry(sec, 4.0 * (nb * F + 2 * D))
+    out["update"]["note"] = "update kernel + the caps pass (theta_max_norm 40): two dependent launches"
+    # the same update without caps: one launch (k_update only), i.e. the HBM-bound kernel by itself
+    sec = _time(lambda: K.update(theta, fac, fit, layout, pop, antithetic, lr, 0.0, 0.0, out=newt, workspace=ws), it)
+    out["update_nocaps"] = _entry(sec, 4.0 * (nb * F + 2 * D))
     out["sizes"] = {"pop": pop, "members": [member_lo, member_hi], "n_base": nb, "D": D,
                     "factor_len": F, "n_tiles": layout.n_tiles}
     return out

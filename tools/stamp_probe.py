@@ -96,14 +96,29 @@ def main():
         bm, bn = (512, 128) if C == 128 else (256, 256)
         nblk = (8 * hw * hw // bm) * (C // bn if C >= bn else 1)
 
-        def conv():
+        rs = torch.randn_like(xc)
+        nw = torch.randn(C, device=dev).bfloat16()
+        nb = torch.randn(C, device=dev).bfloat16()
+
+        def conv(act=0):
             rc = lib.eggroll_conv_nhwc(ctypes.c_void_p(xc.data_ptr()), ctypes.c_void_p(wp.data_ptr()), None,
                                        ctypes.c_int64(8), ctypes.c_int64(hw), ctypes.c_int64(hw), ctypes.c_int64(C),
-                                       ctypes.c_int64(C), ctypes.c_int32(3), ctypes.c_int32(1), ctypes.c_int32(0),
+                                       ctypes.c_int64(C), ctypes.c_int32(3), ctypes.c_int32(1), ctypes.c_int32(act),
                                        ctypes.c_void_p(yc.data_ptr()), st)
             assert rc == 0
+
+        def conv_norm():
+            rc = lib.eggroll_conv3x3_rmsnorm_nhwc(
+                ctypes.c_void_p(xc.data_ptr()), ctypes.c_void_p(wp.data_ptr()), None, ctypes.c_int64(8),
+                ctypes.c_int64(hw), ctypes.c_int64(hw), ctypes.c_int64(C), ctypes.c_int64(C), ctypes.c_int32(1),
+                ctypes.c_float(1e-5), ctypes.c_void_p(nw.data_ptr()), ctypes.c_void_p(nb.data_ptr()),
+                ctypes.c_void_p(rs.data_ptr()), ctypes.c_void_p(yc.data_ptr()), st)
+            assert rc == 0
         report(f"conv3x3 8x{hw}x{hw}x{C}", nblk, conv)
-        del xc, yc
+        report(f"conv3x3 8x{hw}x{hw}x{C} silu", nblk, lambda: conv(2))
+        if C in (128, 256):
+            report(f"conv3x3+rmsnorm 8x{hw}x{hw}x{C}", nblk, conv_norm)
+        del xc, yc, rs
 
 
 if __name__ == "__main__":
