@@ -1102,6 +1102,9 @@ extern "C" int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps
     else if (nch <= 64) launch_rownorm<64, 1>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
     else if (nch <= 128) launch_rownorm<64, 2>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
     else if (nch <= 256) launch_rownorm<64, 4>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
+    // Sana's C = 2240 (280 chunks): 5 chunks per lane use 88 % of the slots (8: 55 %, 64 dead value
+    // registers); a lane sums the same chunks in the same order either way, so the bits do not change
+    else if (nch <= 320) launch_rownorm<64, 5>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
     else launch_rownorm<64, 8>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
     EGG_CHECK_LAUNCH("rownorm");
     return EGGROLL_OK;

@@ -310,7 +310,7 @@ def test_dwconv_rejects_unsupported_channels(dev):
 
 
 # ---------------------------------------------------------------------------------- fused row ops (model)
-@pytest.mark.parametrize("C", [32, 128, 256, 512, 1024, 2240])
+@pytest.mark.parametrize("C", [32, 128, 256, 512, 1024, 2240, 2560, 4096])
 @pytest.mark.parametrize("mode", ["rms_w_b_res", "rms_relu", "layer_adaln"])
 def test_rownorm_vs_torch(dev, C, mode):
     g = torch.Generator().manual_seed(C)
