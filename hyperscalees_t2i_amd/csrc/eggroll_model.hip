@@ -714,7 +714,8 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
     __shared__ __attribute__((aligned(16))) unsigned short wl[3 * 9 * HD_C];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int bid = blockIdx.x;
+    // XCD-contiguous tile ranges: horizontally adjacent tiles (sharing 2 halo columns) on one L2
+    int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int xt = bid % xtiles;
     bid /= xtiles;
     const int band = bid % bands;
