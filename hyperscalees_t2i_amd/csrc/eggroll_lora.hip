@@ -660,11 +660,30 @@ struct EpiArgs {
 };
 __device__ __forceinline__ float epi_silu(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
 
+// x * sigmoid(x) on two values: the multiplies / add as packed fp32 ops (v_pk_mul_f32 / v_pk_add_f32),
+// exp2 and rcp per value: the same operations, value by value, as x * rcp(1 + __expf(-x)) (v_mul by
+// log2(e), v_exp_f32, v_add, v_rcp_f32, v_mul), so the same bits (test_lora_linear_pop_epilogue_bitexact)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 silu2(f32x2 v) {
+    f32x2 t = v * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+    t.x = __builtin_amdgcn_exp2f(t.x);
+    t.y = __builtin_amdgcn_exp2f(t.y);
+    t = t + (f32x2){1.0f, 1.0f};
+    t.x = __builtin_amdgcn_rcpf(t.x);
+    t.y = __builtin_amdgcn_rcpf(t.y);
+    return v * t;
+}
+
+
 template <int EPI>
 __device__ __forceinline__ u16x8 epi_apply(u16x8 v, int row, int col, const EpiArgs& ea) {
     if constexpr (EPI == EPI_SILU) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(epi_silu(bf16_to_f32(v[u])));
+        for (int u = 0; u < 8; u += 2) {
+            const f32x2 t = silu2((f32x2){bf16_to_f32(v[u]), bf16_to_f32(v[u + 1])});
+            v[u] = f32_to_bf16(t.x);
+            v[u + 1] = f32_to_bf16(t.y);
+        }
     } else if constexpr (EPI == EPI_RES || EPI == EPI_GATED) {
         const u16x8 r = *reinterpret_cast<const u16x8*>(ea.res + (int64_t)row * ea.ldr + col);
         if constexpr (EPI == EPI_RES) {
@@ -1542,9 +1561,10 @@ __device__ __forceinline__ void store_tile_t_act(f32x4 (&acc)[8][4], char* smem,
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float v = acc[i][j][e];
-                    acc[i][j][e] = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+                for (int e = 0; e < 4; e += 2) {
+                    const f32x2 t = silu2((f32x2){acc[i][j][e], acc[i][j][e + 1]});
+                    acc[i][j][e] = t.x;
+                    acc[i][j][e + 1] = t.y;
                 }
     }
     store_tile_t(acc, smem, wave, lane, m0, n0, rbase, cbase, M, N, Y, ldy);
@@ -1845,10 +1865,11 @@ __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, 
             const int slot = (cc >> 3) ^ (rr & (SLOTS - 1));
             u16x4 o;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float v = acc[i][j][e];
-                if constexpr (ACT == 1) v = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
-                o[e] = f32_to_bf16(v);
+            for (int e = 0; e < 4; e += 2) {
+                f32x2 v = {acc[i][j][e], acc[i][j][e + 1]};
+                if constexpr (ACT == 1) v = silu2(v);
+                o[e] = f32_to_bf16(v.x);
+                o[e + 1] = f32_to_bf16(v.y);
             }
             *reinterpret_cast<u16x4*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) = o;
         }
