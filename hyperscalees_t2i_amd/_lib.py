@@ -6,6 +6,7 @@ fails, an exception is raised.  Build it with `python -m hyperscalees_t2i_amd.bu
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import os
 import re
 from pathlib import Path
@@ -13,6 +14,8 @@ from pathlib import Path
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = _PKG / "_build" / "libeggroll.so"
 HEADER = _PKG.parent / "include" / "eggroll.h"
+SOURCE_FILES = [_PKG / "csrc" / n for n in ("eggroll_es.hip", "eggroll_lora.hip", "eggroll_model.hip", "common.h")] \
+    + [HEADER]
 
 i32, i64, u32, u64, f32 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
 vp = C.c_void_p
@@ -38,6 +41,7 @@ SIGNATURES = {
                                               vp, i64, vp, i32, vp]),
     "eggroll_lora_workspace_bytes": (i64, [i64, i64, i32, i64]),
     "eggroll_lora_project": (C.c_int, [vp, i64, vp, i64, i64, i32, i64, i64, i64, vp, vp]),
+    "eggroll_lora_project_multi": (C.c_int, [vp, i64, vp, i64, vp, i32, i32, i64, i64, i64, vp, vp]),
     "eggroll_dwconv_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i32, i32, i32, vp, vp]),
     "eggroll_rownorm": (C.c_int, [vp, i64, i64, f32, i32, vp, vp, vp, vp, i64, i64, i32, vp, vp, vp]),
     "eggroll_gated_residual": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, vp]),
@@ -58,7 +62,8 @@ SIGNATURES = {
     "eggroll_lora_expand": (C.c_int, [vp, vp, i64, i64, i32, f32, i64, i64, i64, vp, i64, vp]),
     "eggroll_lora_linear_pop_epi": (C.c_int, [vp, i64, vp, i64, vp, vp, i64, i64, i64, i32, f32, i64, i64, i64, i64,
                                               vp, i64, vp, i32, vp, i64, vp, i64, i64, vp]),
-    "eggroll_cross_attention": (C.c_int, [vp, i64, vp, vp, i64, vp, vp, i64, i64, i64, i64, i64, f32, vp, i64, vp]),
+    "eggroll_cross_attention": (C.c_int, [vp, i64, vp, vp, i64, vp, vp, i64, i64, i64, i64, i64, i64, f32, vp, i64,
+                                         vp]),
     "eggroll_clip_preprocess": (C.c_int, [vp, i64, i64, i64, i64, i64, i64, i64, i32, vp, vp, i32, i32, i64, i64,
                                           i64, vp, vp, vp, vp, vp]),
 }
@@ -76,15 +81,43 @@ def header_symbols() -> list:
     return sorted(set(re.findall(r"\b(eggroll_[a-z0-9_]+)\s*\(", txt)))
 
 
+def source_digest() -> str:
+    """sha256 over the library's sources + public header (what build_ext compiles)."""
+    h = hashlib.sha256()
+    for f in SOURCE_FILES:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def check_fresh(path: Path = LIB_PATH) -> None:
+    """Raise if the library at `path` was not built from the sources in this tree.
+
+    build_ext writes the digest of the sources it compiled next to the library; a prebuilt .so
+    pushed with a newer source tree (or an older one) is refused instead of silently tested."""
+    stamp = path.with_name(path.name + ".srcsha256")
+    if not all(f.exists() for f in SOURCE_FILES):
+        return  # installed without sources: nothing to compare against
+    if not stamp.exists():
+        raise EggrollError(f"{path} has no source stamp ({stamp.name}): rebuild with "
+                           "`python -m hyperscalees_t2i_amd.build_ext --force`")
+    if stamp.read_text().strip() != source_digest():
+        raise EggrollError(f"stale {path}: csrc/ or include/eggroll.h changed since it was built; rebuild with "
+                           "`python -m hyperscalees_t2i_amd.build_ext`")
+
+
 def load():
     global _lib
     if _lib is not None:
         return _lib
-    path = Path(os.environ.get("EGGROLL_LIB", LIB_PATH))
+    override = os.environ.get("EGGROLL_LIB")
+    path = Path(override or LIB_PATH)
     if not path.exists():
         raise EggrollError(
             f"libeggroll.so not found at {path}: build it with `python -m hyperscalees_t2i_amd.build_ext` "
             "(there is no CPU fallback)")
+    if not override:
+        check_fresh(path)
     lib = C.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

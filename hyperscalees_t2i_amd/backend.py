@@ -156,34 +156,14 @@ class SanaBackend(ESBackend):
     def save_lora(self, save_dir: Path) -> None:
         """PEFT-style adapter dir: adapter_config.json + adapter_model.safetensors
         (keys base_model.model.<module>.lora_{A,B}.weight)."""
-        from safetensors.torch import save_file
-        save_dir = Path(save_dir)
-        save_dir.mkdir(parents=True, exist_ok=True)
-        tensors = {}
-        for name, p in self.es_model.transformer.named_parameters():
-            if p.requires_grad:
-                tensors[f"base_model.model.{name}"] = p.detach().float().cpu().contiguous()
-        save_file(tensors, str(save_dir / "adapter_model.safetensors"))
-        cfg = {"peft_type": "LORA", "r": self.cfg.lora_r, "lora_alpha": self.cfg.lora_alpha,
-               "lora_dropout": self.cfg.lora_dropout, "target_modules": list(self.cfg.lora_target_modules),
-               "base_model_name_or_path": self.cfg.model_name, "bias": "none", "task_type": None}
-        (save_dir / "adapter_config.json").write_text(json.dumps(cfg, indent=2))
+        _save_adapter(self.es_model.transformer, Path(save_dir),
+                      {"peft_type": "LORA", "r": self.cfg.lora_r, "lora_alpha": self.cfg.lora_alpha,
+                       "lora_dropout": self.cfg.lora_dropout, "target_modules": list(self.cfg.lora_target_modules),
+                       "base_model_name_or_path": self.cfg.model_name, "bias": "none", "task_type": None})
 
     def load_lora(self, save_dir: Path) -> None:
-        """Inverse of save_lora (resume; the reference is write-only): copy the adapter tensors of
-        save_dir/adapter_model.safetensors back into the LoRA parameters.  Every trainable parameter
-        must be present with its shape, and no extra key may exist (ValueError otherwise)."""
-        from safetensors.torch import load_file
-        tensors = load_file(str(Path(save_dir) / "adapter_model.safetensors"))
-        want = {f"base_model.model.{n}": p for n, p in self.es_model.transformer.named_parameters() if p.requires_grad}
-        if set(tensors) != set(want):
-            raise ValueError(f"adapter keys differ: missing {sorted(set(want) - set(tensors))[:3]}, "
-                             f"unexpected {sorted(set(tensors) - set(want))[:3]}")
-        with torch.no_grad():
-            for k, p in want.items():
-                if tuple(tensors[k].shape) != tuple(p.shape):
-                    raise ValueError(f"{k}: shape {tuple(tensors[k].shape)} != {tuple(p.shape)}")
-                p.copy_(tensors[k].to(p.device, p.dtype))
+        """Inverse of save_lora (resume; the reference is write-only), see _load_adapter."""
+        _load_adapter(self.es_model.transformer, Path(save_dir))
 
     def step_sampling_info(self, seed: int) -> Dict[str, Any]:
         """es_backend.py:234-263 (bit-exact indices: np.random.RandomState(seed).choice)."""
@@ -247,6 +227,22 @@ def _save_adapter(model: torch.nn.Module, save_dir: Path, cfg_dict: Dict[str, An
                for n, p in model.named_parameters() if p.requires_grad}
     save_file(tensors, str(save_dir / "adapter_model.safetensors"))
     (save_dir / "adapter_config.json").write_text(json.dumps(cfg_dict, indent=2))
+
+
+def _load_adapter(model: torch.nn.Module, save_dir: Path) -> None:
+    """Copy save_dir/adapter_model.safetensors back into the model's LoRA parameters.  Every trainable
+    parameter must be present with its shape, and no extra key may exist (ValueError otherwise)."""
+    from safetensors.torch import load_file
+    tensors = load_file(str(Path(save_dir) / "adapter_model.safetensors"))
+    want = {f"base_model.model.{n}": p for n, p in model.named_parameters() if p.requires_grad}
+    if set(tensors) != set(want):
+        raise ValueError(f"adapter keys differ: missing {sorted(set(want) - set(tensors))[:3]}, "
+                         f"unexpected {sorted(set(tensors) - set(want))[:3]}")
+    with torch.no_grad():
+        for k, p in want.items():
+            if tuple(tensors[k].shape) != tuple(p.shape):
+                raise ValueError(f"{k}: shape {tuple(tensors[k].shape)} != {tuple(p.shape)}")
+            p.copy_(tensors[k].to(p.device, p.dtype))
 
 
 def imagenet_prompt_text(class_id: int, labels_path: Union[str, Path] = "imagenet_classes.txt") -> str:
@@ -328,6 +324,11 @@ class VarBackend(ESBackend):
                        "target_modules": list(c.lora_target_modules),
                        "base_model_name_or_path": f"FoundationVision/var (depth={self.es_model.model_depth})",
                        "bias": "none", "task_type": None})
+
+    def load_lora(self, save_dir: Path) -> None:
+        """Inverse of save_lora (resume), see _load_adapter.  The mat_qkv LoRA entries round-trip too:
+        they are in theta (perturbed, updated) even though the reference's F.linear bypasses them."""
+        _load_adapter(self.es_model.transformer, Path(save_dir))
 
     def _sample_classes_unique(self, seed: int, num_classes_total: int = 1000) -> List[int]:
         return sample_classes_unique(seed, self.cfg.allowed_classes, self.cfg.classes_per_gen, num_classes_total)

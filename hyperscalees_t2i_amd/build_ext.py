@@ -27,17 +27,23 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm required to build libeggroll)")
 
 
+STAMP = LIB.with_name(LIB.name + ".srcsha256")
+
+
 def _stale() -> bool:
-    if not LIB.exists():
+    """The library is current iff its stamp holds the digest of today's sources (content, not mtime:
+    a snapshot copied to another machine keeps its bytes but not necessarily its timestamps)."""
+    from ._lib import source_digest
+    if not LIB.exists() or not STAMP.exists():
         return True
-    t = LIB.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES] + [CSRC / "common.h", ROOT / "include" / "eggroll.h"]
-    return any(d.stat().st_mtime > t for d in deps)
+    return STAMP.read_text().strip() != source_digest()
 
 
 def build(force: bool = False, verbose: bool = True) -> Path:
+    from ._lib import source_digest
     if not force and not _stale():
         return LIB
+    digest = source_digest()
     BUILD.mkdir(parents=True, exist_ok=True)
     objs, procs = [], []
     for s in SOURCES:   # the translation units compile in parallel (one hipcc each)
@@ -57,6 +63,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    STAMP.write_text(digest + "\n")
     return LIB
 
 

@@ -921,7 +921,20 @@ int64_t eggroll_tile_table(const eggroll_mat_t* mats_host, int32_t n_mats, int32
     }
     int64_t n = 0;
     for (int32_t i = 0; i < n_mats; ++i) {
-        const int64_t c = egg_tile_count(mats_host[i], rank);
+        const eggroll_mat_t& mt = mats_host[i];
+        if (mt.rows < 1 || mt.cols < 0) {
+            set_error("tile_table: mat %d has rows=%lld cols=%lld", i, (long long)mt.rows, (long long)mt.cols);
+            return EGGROLL_ERR_ARG;
+        }
+        // the generic per-element path (T_VEC / T_GEN) indexes elements in 32-bit ints
+        const int kind = egg_tile_kind(mt, rank);
+        const int64_t numel = mt.cols ? mt.rows * mt.cols : mt.rows;
+        if ((kind == T_VEC || kind == T_GEN) && numel >= (1ll << 31) - EGGROLL_CHUNK) {
+            set_error("tile_table: mat %d (%lld elements) is too large for the generic per-element path", i,
+                      (long long)numel);
+            return EGGROLL_ERR_ARG;
+        }
+        const int64_t c = egg_tile_count(mt, rank);
         for (int64_t t = 0; t < c; ++t, ++n) {
             if (tiles_host && n < capacity) {
                 tiles_host[n].mat = i;

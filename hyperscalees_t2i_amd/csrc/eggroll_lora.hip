@@ -143,6 +143,131 @@ __global__ __launch_bounds__(256) void k_lora_project_ra(const unsigned short* _
 }
 
 // ------------------------------------------------------------------------------------
+// Multi-linear projection on MFMA: T_l[row, q] = X[row,:] . A_{k,l}[q,:] for n_lin LoRA linears that
+// read the SAME X (Sana attn1 to_q / to_k / to_v, attn2 to_k / to_v): X streams from HBM once instead
+// of once per linear.  As a GEMM it is [M x K] x [K x 16]: the B operand holds the NQ = n_lin * r
+// rows of A as bf16 hi / lo pairs (columns q and NQ + q: hi = bf16(a), lo = bf16(a - hi), so
+// hi + lo carries a to ~2^-16 relative), X is the A operand straight from global memory, fp32
+// accumulation.  The reduction over K is order-free, so K is permuted to make every lane's X read
+// contiguous: in each 128-column group lane-group h = lane >> 4 owns columns [h*32, h*32 + 32) as
+// four 16-byte pieces, piece j feeding MFMA k-step j; the B image in LDS uses the same permutation
+// (a K % 128 tail runs in the plain 8-column layout).  The B image of the block's member is built in
+// LDS once (K * 32 bytes); each wave runs two 16-row groups (32 rows, 8 KiB of X in flight) per pass.
+//   img[s][lane] = 8 bf16: column n = lane & 15, K-columns col(s, lane >> 4, 0..7).
+// ------------------------------------------------------------------------------------
+constexpr int PM_ROWS_PER_BLOCK = 256;  // 4 waves x 2 groups x 16 rows x 2 passes
+
+__device__ __forceinline__ int64_t pm_col(int s, int h, int64_t ng) {
+    // first of the 8 consecutive K-columns of k-step s held by lane-group h
+    return s < 4 * ng ? (int64_t)(s >> 2) * 128 + h * 32 + (s & 3) * 8 : ng * 128 + (int64_t)(s - 4 * ng) * 32 + h * 8;
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) void k_lora_project_mfma(const unsigned short* __restrict__ X, int64_t ldx,
+                                                           const float* __restrict__ theta_pop, int64_t ld_theta,
+                                                           int64_t offA0, int64_t offA1, int64_t offA2,
+                                                           int64_t offA3, int r, int64_t rows_per_member,
+                                                           int64_t M, int64_t K, float* __restrict__ T) {
+    extern __shared__ __attribute__((aligned(16))) char pm_smem[];
+    bf16x8* img = reinterpret_cast<bf16x8*>(pm_smem);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 4, n = lane & 15;
+    const int nsteps = (int)(K / 32);
+    const int64_t ng = K / 128;
+    const int64_t r0 = (int64_t)blockIdx.x * PM_ROWS_PER_BLOCK;
+    const int64_t r1 = r0 + PM_ROWS_PER_BLOCK < M ? r0 + PM_ROWS_PER_BLOCK : M;
+    const int64_t kl_first = r0 / rows_per_member, kl_last = (r1 - 1) / rows_per_member;
+    for (int64_t kl = kl_first; kl <= kl_last; ++kl) {
+        // ---- B image of member kl: entry (s, ln) = 8 bf16 of column ln & 15 ----
+        if (kl != kl_first) __syncthreads();  // every wave is done with the previous image
+        for (int e = threadIdx.x; e < nsteps * 64; e += 256) {
+            const int s = e >> 6, ln = e & 63, cn = ln & 15;
+            bf16x8 v;
+            if (cn < 2 * NQ) {
+                const int q = cn < NQ ? cn : cn - NQ, l = q / r, qq = q - l * r;
+                const int64_t off = l == 0 ? offA0 : l == 1 ? offA1 : l == 2 ? offA2 : offA3;
+                const float* a = theta_pop + kl * ld_theta + off + (int64_t)qq * K + pm_col(s, ln >> 4, ng);
+                const float4 a0 = *reinterpret_cast<const float4*>(a);
+                const float4 a1 = *reinterpret_cast<const float4*>(a + 4);
+                const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const __bf16 hi = (__bf16)av[t];
+                    v[t] = cn < NQ ? hi : (__bf16)(av[t] - (float)hi);
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = (__bf16)0.0f;
+            }
+            img[e] = v;
+        }
+        __syncthreads();
+        const int64_t mlo = kl * rows_per_member > r0 ? kl * rows_per_member : r0;
+        const int64_t mhi = (kl + 1) * rows_per_member < r1 ? (kl + 1) * rows_per_member : r1;
+        for (int64_t g0 = r0 + wave * 32; g0 < r1; g0 += 4 * 32) {
+            if (g0 + 32 <= mlo || g0 >= mhi) continue;  // wave-uniform: no row of this pass in member kl
+            const int64_t ra = g0 + n, rb = g0 + 16 + n;
+            const bool va = ra >= mlo && ra < mhi, vb = rb >= mlo && rb < mhi;
+            const unsigned short* xa = X + (va ? ra : mlo) * ldx + h * 32;
+            const unsigned short* xb = X + (vb ? rb : mlo) * ldx + h * 32;
+            f32x4 acc_a = {0.f, 0.f, 0.f, 0.f}, acc_b = acc_a;
+            const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+            u16x8 ca[4], cb[4];
+            if (ng > 0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    ca[j] = va ? *reinterpret_cast<const u16x8*>(xa + j * 8) : z;
+                    cb[j] = vb ? *reinterpret_cast<const u16x8*>(xb + j * 8) : z;
+                }
+            }
+            for (int64_t G = 0; G < ng; ++G) {
+                u16x8 na[4], nb[4];
+                const bool more = G + 1 < ng;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {  // next group's X in flight under this group's MFMAs
+                    na[j] = (more && va) ? *reinterpret_cast<const u16x8*>(xa + (G + 1) * 128 + j * 8) : z;
+                    nb[j] = (more && vb) ? *reinterpret_cast<const u16x8*>(xb + (G + 1) * 128 + j * 8) : z;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bf16x8 bfr = img[(G * 4 + j) * 64 + lane];
+                    acc_a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ca[j]), bfr, acc_a,
+                                                                    0, 0, 0);
+                    acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cb[j]), bfr, acc_b,
+                                                                    0, 0, 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    ca[j] = na[j];
+                    cb[j] = nb[j];
+                }
+            }
+            for (int s = (int)(4 * ng); s < nsteps; ++s) {  // K % 128 tail, plain layout
+                const int64_t c = pm_col(s, h, ng) - h * 32;
+                const u16x8 xa8 = va ? *reinterpret_cast<const u16x8*>(xa + c) : z;
+                const u16x8 xb8 = vb ? *reinterpret_cast<const u16x8*>(xb + c) : z;
+                const bf16x8 bfr = img[s * 64 + lane];
+                acc_a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xa8), bfr, acc_a, 0, 0, 0);
+                acc_b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xb8), bfr, acc_b, 0, 0, 0);
+            }
+            // D[4h + i][n]: T[q] = D[q] (hi) + D[NQ + q] (lo), joined across lanes n and n + NQ
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float ta = acc_a[i] + __shfl(acc_a[i], (lane + NQ) & 63, 64);
+                const float tb = acc_b[i] + __shfl(acc_b[i], (lane + NQ) & 63, 64);
+                if (n < NQ) {
+                    const int l = n / r, qq = n - l * r;
+                    float* Tl = T + (int64_t)l * M * r;
+                    const int64_t rowa = g0 + 4 * h + i, rowb = g0 + 16 + 4 * h + i;
+                    if (rowa >= mlo && rowa < mhi) Tl[rowa * r + qq] = ta;
+                    if (rowb >= mlo && rowb < mhi) Tl[rowb * r + qq] = tb;
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Base GEMM + fused LoRA epilogue, templated on the tile:
 //   Tile<BM, BN, WM, WN>: BM x BN output tile, BK = 64, WM x WN waves (wave tile (BM/WM) x (BN/WN)),
 //   2 LDS stages of (BM + BN) rows x 128 B, one barrier per K-tile: the global_load_lds of K-tile
@@ -2099,6 +2224,40 @@ int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int
     if (M == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(X && theta_pop && T, "lora_project: NULL pointer");
     return project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T, as_stream(stream));
+}
+
+int eggroll_lora_project_multi(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
+                               const int64_t* offA_host, int32_t n_lin, int32_t r, int64_t rows_per_member, int64_t M,
+                               int64_t K, float* T, void* stream) {
+    EGG_CHECK_ARG(n_lin >= 1 && n_lin <= 4 && r >= 1 && n_lin * r <= 8,
+                  "lora_project_multi: need 1 <= n_lin <= 4 and n_lin * r <= 8 (n_lin=%d r=%d)", n_lin, r);
+    EGG_CHECK_ARG(M >= 0 && K >= 32 && K % 32 == 0 && K <= 4096, "lora_project_multi: need K %% 32 == 0, K <= 4096");
+    EGG_CHECK_ARG(ldx % 8 == 0 && ldx >= K, "lora_project_multi: ldx must be a multiple of 8 and >= K");
+    EGG_CHECK_ARG(rows_per_member > 0 && ld_theta % 4 == 0, "lora_project_multi: bad rows_per_member / ld_theta");
+    if (M == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(X && theta_pop && T && offA_host, "lora_project_multi: NULL pointer");
+    int64_t off[4] = {0, 0, 0, 0};
+    for (int l = 0; l < n_lin; ++l) {
+        off[l] = offA_host[l];
+        EGG_CHECK_ARG(off[l] >= 0 && off[l] % 4 == 0 && off[l] + (int64_t)r * K <= ld_theta,
+                      "lora_project_multi: offA[%d] must be 16-byte aligned and inside a theta row", l);
+    }
+    const unsigned grid = (unsigned)((M + PM_ROWS_PER_BLOCK - 1) / PM_ROWS_PER_BLOCK);
+    const size_t lds = (size_t)K * 32;
+    hipStream_t st = as_stream(stream);
+#define EGG_PM_CASE(nq)                                                                                          \
+    case nq:                                                                                                     \
+        hipLaunchKernelGGL(k_lora_project_mfma<nq>, dim3(grid), dim3(256), lds, st, (const unsigned short*)X, ldx, \
+                           theta_pop, ld_theta, off[0], off[1], off[2], off[3], (int)r, rows_per_member, M, K, T); \
+        break;
+    switch (n_lin * r) {
+        EGG_PM_CASE(1) EGG_PM_CASE(2) EGG_PM_CASE(3) EGG_PM_CASE(4)
+        EGG_PM_CASE(5) EGG_PM_CASE(6) EGG_PM_CASE(7) EGG_PM_CASE(8)
+        default: break;
+    }
+#undef EGG_PM_CASE
+    EGG_CHECK_LAUNCH("lora_project_multi");
+    return EGGROLL_OK;
 }
 
 int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,

@@ -930,7 +930,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
                                                     const unsigned short* __restrict__ v, int64_t ldkv,
                                                     const unsigned short* __restrict__ bias,
                                                     const int* __restrict__ enc_index, int heads, int N, int L,
-                                                    float scale, unsigned short* __restrict__ o, int64_t ldo) {
+                                                    int U, float scale, unsigned short* __restrict__ o, int64_t ldo) {
     // NWAVE waves sweep the image's queries in blocks of 16 * QF (QF query fragments share every k / v
     // fragment read from LDS)
     constexpr int RS = HD + 8, KSN = (HD + 31) / 32, DF = HD / 16;  // LDS row stride, Q.K k-steps, PV dim frags
@@ -941,7 +941,9 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     constexpr int NT = 64 * NWAVE;
     const int bh = xcd_remap(blockIdx.x, gridDim.x);
     const int b = bh / heads, h = bh - b * heads;
-    const int u = enc_index ? enc_index[b] : b;
+    const int u_in = enc_index ? enc_index[b] : b;
+    const bool u_bad = u_in < 0 || u_in >= U;  // out-of-range caption row: NaN output, no out-of-bounds read
+    const int u = u_bad ? 0 : u_in;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
     // stage k / v rows of caption u, head h: 14 chunks of 16 B per row; rows >= L are zeros
     constexpr int CH = HD / 8;
@@ -957,7 +959,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
         *reinterpret_cast<u16x8m*>(sv + r * RS + cc * 8) = vv;
     }
     for (int r = tid; r < XA_LMAX; r += NT)
-        sb[r] = r < L ? (bias ? b2f(bias[(int64_t)u * L + r]) : 0.0f) : -INFINITY;
+        sb[r] = u_bad ? __builtin_nanf("") : r < L ? (bias ? b2f(bias[(int64_t)u * L + r]) : 0.0f) : -INFINITY;
     __syncthreads();
     const int nkf = (L + 15) / 16, nkb = (L + 31) / 32;  // key fragments / 32-key PV steps in use
     const int nqb = (N + 16 * QF - 1) / (16 * QF);
@@ -1334,11 +1336,13 @@ extern "C" int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, in
 
 extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
                                        const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
-                                       int64_t heads, int64_t head_dim, int64_t L, float scale, void* o, int64_t ldo,
-                                       void* stream) {
+                                       int64_t heads, int64_t head_dim, int64_t L, int64_t U, float scale, void* o,
+                                       int64_t ldo, void* stream) {
     EGG_CHECK_ARG(head_dim == 64 || head_dim == 80 || head_dim == 112, "cross_attention: head_dim %lld unsupported "
                   "(64, 80, 112)", (long long)head_dim);
     EGG_CHECK_ARG(B >= 0 && N > 0 && heads > 0 && L > 0 && L <= XA_LMAX, "cross_attention: bad sizes (L <= %d)", XA_LMAX);
+    EGG_CHECK_ARG(U > 0 && U * L < (1ll << 31) && (enc_index || U >= B),
+                  "cross_attention: U=%lld caption rows (need U >= B without enc_index)", (long long)U);
     EGG_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldo % 4 == 0 && ldq >= heads * head_dim &&
                   ldkv >= heads * head_dim && ldo >= heads * head_dim, "cross_attention: bad strides");
     if (B == 0) return EGGROLL_OK;
@@ -1352,7 +1356,8 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
 #define EGG_XA(HD_)                                                                                              \
     hipLaunchKernelGGL((k_cross_attn<HD_, 8, 1>), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream),  \
                        (const unsigned short*)q, ldq, (const unsigned short*)k, (const unsigned short*)v, ldkv,    \
-                       (const unsigned short*)bias, enc_index, (int)heads, (int)N, (int)L, scale, (unsigned short*)o, ldo)
+                       (const unsigned short*)bias, enc_index, (int)heads, (int)N, (int)L, (int)U, scale, (unsigned short*)o, \
+                       ldo)
     if (head_dim == 112) EGG_XA(112);
     else if (head_dim == 80) EGG_XA(80);
     else EGG_XA(64);

@@ -384,6 +384,25 @@ def lora_project(x: torch.Tensor, theta_pop: torch.Tensor, offA: int, r: int, ro
     return out
 
 
+def lora_project_multi(x: torch.Tensor, theta_pop: torch.Tensor, offAs: Sequence[int], r: int, rows_per_member: int,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """T_l = X A_{k,l}^T for several LoRA linears reading the same x, x read once (MFMA, A as bf16 hi + lo:
+    equal to lora_project to fp32 rounding).  Returns [n_lin, M, r] fp32."""
+    _dev(x, "lora_project_multi(x)", torch.bfloat16)
+    _dev(theta_pop, "lora_project_multi(theta_pop)", torch.float32)
+    M, Kd = x.shape
+    n = len(offAs)
+    if out is None:
+        out = torch.empty((n, M, r), dtype=torch.float32, device=x.device)
+    _dev(out, "lora_project_multi(out)", torch.float32)
+    if out.numel() < n * M * r:
+        raise ValueError("lora_project_multi: out too small")
+    offs = np.asarray([int(o) for o in offAs], dtype=np.int64)
+    _lib.call("eggroll_lora_project_multi", x.data_ptr(), x.stride(0), theta_pop.data_ptr(), theta_pop.stride(0),
+              offs.ctypes.data, n, r, rows_per_member, M, Kd, out.data_ptr(), _stream(x.device))
+    return out
+
+
 def lora_expand(T: torch.Tensor, theta_pop: torch.Tensor, offB: int, r: int, scale: float, rows_per_member: int,
                 y: torch.Tensor) -> torch.Tensor:
     _dev(T, "lora_expand(T)", torch.float32)
@@ -754,16 +773,31 @@ def cross_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, N
             raise _lib.EggrollError(f"cross_attention({nm}): expected a bf16 device view with unit inner stride")
     if k.stride(0) != v.stride(0):
         raise ValueError("cross_attention: k / v must share a row stride")
+    if (k.shape[0] != v.shape[0] or k.shape[0] % L or k.shape[0] == 0 or min(k.shape[1], v.shape[1]) < heads * head_dim):
+        raise ValueError(f"cross_attention: k / v {tuple(k.shape)} / {tuple(v.shape)} are not [U*L, >= heads*hd] "
+                         f"with L={L}")
+    U = k.shape[0] // L
+    if q.shape[0] < B * N or q.shape[1] < heads * head_dim:
+        raise ValueError(f"cross_attention: q {tuple(q.shape)} has fewer than B*N={B * N} rows of heads*hd")
     if out is None:
         out = torch.empty((B * N, heads * head_dim), dtype=torch.bfloat16, device=q.device)
     if bias is not None:
         _dev(bias, "cross_attention(bias)", torch.bfloat16)
+        if tuple(bias.shape) != (U, L):
+            raise ValueError(f"cross_attention: bias {tuple(bias.shape)} must be [U, L] = [{U}, {L}]")
     ei = None
     if enc_index is not None:
+        if enc_index.numel() != B:
+            raise ValueError(f"cross_attention: enc_index has {enc_index.numel()} entries, expected B={B}")
+        if enc_index.device.type == "cpu" and B and (int(enc_index.min()) < 0 or int(enc_index.max()) >= U):
+            raise ValueError(f"cross_attention: enc_index outside [0, {U})")
+        # a device-resident enc_index is range-checked in the kernel (out-of-range images come out NaN)
         ei = enc_index.to(device=q.device, dtype=torch.int32).contiguous()
+    elif U < B:
+        raise ValueError(f"cross_attention: {U} caption rows for B={B} images without enc_index")
     e0 = OpTimer.begin()
     _lib.call("eggroll_cross_attention", q.data_ptr(), q.stride(0), k.data_ptr(), v.data_ptr(), k.stride(0), _p(bias),
-              _p(ei), B, N, heads, head_dim, L, float(scale), out.data_ptr(), out.stride(0), _stream(q.device))
+              _p(ei), B, N, heads, head_dim, L, U, float(scale), out.data_ptr(), out.stride(0), _stream(q.device))
     OpTimer.end(e0, "cross_attention", 2.0 * (2 * B * N * heads * head_dim + 2 * k.shape[0] * heads * head_dim),
                 f"B{B} N{N} L{L}")
     return out

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Dict, Iterable, List, Optional
+from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
 from torch import nn
@@ -40,11 +40,17 @@ class PopulationContext:
     theta_pop: Optional[torch.Tensor] = None  # [n_members, ld] fp32 (perturbed theta per member)
     n_members: int = 1
     T_ws: Optional[torch.Tensor] = None       # reusable fp32 workspace for T = X A_k^T
+    multi_ws: Optional[torch.Tensor] = None   # T of the linears sharing one input (shared_projection)
 
     def workspace(self, numel: int, device) -> torch.Tensor:
         if self.T_ws is None or self.T_ws.numel() < numel or self.T_ws.device != torch.device(device):
             self.T_ws = torch.empty(max(numel, 1), dtype=torch.float32, device=device)
         return self.T_ws
+
+    def multi_workspace(self, numel: int, device) -> torch.Tensor:
+        if self.multi_ws is None or self.multi_ws.numel() < numel or self.multi_ws.device != torch.device(device):
+            self.multi_ws = torch.empty(max(numel, 1), dtype=torch.float32, device=device)
+        return self.multi_ws[:numel]
 
 
 class GemmTimer:
@@ -131,10 +137,12 @@ class LoRALinear(nn.Module):
                 self.lora_B.weight.zero_()
 
     def forward(self, x: torch.Tensor, epi: Optional[str] = None, res: Optional[torch.Tensor] = None,
-                gate: Optional[torch.Tensor] = None, rows_per_group: int = 1) -> torch.Tensor:
+                gate: Optional[torch.Tensor] = None, rows_per_group: int = 1,
+                T: Optional[torch.Tensor] = None) -> torch.Tensor:
         """epi (optional): an elementwise op on the output, fused into the GEMM epilogue on the
         population path (kernels.lora_linear_pop_epi): "res" -> res + y, "gated" -> res + gate[g] * y,
-        both written into `res` in place and returned."""
+        both written into `res` in place and returned.  T (optional, population path): this linear's
+        X A_k^T already computed by shared_projection — only the GEMM + LoRA epilogue run here."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if x2.dtype != torch.bfloat16:
@@ -166,7 +174,10 @@ class LoRALinear(nn.Module):
                 raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")
             rpm = M // ctx.n_members
             ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device)
-            if GemmTimer.active:  # the same two kernels as lora_linear_pop's unfused path, timed apart
+            if T is not None:     # projection already done for the linears sharing this input
+                y = K.lora_gemm(x2, self.weight, self.bias, T, ctx.theta_pop, self.theta_off_B, self.r, self.scale,
+                                rpm)
+            elif GemmTimer.active:  # the same two kernels as lora_linear_pop's unfused path, timed apart
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 T = ws[: M * self.r].view(M, self.r)
                 ev[0].record()
@@ -191,6 +202,35 @@ class LoRALinear(nn.Module):
         else:
             y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
         return y.view(*shp[:-1], self.out_features)
+
+
+# Linears that read the same input (Sana attn1 to_q / to_k / to_v, attn2 to_k / to_v) get their LoRA
+# projections T_l = X A_{k,l}^T from ONE pass over X (kernels.lora_project_multi) instead of one pass
+# per linear; False restores the per-linear projection (A/B measurement).
+SHARED_PROJECTION = True
+
+
+def shared_projection(mods: Sequence[LoRALinear], x: torch.Tensor) -> List[Optional[torch.Tensor]]:
+    """[T_l] for mods on input x (population path), or [None] * len(mods) where it does not apply
+    (single-member mode, LoRA off, GemmTimer's per-kernel timing, unsupported shapes)."""
+    none = [None] * len(mods)
+    ctx = mods[0].ctx if mods else None
+    if (not SHARED_PROJECTION or GemmTimer.active or ctx is None or ctx.theta_pop is None or len(mods) < 2
+            or any(m.ctx is not ctx for m in mods)):
+        return none
+    r, Kd = mods[0].r, mods[0].in_features
+    if (r == 0 or any(m.r != r or m.in_features != Kd for m in mods) or len(mods) * r > 8 or len(mods) > 4
+            or Kd % 32 or Kd > 4096):
+        return none
+    x2 = x.reshape(-1, Kd)
+    if x2.dtype != torch.bfloat16 or not x2.is_contiguous():
+        return none
+    M = x2.shape[0]
+    if M % ctx.n_members:
+        raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")
+    ws = ctx.multi_workspace(len(mods) * M * r, x2.device).view(len(mods), M, r)
+    K.lora_project_multi(x2, ctx.theta_pop, [m.theta_off_A for m in mods], r, M // ctx.n_members, out=ws)
+    return [ws[i] for i in range(len(mods))]
 
 
 def lora_modules(model: nn.Module) -> List[LoRALinear]:

@@ -130,9 +130,10 @@ class LinearSelfAttention(nn.Module):
         """With res / gate: returns res += gate[image] * attn1(x), the gated residual fused into
         to_out's GEMM epilogue (the block's `x + gate_msa * attn_output`)."""
         B, N, D = x.shape
-        q = self.norm_q(self.to_q(x), act="relu").view(B * N, -1)   # RMS norm + ReLU fused
-        k = self.norm_k(self.to_k(x), act="relu").view(B * N, -1)
-        v = self.to_v(x).view(B * N, -1)
+        Tq, Tk, Tv = lora.shared_projection([self.to_q, self.to_k, self.to_v], x)   # X read once for 3 LoRAs
+        q = self.norm_q(self.to_q(x, T=Tq), act="relu").view(B * N, -1)   # RMS norm + ReLU fused
+        k = self.norm_k(self.to_k(x, T=Tk), act="relu").view(B * N, -1)
+        v = self.to_v(x, T=Tv).view(B * N, -1)
         o = K.linear_attention(q, k, v, B, N, self.heads, self.head_dim, relu_qk=False)
         if res is not None:
             return self.to_out[0](o.view(B, N, -1), epi="gated", res=res, gate=gate, rows_per_group=N)
@@ -166,8 +167,9 @@ class CrossAttention(nn.Module):
         hd = self.head_dim
         if self.use_kernel and hd == 112 and L <= 320:
             q = self.norm_q(self.to_q(x)).view(B * N, -1)
-            k = self.norm_k(self.to_k(enc)).view(U * L, -1)
-            v = self.to_v(enc).view(U * L, -1)
+            Tk, Tv = lora.shared_projection([self.to_k, self.to_v], enc)
+            k = self.norm_k(self.to_k(enc, T=Tk)).view(U * L, -1)
+            v = self.to_v(enc, T=Tv).view(U * L, -1)
             o = K.cross_attention(q, k, v, B, N, self.heads, hd, L, hd ** -0.5, bias=mask_bias.contiguous(),
                                   enc_index=enc_index).view(B, N, -1)
             if res is not None:   # res += to_out(o): the block's residual add fused into the GEMM epilogue

@@ -193,6 +193,16 @@ int eggroll_lora_linear_pop_sel(const void* X, int64_t ldx, const void* W, int64
 int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
                          int64_t offA, int32_t r, int64_t rows_per_member, int64_t M, int64_t K,
                          float* T, void* stream);
+/* T = X A^T for n_lin LoRA linears that read the same X (Sana attn1 to_q/to_k/to_v, attn2 to_k/to_v:
+ * the PEFT lora_A products of es_backend.py:193-200 sharing one input), X read from HBM once:
+ *   T[l*M*r + row*r + q] = sum_k X[row,k] * A_{k,l}[q,k],  A_{k,l} = theta_pop[kl*ld_theta + offA_host[l]]
+ * as [r][K] (kl = row / rows_per_member).  MFMA with A split into bf16 hi + lo (|error| <= ~2^-16
+ * relative per product, fp32 accumulation), so T agrees with eggroll_lora_project to fp32 rounding,
+ * not bit for bit.  offA_host: HOST array of n_lin offsets (multiples of 4).  1 <= n_lin <= 4,
+ * n_lin * r <= 8, K % 32 == 0, K <= 4096, ldx % 8 == 0.                                        */
+int eggroll_lora_project_multi(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
+                               const int64_t* offA_host, int32_t n_lin, int32_t r, int64_t rows_per_member,
+                               int64_t M, int64_t K, float* T, void* stream);
 int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
                         int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
                         void* Y, int64_t ldy, void* stream);
@@ -312,11 +322,13 @@ int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, int64_t W, in
 /* Softmax cross-attention over a short key sequence (Sana attn2: diffusers SanaAttnProcessor2_0,
  * F.scaled_dot_product_attention with the caption mask as an additive bias):
  *   o[b,n,h,:] = softmax_j(scale * q[b,n,h,:] . k[u,j,h,:] + bias[u,j]) @ v[u,:,h,:],  u = enc_index[b]
- * q / o bf16 rows b*N + n (head h at columns h*head_dim), k / v bf16 rows u*L + j; bias bf16 [U][L]
- * or NULL; enc_index int32 [B] or NULL (u = b).  head_dim 112, L <= 320; MFMA, fp32 softmax.        */
+ * q / o bf16 rows b*N + n (head h at columns h*head_dim), k / v bf16 rows u*L + j (U caption rows); bias
+ * bf16 [U][L] or NULL; enc_index int32 [B] or NULL (u = b, needs U >= B).  An enc_index entry outside
+ * [0, U) gives that image NaN output (no out-of-bounds read).  head_dim 64 / 80 / 112 (112: Sana attn2;
+ * 64 / 80: the CLIP towers' self-attention), L <= 320; MFMA, fp32 softmax.                           */
 int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, const void* bias,
                             const int32_t* enc_index, int64_t B, int64_t N, int64_t heads, int64_t head_dim,
-                            int64_t L, float scale, void* o, int64_t ldo, void* stream);
+                            int64_t L, int64_t U, float scale, void* o, int64_t ldo, void* stream);
 
 #ifdef __cplusplus
 }

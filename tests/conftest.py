@@ -17,6 +17,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (ROCm device); runs the HIP kernels")
 
 
+def pytest_sessionstart(session):
+    """Refuse to test a stale prebuilt libeggroll.so: its source stamp (written by build_ext) must equal
+    the digest of csrc/* + include/eggroll.h in this tree (content, not mtime — snapshots copied to a
+    GPU box keep bytes, not timestamps)."""
+    from hyperscalees_t2i_amd import _lib
+    if _lib.LIB_PATH.exists() and not os.environ.get("EGGROLL_LIB"):
+        try:
+            _lib.check_fresh()
+        except _lib.EggrollError as e:
+            pytest.exit(f"libeggroll.so is stale: {e}", returncode=3)
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

@@ -103,3 +103,100 @@ def test_factor_pack_roundtrip():
     p = lay.pack_factors(x)
     assert p.shape == (3, lay.factor_ld) and np.array_equal(lay.unpack_factors(p), x)
     assert lay.factor_len_packed == 2 * (2 + 7) + 2 * (5 + 2) + 3 + 2 * 2
+
+
+# --------------------------------------------------------------------------------------------
+# The documented binding == _lib.SIGNATURES == the header's prototypes
+# --------------------------------------------------------------------------------------------
+import re  # noqa: E402
+from pathlib import Path  # noqa: E402
+
+_CT = {"vp": C.c_void_p, "i32": C.c_int32, "i64": C.c_int64, "u32": C.c_uint32, "u64": C.c_uint64,
+       "f32": C.c_float, "C.c_char_p": C.c_char_p}
+
+
+def _norm(t):
+    """ctypes type -> comparable token (c_int is c_int32 on this ABI)."""
+    return {C.c_int: "i32", C.c_int32: "i32", C.c_int64: "i64", C.c_uint32: "u32", C.c_uint64: "u64",
+            C.c_float: "f32", C.c_void_p: "vp", C.c_char_p: "str"}[t]
+
+
+def header_prototypes():
+    """{name: (ret, [arg tokens])} parsed from include/eggroll.h (pointers -> vp)."""
+    txt = re.sub(r"/\*.*?\*/", "", _lib.HEADER.read_text(), flags=re.S)
+    out = {}
+    for ret, name, args in re.findall(r"(const char\s*\*|int64_t|int)\s+(eggroll_\w+)\s*\(([^;]*?)\)\s*;", txt):
+        toks = []
+        for a in [a.strip() for a in args.split(",") if a.strip() and a.strip() != "void"]:
+            if "*" in a:
+                toks.append("vp")
+            else:
+                base = a.replace("const ", "").split()[0]
+                toks.append({"int64_t": "i64", "int32_t": "i32", "uint64_t": "u64", "uint32_t": "u32",
+                             "float": "f32", "int": "i32"}[base])
+        out[name] = ({"int": "i32", "int64_t": "i64"}.get(ret, "str"), toks)
+    return out
+
+
+def integration_blocks():
+    md = (Path(__file__).resolve().parent.parent / "INTEGRATION.md").read_text()
+    return re.findall(r"```python\n(.*?)```", md, flags=re.S)
+
+
+def test_signatures_match_header_prototypes():
+    proto = header_prototypes()
+    assert set(proto) == set(_lib.SIGNATURES)
+    for name, (res, args) in _lib.SIGNATURES.items():
+        assert proto[name] == (_norm(res), [_norm(a) for a in args]), name
+
+
+def test_integration_stub_matches_header():
+    stub = integration_blocks()[0]
+    got = {}
+    for name, res, args in re.findall(r"lib\.(eggroll_\w+)\.restype, lib\.\1\.argtypes = ([\w.]+), \[([^\]]*)\]", stub):
+        got[name] = (_norm(_CT[res]), [_norm(_CT[a.strip()]) for a in args.split(",") if a.strip()])
+    assert set(got) == set(_lib.SIGNATURES), "INTEGRATION.md stub drifts from the library's exports"
+    for name, (res, args) in _lib.SIGNATURES.items():
+        assert got[name] == (_norm(res), [_norm(a) for a in args]), name
+
+
+def test_integration_stub_binds_the_library():
+    """The stub's bind() runs against the built library, and its theta_records / tile_table helpers
+    reproduce the package's own layout and tile table."""
+    ns = {}
+    exec(integration_blocks()[0], ns)
+    lib = ns["bind"](str(_lib.LIB_PATH))
+    assert lib.eggroll_version().decode().startswith("eggroll-mi355x")
+    shapes = [(2, 2240), (2240, 2), (6,), (2, 30), (13440, 2), (3, 5)]
+    for r in (1, 2, 4):
+        mats, D, flen = ns["theta_records"](shapes, r)
+        lay = ThetaLayout(shapes, r)
+        assert np.array_equal(mats, lay.mats) and D == lay.D and flen == lay.factor_len
+        assert np.array_equal(ns["tile_table"](lib, mats, r), lay.tile_table())
+
+
+def test_tile_table_rejects_oversized_generic_matrix():
+    """The generic per-element path indexes in 32-bit ints: a T_GEN matrix of >= 2^31 elements is an
+    argument error, not a silent overflow (fast-path tiles have no such limit)."""
+    lib = _lib.load()
+    big = np.array([[3, 1 << 30, 0, 0, 0, 0]], dtype=np.int64)        # rank 3: generic tiles, 3 * 2^30 elements
+    assert lib.eggroll_tile_table(big.ctypes.data, 1, 3, None, 0) == -1
+    assert b"too large" in lib.eggroll_last_error()
+    ok = np.array([[2, 1 << 30, 0, 0, 0, 0]], dtype=np.int64)         # lora_A-shaped, rank 1: wide tiles
+    assert lib.eggroll_tile_table(ok.ctypes.data, 1, 1, None, 0) == (1 << 30) // 1024
+
+
+def test_stale_library_is_refused(tmp_path):
+    """_lib.check_fresh: a library whose source stamp is missing or differs from today's sources is
+    refused (what conftest and _lib.load() run before any test touches it)."""
+    import shutil
+    lib = tmp_path / "libeggroll.so"
+    shutil.copy(_lib.LIB_PATH, lib)
+    with pytest.raises(_lib.EggrollError, match="no source stamp"):
+        _lib.check_fresh(lib)
+    (tmp_path / "libeggroll.so.srcsha256").write_text("0" * 64 + "\n")
+    with pytest.raises(_lib.EggrollError, match="stale"):
+        _lib.check_fresh(lib)
+    (tmp_path / "libeggroll.so.srcsha256").write_text(_lib.source_digest() + "\n")
+    _lib.check_fresh(lib)
+    _lib.check_fresh()                       # the in-tree library is current

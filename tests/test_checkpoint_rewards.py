@@ -144,3 +144,32 @@ def test_clip_vision_tower_matches_transformers(dev, which):
     cos = float(torch.nn.functional.cosine_similarity(ours, ref, dim=-1).min())
     print(f"[clip tower {which}] rel {rel:.2e} min cos {cos:.6f}")
     assert rel < 2e-2 and cos > 0.9995
+
+
+def test_var_checkpoint_roundtrip(tmp_path):
+    """VarBackend save_lora / load_lora (shared adapter helpers) on CPU at a tiny VAR: the adapter holds
+    every theta entry in parameter order — the mat_qkv LoRA entries the reference's F.linear bypasses
+    included — and resume restores theta exactly."""
+    from safetensors.torch import load_file
+    from hyperscalees_t2i_amd.backend import VarBackend, VarConfig
+    from hyperscalees_t2i_amd.var import VARArch
+    be = VarBackend("cpu", VarConfig(arch=VARArch(depth=2, vae_ch=32), ckpt_dir="/nonexistent"))
+    be.init_and_attach_lora()
+    params, shapes = be.collect_lora_params()
+    theta = torch.randn(sum(p.numel() for p in params), generator=torch.Generator().manual_seed(5))
+    save_latest_checkpoint(theta=theta, backend=be, lora_params=params, lora_shapes=shapes,
+                           save_dir=tmp_path / "var_lora", meta_path=tmp_path / "var_meta.pt", epoch=2, stats={},
+                           extra_meta={})
+    ad = load_file(str(tmp_path / "var_lora" / "adapter_model.safetensors"))
+    names = [n for n, p in be.es_model.transformer.named_parameters() if p.requires_grad]
+    assert any(".mat_qkv.lora_A" in n for n in names)
+    assert torch.equal(torch.cat([ad[f"base_model.model.{n}"].reshape(-1) for n in names]), theta)
+    cfg = json.loads((tmp_path / "var_lora" / "adapter_config.json").read_text())
+    assert cfg["r"] == 4 and cfg["lora_alpha"] == 16
+    with torch.no_grad():
+        for p in params:
+            p.zero_()
+    be.load_lora(tmp_path / "var_lora")
+    assert torch.equal(flatten_params(params), theta)
+    th, meta = load_latest_checkpoint(tmp_path / "var_meta.pt")
+    assert torch.equal(th, theta) and meta["backend"] == be.name

@@ -775,3 +775,113 @@ def test_cross_attention_vs_sdpa(dev, B, N, H, L, U):
     rel = float((ours - ref).norm() / ref.norm())
     assert rel < 1e-2, rel     # bf16 P (probabilities rounded before the PV MFMA) + bf16 output
     assert float((ours - ref).abs().max()) < 3e-2 * float(ref.abs().max())
+
+
+def test_cross_attention_out_of_range_caption_is_nan_not_oob(dev):
+    """A device-resident enc_index entry outside [0, U) poisons that image (NaN) without reading past
+    k / v; the other images are unaffected.  Host-side checks reject bad shapes and CPU indices."""
+    hd, B, N, H, L, U = 112, 3, 16, 2, 40, 2
+    g = torch.Generator(device=dev).manual_seed(3)
+    q = torch.randn((B * N, H * hd), generator=g, device=dev).to(torch.bfloat16)
+    k = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
+    v = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
+    good = K.cross_attention(q, k, v, B, N, H, hd, L, 0.1, enc_index=torch.tensor([0, 1, 1], device=dev)).float()
+    bad = K.cross_attention(q, k, v, B, N, H, hd, L, 0.1, enc_index=torch.tensor([0, 7, 1], device=dev)).float()
+    torch.cuda.synchronize()
+    assert torch.isnan(bad[N:2 * N]).all()
+    assert torch.equal(bad[:N], good[:N]) and torch.equal(bad[2 * N:], good[2 * N:])
+    with pytest.raises(ValueError):
+        K.cross_attention(q, k, v, B, N, H, hd, L, 0.1, enc_index=torch.tensor([0, 2, 1]))     # CPU, out of range
+    with pytest.raises(ValueError):
+        K.cross_attention(q, k, v, B, N, H, hd, L, 0.1)                                        # U < B, no index
+    with pytest.raises(ValueError):
+        K.cross_attention(q, k, v, B, N, H, hd, L, 0.1, bias=torch.zeros((U, L + 1), device=dev, dtype=torch.bfloat16),
+                          enc_index=torch.tensor([0, 1, 1], device=dev))
+
+
+@pytest.mark.parametrize("M,Kd,r,n_lin,rpm", [
+    (4096, 2240, 2, 3, 1024),   # Sana attn1 q/k/v: K % 128 = 64 tail, members block-aligned
+    (1000, 2240, 2, 2, 300),    # attn2 k/v-like: ragged M, members straddling blocks
+    (777, 128, 1, 1, 100),      # one linear, rows_per_member not a multiple of 16
+    (530, 96, 4, 2, 530),       # K < 128 (tail only), NQ = 8
+    (2048, 512, 1, 4, 512),     # 4 linears, NQ = 4
+    (300, 160, 3, 1, 17),       # r = 3, tiny members
+])
+def test_lora_project_multi_vs_fp64_and_single(dev, M, Kd, r, n_lin, rpm):
+    """eggroll_lora_project_multi (MFMA, A as bf16 hi + lo) vs fp64 X A^T and vs the per-linear VALU
+    projection: both within the hi/lo split's 2^-16 relative error of sum |x| |a| per output."""
+    g = torch.Generator().manual_seed(M + Kd)
+    x = _bf(torch.randn(M, Kd, generator=g)).to(dev)
+    nm = -(-M // rpm)
+    offs = [8 + l * (r * Kd + 12) for l in range(n_lin)]
+    ld = -(-(offs[-1] + r * Kd + 4) // 4) * 4
+    tp = (torch.randn(nm, ld, generator=g) * 0.05).to(dev)
+    T = K.lora_project_multi(x, tp, offs, r, rpm)
+    torch.cuda.synchronize()
+    xs = x.double().cpu()
+    tps = tp.double().cpu()
+    member = torch.arange(M) // rpm
+    for l, off in enumerate(offs):
+        A = tps[:, off:off + r * Kd].view(nm, r, Kd)[member]                    # [M, r, K]
+        ref = torch.einsum("mk,mqk->mq", xs, A)
+        bound = torch.einsum("mk,mqk->mq", xs.abs(), A.abs()) * 2 ** -15 + 1e-6
+        got = T[l].double().cpu()
+        assert ((got - ref).abs() <= bound).all(), float(((got - ref).abs() / bound).max())
+        if r in (1, 2, 3, 4):
+            single = K.lora_project(x, tp, off, r, rpm).double().cpu()
+            assert ((got - single).abs() <= 2 * bound).all()
+
+
+def test_lora_project_multi_rejects_bad_args(dev):
+    x = torch.zeros((64, 100), dtype=torch.bfloat16, device=dev)
+    tp = torch.zeros((1, 1024), device=dev)
+    with pytest.raises(K._lib.EggrollError, match="K % 32"):
+        K.lora_project_multi(x, tp, [0], 1, 64)                     # K = 100
+    x = torch.zeros((64, 128), dtype=torch.bfloat16, device=dev)
+    with pytest.raises(K._lib.EggrollError, match="n_lin"):
+        K.lora_project_multi(x, tp, [0, 256, 512], 3, 64)           # n_lin * r = 9
+    with pytest.raises(K._lib.EggrollError, match="aligned"):
+        K.lora_project_multi(x, tp, [2], 1, 64)
+
+
+def _integration_blocks():
+    import re
+    from pathlib import Path
+    md = (Path(__file__).resolve().parent.parent / "INTEGRATION.md").read_text()
+    return re.findall(r"```python\n(.*?)```", md, flags=re.S)
+
+
+@pytest.mark.parametrize("pop,r,caps", [(8, 1, (0.0, 40.0)), (7, 2, (0.5, 1.0))])
+def test_integration_example_runs(dev, pop, r, caps):
+    """INTEGRATION.md's ctypes stub + epoch-tail example, executed as documented against the built
+    library: theta' equals the package path's (same kernels, bit for bit) and the oracle's epoch tail
+    (reference formula on the same factors) within the update's fp32 tolerance."""
+    ns = {}
+    for blk in _integration_blocks()[:2]:
+        exec(blk, ns)
+    lib = ns["bind"](str(K._lib.LIB_PATH))
+    shapes = [(2, 40), (40, 2), (6,), (2, 12), (33, 2)]
+    lay = K.ThetaLayout(shapes, r)
+    g = torch.Generator().manual_seed(pop)
+    theta = (torch.randn(lay.D, generator=g) * 0.3).to(dev)
+    S = torch.randn(pop, 4, generator=g).to(dev)
+    max_step, max_theta = caps
+    out, theta_pop, factors, fit, order = ns["es_epoch_tail"](lib, shapes, theta, S, epoch=5, pop=pop, r=r,
+                                                              sigma=0.01, lr_scale=0.1, theta_max_norm=max_theta,
+                                                              max_step_norm=max_step)
+    # the package path on the same inputs
+    f_pkg = K.noise_factors(5, K.n_base_samples(pop, True), lay, dev)
+    fit_pkg = K.fitness(S, True)
+    out_pkg = K.update(theta, f_pkg, fit_pkg, lay, pop, True, 0.1 * 0.01, max_step, max_theta)
+    pop_pkg = K.perturb(theta, f_pkg, lay, pop, True, 0, pop, 0.01)
+    torch.cuda.synchronize()
+    assert torch.equal(factors[:, :lay.factor_len], f_pkg[:, :lay.factor_len])
+    assert torch.equal(out, out_pkg) and torch.equal(theta_pop, pop_pkg)
+    assert torch.equal(order, fit_pkg["order"])
+    # the oracle's epoch tail on eps rows built from the same factors
+    fac = lay.unpack_factors(factors.cpu().numpy())
+    eps = O.dev_eps_rows(fac, shapes, pop, r, True, 0, pop)
+    ref, info = O.ref_es_tail(S.cpu().numpy(), eps, theta.cpu().numpy(), promptnorm=True, lr_scale=0.1, sigma=0.01,
+                              max_step_norm=max_step, theta_max_norm=max_theta)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-7)
+    assert np.array_equal(order.cpu().numpy(), info["order"])
