@@ -245,6 +245,18 @@ def main():
     aux64 = None
     if pop != 64 and not args.small and args.workload == "sana":
         aux64 = aux_kernel_rooflines(noiser.layout, 64, 0, args.pop_per_gpu, device, theta=theta)
+    # the same ES kernels at one GPU's share of the other node-level configs' theta layouts:
+    # configs[3] Z-Image-Turbo (egg rank 4, pop 128 over 8 GPUs: the larger rank-(N*r) update) and
+    # configs[4] Infinity-8B (pop 32 over 8 GPUs); the model hosts themselves are out of scope
+    aux_cfg = None
+    if not args.small and args.workload == "sana":
+        from hyperscalees_t2i_amd.kernels import ThetaLayout
+        from hyperscalees_t2i_amd.model_shapes import infinity_lora_shapes, zimage_turbo_lora_shapes
+        aux_cfg = {
+            "configs3_zimage_turbo_r4_pop128": aux_kernel_rooflines(ThetaLayout(zimage_turbo_lora_shapes(), 4), 128, 0,
+                                                                    16, device),
+            "configs4_infinity_8b_pop32": aux_kernel_rooflines(ThetaLayout(infinity_lora_shapes(), 1), 32, 0, 4,
+                                                               device)}
 
     value = pop * args.steps / elapsed
     variants = {k: v for k, v in gemm.items() if k != "all" and "tflops" in v}
@@ -309,6 +321,7 @@ def main():
             "phases_ms": phases,
             "aux_kernels": aux,
             "aux_kernels_pop64_per_gpu": aux64,
+            "aux_kernels_other_configs_per_gpu": aux_cfg,
             "model_kernels": model_kernels,
         }
         print(json.dumps(line), flush=True)

@@ -9,7 +9,13 @@ projection), restated for throughput on every image of every local member at onc
   * the LAST layer runs its attention output, MLP and residuals on the [CLS] rows only — the only
     rows get_image_features reads (its keys / values still come from every token);
   * one batch for all images (no per-image or per-chunk model calls).
-Numerics follow the module in bf16 (the towers are built in bf16, rewards.py:150-155).
+Precision (`fp32_residual`, default on): GEMM operands are bf16 (MFMA) with fp32 accumulation,
+but everything that carries the signal from layer to layer is fp32 — the patch embedding, the
+residual stream h, every LayerNorm (fp32 in, bf16 out for the next GEMM), each block's output added
+to h in fp32, the post-LN and the projection.  The reference runs these towers in fp32
+(rewards.py:32-60, from_pretrained defaults); a bf16 residual stream rounds h 64 times per CLIP-H
+image and was the largest single term of the member-eval S drift.  fp32_residual=False
+is the plain bf16 module (kept for A/B).
 """
 from __future__ import annotations
 
@@ -23,9 +29,10 @@ ACT = {"gelu": lambda x: F.gelu(x), "quick_gelu": lambda x: x * torch.sigmoid(1.
 
 
 class CLIPVisionTower:
-    def __init__(self, model, pad_head_dim: bool = False, use_kernel: bool = True):
+    def __init__(self, model, pad_head_dim: bool = False, use_kernel: bool = True, fp32_residual: bool = True):
         vm = model.vision_model
         self.pad_head_dim = pad_head_dim
+        self.fp32_residual = fp32_residual
         self.use_kernel = use_kernel   # libeggroll's MFMA attention (eggroll_cross_attention, k = v = own tokens)
         cfg = model.config.vision_config
         self.C, self.heads = cfg.hidden_size, cfg.num_attention_heads
@@ -39,6 +46,9 @@ class CLIPVisionTower:
         self.pre = vm.pre_layrnorm
         self.post = vm.post_layernorm
         self.proj = model.visual_projection.weight.detach()
+        if fp32_residual:   # fp32 copies of the small tensors that act on the fp32 stream
+            f = lambda t: t.detach().float()  # noqa: E731
+            self.patch_w32, self.cls32, self.pos32, self.proj32 = f(self.patch_w), f(self.cls), f(self.pos), f(self.proj)
         self.layers: List[dict] = []
         for L in vm.encoder.layers:
             a = L.self_attn
@@ -54,9 +64,59 @@ class CLIPVisionTower:
     def _ln(mod, x):
         return F.layer_norm(x, mod.normalized_shape, mod.weight, mod.bias, mod.eps)
 
+    @staticmethod
+    def _ln32(mod, x, out_dtype):
+        """LayerNorm of the fp32 stream in fp32 (the module's bf16 affine upcast), rounded once to the
+        GEMM operand dtype."""
+        w = None if mod.weight is None else mod.weight.float()
+        b = None if mod.bias is None else mod.bias.float()
+        return F.layer_norm(x, mod.normalized_shape, w, b, mod.eps).to(out_dtype)
+
+    @torch.no_grad()
+    def _forward32(self, pixels: torch.Tensor) -> torch.Tensor:
+        n = pixels.shape[0]
+        p, C, H, hd = self.patch, self.C, self.heads, self.hd
+        dt = self.patch_w.dtype
+        x = pixels.float()
+        g = x.shape[-1] // p
+        cols = x.view(n, 3, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(n, g * g, 3 * p * p)
+        P = cols.shape[1]
+        T = P + 1
+        h = torch.empty((n, T, C), dtype=torch.float32, device=x.device)
+        h[:, 0] = self.cls32
+        h[:, 1:] = cols @ self.patch_w32.t()
+        h += self.pos32[None, :T]
+        h = F.layer_norm(h, self.pre.normalized_shape, self.pre.weight.float(), self.pre.bias.float(), self.pre.eps)
+        kernel = self.use_kernel and hd in (64, 80, 112) and T <= 320
+        from . import kernels as K
+        last = len(self.layers) - 1
+        for i, L in enumerate(self.layers):
+            y = self._ln32(L["ln1"], h, dt)
+            last_i = i == last
+            if kernel:
+                qkv = F.linear(y, L["wqkv"], L["bqkv"]).view(n * T, 3 * C)
+                qv = qkv[::T] if last_i else qkv
+                o = K.cross_attention(qv, qkv[:, C:], qkv[:, 2 * C:], n, 1 if last_i else T, H, hd, T, L["scale"])
+                o = o.view(n, -1, C)
+            else:
+                qkv = F.linear(y, L["wqkv"], L["bqkv"]).view(n, T, 3, H, hd)
+                k, v = qkv[:, :, 1].transpose(1, 2), qkv[:, :, 2].transpose(1, 2)
+                q = (qkv[:, :1, 0] if last_i else qkv[:, :, 0]).transpose(1, 2)
+                o = F.scaled_dot_product_attention(q, k, v, scale=L["scale"]).transpose(1, 2).reshape(n, -1, C)
+            if last_i:       # only the [CLS] row is read by get_image_features
+                h = h[:, :1]
+            h = h + F.linear(o, L["wo"], L["bo"]).float()
+            y = self._ln32(L["ln2"], h, dt)
+            h = h + F.linear(self.act(F.linear(y, L["w1"], L["b1"])), L["w2"], L["b2"]).float()
+        pooled = F.layer_norm(h[:, 0], self.post.normalized_shape, self.post.weight.float(), self.post.bias.float(),
+                              self.post.eps)
+        return pooled @ self.proj32.t()
+
     @torch.no_grad()
     def __call__(self, pixels: torch.Tensor) -> torch.Tensor:
         """pixels [n, 3, S, S] (normalised fp32) -> projected image embeddings [n, proj] fp32."""
+        if self.fp32_residual:
+            return self._forward32(pixels)
         n = pixels.shape[0]
         p, C, H, hd = self.patch, self.C, self.heads, self.hd
         x = pixels.to(self.patch_w.dtype)

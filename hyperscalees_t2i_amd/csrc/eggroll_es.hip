@@ -39,23 +39,38 @@ __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float& z0, 
     z1 = rr * __builtin_amdgcn_sinf(u2);
 }
 
+// One thread = NOISE_QPT quads (16-byte stores) of one base sample, 256 quads apart so every store
+// instruction of a wave is one contiguous KiB; the NOISE_QPT independent Philox chains interleave
+// (ILP) and a quarter as many workgroups are dispatched as with one quad per thread.
+constexpr int NOISE_QPT = 4;
+
 __global__ __launch_bounds__(256) void k_noise(uint32_t k0, uint32_t k1, int64_t base_lo,
                                                int64_t factor_len, int64_t ld, float* __restrict__ out) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t g0 = q * 4;
-    if (g0 >= factor_len) return;
+    const int64_t quads = (factor_len + 3) / 4;
+    const int64_t qb = (int64_t)blockIdx.x * (256 * NOISE_QPT) + threadIdx.x;
     const int64_t j = base_lo + blockIdx.y;
-    u32x4 c{(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)j, kNoiseTag};
-    const u32x4 w = philox4x32_10_dev(c, k0, k1);
-    float4 v;
-    box_muller(w.x, w.y, v.x, v.y);
-    box_muller(w.z, w.w, v.z, v.w);
-    float* dst = out + (int64_t)blockIdx.y * ld + g0;
-    if (g0 + 4 <= factor_len) {
-        *reinterpret_cast<float4*>(dst) = v;
-    } else {
-        const float t[4] = {v.x, v.y, v.z, v.w};
-        for (int i = 0; i < 4 && g0 + i < factor_len; ++i) dst[i] = t[i];
+    float* row = out + (int64_t)blockIdx.y * ld;
+    float4 v[NOISE_QPT];
+#pragma unroll
+    for (int u = 0; u < NOISE_QPT; ++u) {
+        const int64_t q = qb + u * 256;
+        u32x4 c{(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)j, kNoiseTag};
+        const u32x4 w = philox4x32_10_dev(c, k0, k1);
+        box_muller(w.x, w.y, v[u].x, v[u].y);
+        box_muller(w.z, w.w, v[u].z, v[u].w);
+    }
+#pragma unroll
+    for (int u = 0; u < NOISE_QPT; ++u) {
+        const int64_t q = qb + u * 256;
+        if (q >= quads) break;
+        const int64_t g0 = q * 4;
+        float* dst = row + g0;
+        if (g0 + 4 <= factor_len) {
+            *reinterpret_cast<float4*>(dst) = v[u];
+        } else {
+            const float t[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            for (int i = 0; i < 4 && g0 + i < factor_len; ++i) dst[i] = t[i];
+        }
     }
 }
 
@@ -811,7 +826,7 @@ int eggroll_noise_factors(uint64_t seed, int64_t base_lo, int64_t base_hi, int64
     if (base_hi == base_lo || factor_len == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(out != nullptr, "noise_factors: out is NULL");
     const int64_t quads = (factor_len + 3) / 4;
-    dim3 grid((unsigned)((quads + 255) / 256), (unsigned)(base_hi - base_lo));
+    dim3 grid((unsigned)((quads + 256 * NOISE_QPT - 1) / (256 * NOISE_QPT)), (unsigned)(base_hi - base_lo));
     hipLaunchKernelGGL(k_noise, grid, dim3(256), 0, as_stream(stream), (uint32_t)seed, (uint32_t)(seed >> 32),
                        base_lo, factor_len, ld, out);
     EGG_CHECK_LAUNCH("noise_factors");
@@ -904,8 +919,10 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
                        n_base, fitness, stats, pop, antithetic, mats, tiles, rank, sqrt_r, lr, theta_out, partials);
     EGG_CHECK_LAUNCH("update");
     if (caps) {
+        // every block re-reduces all per-tile partials (fixed order) before deciding, so the decision
+        // costs blocks x n_tiles x 32 B of L2 reads; 64 blocks still rescale D in one sweep if a cap fires
         int64_t blocks = (D + 1023) / 1024;
-        if (blocks > 256) blocks = 256;
+        if (blocks > 64) blocks = 64;
         hipLaunchKernelGGL(k_update_caps, dim3((unsigned)blocks), dim3(256), 0, st, theta, D, partials, n_tiles, stats,
                            max_step_norm, theta_max_norm, sc, theta_out);
         EGG_CHECK_LAUNCH("update_caps");

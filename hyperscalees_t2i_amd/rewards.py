@@ -214,6 +214,13 @@ def _text_features(model, ids: torch.Tensor, mask: torch.Tensor) -> torch.Tensor
     return model.text_projection(out.pooler_output).float()
 
 
+@dataclass
+class _TextOnly:
+    """text_model + text_projection of a CLIPModel (what _text_features reads)."""
+    text_model: object
+    text_projection: object
+
+
 def split_mix_weights(mix_weights) -> Tuple[float, float, float, float]:
     """rewards.py:247-253: (w_aes, w_align, w_noart) with w_pick = 0, or all four; else ValueError."""
     w = tuple(float(x) for x in mix_weights)
@@ -230,13 +237,28 @@ class RewardModels:
     pick: object
     mix_weights: Tuple[float, ...] = (0.0, 0.0, 0.0, 1.0)  # unifed_es.py:360-363 defaults (length 3 or 4)
     image_batch: int = 256
+    fp32_residual: bool = True     # towers carry their residual stream / norms in fp32 (clip_tower.py)
     _towers: Optional[tuple] = None
+    _text32: Optional[tuple] = None
 
     def towers(self):
-        if self._towers is None:
+        if self._towers is None or self._towers[0].fp32_residual != self.fp32_residual:
             from .clip_tower import CLIPVisionTower
-            self._towers = (CLIPVisionTower(self.clip), CLIPVisionTower(self.pick))
+            self._towers = (CLIPVisionTower(self.clip, fp32_residual=self.fp32_residual),
+                            CLIPVisionTower(self.pick, fp32_residual=self.fp32_residual))
         return self._towers
+
+    def text_models(self):
+        """The text towers + projections the prompt features come from: fp32 copies (once per epoch
+        for a handful of prompts, so the reference's fp32 precision costs nothing) unless the towers
+        run in plain bf16."""
+        if not self.fp32_residual:
+            return self.clip, self.pick
+        if self._text32 is None:
+            import copy
+            self._text32 = tuple(_TextOnly(copy.deepcopy(m.text_model).float(),
+                                           copy.deepcopy(m.text_projection).float()) for m in (self.clip, self.pick))
+        return self._text32
 
     @classmethod
     def build(cls, device, mix_weights=(0.0, 0.0, 0.0, 1.0), tiny: bool = False, seed: int = 7):
@@ -251,9 +273,10 @@ class RewardModels:
         dev = next(self.clip.parameters()).device
         ids, mask = synthetic_tokenize([AESTHETIC_TEXT, NEGATIVE_TEXT] + list(prompts))
         ids, mask = ids.to(dev), mask.to(dev)
-        t_clip = _text_features(self.clip, ids, mask)
+        tc_model, tp_model = self.text_models()
+        t_clip = _text_features(tc_model, ids, mask)
         t_clip = t_clip / t_clip.norm(dim=-1, keepdim=True).clamp_min(1e-6)   # rewards.py:100
-        t_pick = _text_features(self.pick, ids[2:], mask[2:])
+        t_pick = _text_features(tp_model, ids[2:], mask[2:])
         t_pick = t_pick / t_pick.norm(dim=-1, keepdim=True)                   # rewards.py:153
         return {"clip_aes": t_clip[0], "clip_neg": t_clip[1], "clip_prompt": t_clip[2:], "pick_prompt": t_pick}
 

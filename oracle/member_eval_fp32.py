@@ -242,12 +242,23 @@ def generate_fp32(es_model, theta_k, prompt_embeds, prompt_mask, latents, guidan
     guidance = guidance * es_model.transformer_config.guidance_embeds_scale
     eps = transformer_fp32(es_model.transformer, theta_k, lmi.to(f32), scm, prompt_embeds.to(f32), prompt_mask,
                            guidance.to(f32), record)
-    eps = torch.nan_to_num(eps, nan=0.0, posinf=0.0, neginf=0.0)
+    return eps, decode_fp32(es_model, eps, latents)
+
+
+def decode_fp32(es_model, eps, latents):
+    """models/SanaSprint.py:133-160 after the transformer: nan_to_num, SCM combine (the reference's fp16
+    casts), x0, fp32 DC-AE decode.  Also used on the build's bf16 transformer output to split the image
+    drift into its transformer and DC-AE parts."""
+    sd = es_model.sigma_data
+    lmi = latents / sd
+    se = (torch.sin(torch.tensor(1.571, device=latents.device, dtype=f32))
+          / (torch.cos(torch.tensor(1.571, device=latents.device, dtype=f32))
+             + torch.sin(torch.tensor(1.571, device=latents.device, dtype=f32)))).view(1, 1, 1, 1)
+    eps = torch.nan_to_num(eps.to(f32), nan=0.0, posinf=0.0, neginf=0.0)
     pred = ((1 - 2 * se) * lmi + (1 - 2 * se + 2 * se ** 2) * eps.to(lmi.dtype)) / torch.sqrt(se ** 2 + (1 - se) ** 2)
     pred = pred.float() * sd
     x0 = (0.267 * latents - 0.964 * pred) / sd
-    img = dcae_fp32(es_model.vae, x0.to(f32) / es_model.vae.scaling_factor)
-    return eps, img
+    return dcae_fp32(es_model.vae, x0.to(f32) / es_model.vae.scaling_factor)
 
 
 class Rewards32:

@@ -42,3 +42,17 @@ def test_bench_two_ranks_same_device(tmp_path):
     assert line["value"] > 0 and line["steps"] == 2 and line["warmup"] == 1
     assert line["scaling"] == "weak" and line["cpu_baseline"] is None
     assert "member-shard x2" in line["config"]["parallelism"]
+
+
+def test_rccl_collectives_single_rank(tmp_path):
+    """RCCL itself on the box: a fresh child process inits the "nccl" backend as bench.py does and runs
+    the all-gather / all-reduce / barrier call sites of the N>1 path on CUDA tensors (world size 1)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    out = tmp_path / "rccl.json"
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "rccl_worker.py"), str(out)], env=env, timeout=240,
+                       capture_output=True, text=True, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["backend"] == "nccl" and res["world"] == 1
+    assert res["gather_ok"] and res["checksum_ok"] and res["max_over_ranks"] == 3.25

@@ -2,7 +2,9 @@
 
     python tools/fuse_ab.py [--rounds 4] [--knob fuse|xattn]
 fuse: lora.FUSE_EPILOGUES (GEMM-epilogue fusions); xattn: Sana attn2 on eggroll_cross_attention vs
-SDPA; chunk: DC-AE decode chunk size ("fused" arm = the first of --chunks).  2 timed epochs per arm per round (box-to-box spread is +-3 %, so only same-process interleaved
+SDPA; chunk: DC-AE decode chunk size ("fused" arm = the first of --chunks); sharedproj:
+lora.SHARED_PROJECTION (one X pass for attn1 q/k/v and attn2 k/v LoRA projections); towers32: reward
+towers with the fp32 residual stream vs plain bf16.  2 timed epochs per arm per round (box-to-box spread is +-3 %, so only same-process interleaved
 arms are compared)."""
 import argparse
 import json
@@ -18,7 +20,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=4)
-    ap.add_argument("--knob", choices=("fuse", "xattn", "chunk"), default="fuse")
+    ap.add_argument("--knob", choices=("fuse", "xattn", "chunk", "sharedproj", "towers32"), default="fuse")
     ap.add_argument("--chunks", type=str, default="8,16", help="knob chunk: the two DC-AE decode chunk sizes")
     a = ap.parse_args()
     import bench
@@ -39,6 +41,10 @@ def main():
             backend.es_model.vae_chunk = ca if on else cb
         elif a.knob == "fuse":
             lora.FUSE_EPILOGUES = on
+        elif a.knob == "sharedproj":
+            lora.SHARED_PROJECTION = on
+        elif a.knob == "towers32":
+            engine.rewards.fp32_residual = on
         else:
             for blk in blocks:
                 blk.attn2.use_kernel = on

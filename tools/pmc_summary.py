@@ -11,8 +11,16 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from tools.sana_layers import sana_lora_layers  # noqa: E402
 
-fetch_dir, write_dir = sys.argv[1], sys.argv[2]
-reps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+import argparse  # noqa: E402
+ap = argparse.ArgumentParser()
+ap.add_argument("fetch_dir")
+ap.add_argument("write_dir")
+ap.add_argument("reps", type=int, nargs="?", default=2)
+ap.add_argument("--l2", default="", help="pass with TCC_HIT_sum / TCC_MISS_sum")
+ap.add_argument("--ea", default="", help="pass with TCC_EA0_RDREQ_sum / TCC_EA0_RDREQ_DRAM_sum")
+ap.add_argument("--out", default="profiles/pmc_lora_gemm.json")
+A = ap.parse_args()
+fetch_dir, write_dir, reps = A.fetch_dir, A.write_dir, A.reps
 
 
 def load(d, name):
@@ -41,6 +49,19 @@ out = {"kernel": "k_lora_gemm (population LoRA GEMM)", "launches_profiled": laun
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, "
                  "--kernel-include-regex k_lora_gemm, tools/lora_epoch_driver.py (one epoch's launch mix x2); "
                  "FETCH_SIZE doubled per the gfx950 note"}
+if A.l2:
+    hit, _ = load(A.l2, "TCC_HIT_sum")
+    miss, _ = load(A.l2, "TCC_MISS_sum")
+    out["l2_hit_rate"] = hit / max(hit + miss, 1.0)
+    out["l2_requests_per_launch"] = (hit + miss) / launches
+if A.ea:
+    rd, _ = load(A.ea, "TCC_EA0_RDREQ_sum")
+    dram, _ = load(A.ea, "TCC_EA0_RDREQ_DRAM_sum")
+    out["ea_rdreq_per_launch"] = rd / launches
+    out["ea_rdreq_dram_fraction"] = dram / max(rd, 1.0)
+    out["mall_split_note"] = ("rocprofv3 on gfx950 lists no Infinity-Cache (MALL) hit/miss counter; "
+                              "TCC_EA0_RDREQ_DRAM counts L2 read requests destined for the memory controller, "
+                              "which fronts the MALL, so MALL hits and HBM reads are not separable by counters")
 print(json.dumps(out, indent=1))
-Path("profiles").mkdir(exist_ok=True)
-Path("profiles/pmc_lora_gemm.json").write_text(json.dumps(out, indent=1))
+Path(A.out).parent.mkdir(exist_ok=True)
+Path(A.out).write_text(json.dumps(out, indent=1))
