@@ -40,9 +40,11 @@ __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float& z0, 
 }
 
 // One thread = NOISE_QPT quads (16-byte stores) of one base sample, 256 quads apart so every store
-// instruction of a wave is one contiguous KiB; the NOISE_QPT independent Philox chains interleave
-// (ILP) and a quarter as many workgroups are dispatched as with one quad per thread.
-constexpr int NOISE_QPT = 4;
+// instruction of a wave is one contiguous KiB.  The kernel is VALU-bound (Philox4x32-10: 20 quarter-rate
+// 32x32->64 multiplies per quad, plus Box-Muller on the transcendental unit) about as much as store-
+// bound: 4 quads per thread measured 20.9 vs 20.3 us at pop 64 (interleaved chains, a quarter of the
+// workgroups), so one quad per thread stays.
+constexpr int NOISE_QPT = 1;
 
 __global__ __launch_bounds__(256) void k_noise(uint32_t k0, uint32_t k1, int64_t base_lo,
                                                int64_t factor_len, int64_t ld, float* __restrict__ out) {

@@ -39,17 +39,17 @@ TINY = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_
 # the bf16 rounding with depth (measured: 0.3 % at the first linears -> 21 % at block 0's attn2 out)
 # while the member spread of S (1.5) still dwarfs |dS| — so ranks must agree exactly there.
 BOUNDS = {
-    "s0": {"lora_rel": 1.5e-2,   # every LoRA'd / frozen linear output, ||y - y32|| / ||y32|| (measured 0.6 %)
-           "eps_rel": 1.5e-2,    # transformer output (0.57 %)
-           "image_rel": 3e-2,    # decoded image (1.2 %)
-           "reward_abs": 0.1,    # per-image combined reward, PickScore scale exp(logit_scale) = 14.3 (0.043)
-           "S_abs": 0.1},        # S[k, j] (0.040)
-    "s1": {"lora_rel": 0.35, "eps_rel": 0.1, "image_rel": 0.15, "reward_abs": 0.15, "S_abs": 0.1},
+    "s0": {"lora_rel": 9e-3,     # every LoRA'd / frozen linear output, ||y - y32|| / ||y32|| (measured 0.59 %)
+           "eps_rel": 8.5e-3,    # transformer output (0.56 %)
+           "image_rel": 1.8e-2,  # decoded image (1.17 %)
+           "reward_abs": 0.033,  # per-image combined reward, PickScore scale exp(logit_scale) = 14.3 (0.022)
+           "S_abs": 0.017},      # S[k, j] (0.011; member spread of S 0.051)
+    "s1": {"lora_rel": 0.32, "eps_rel": 0.078, "image_rel": 0.095, "reward_abs": 0.11, "S_abs": 0.106},
 }
 KEYS = ("lora_rel", "eps_rel", "image_rel", "reward_abs", "S_abs")
-# test_rank_fidelity_over_seeds (sigma 1e-2, 6 epochs' seeds x 8 members): provisional, set from the
-# first measurement
-RANK_BOUNDS = {"S_abs": 0.03, "pooled_tau": 0.8}
+# test_rank_fidelity_over_seeds (sigma 1e-2, 6 epochs' seeds x 8 members, 168 member pairs): bounds at
+# ~1.5x the measured S drift; pooled Kendall tau >= 0.95 (VERDICT r2 bar)
+RANK_BOUNDS = {"S_abs": 0.028, "pooled_tau": 0.95}   # measured (round 3): S_abs 0.0187, pooled tau 0.964
 
 
 def kendall_tau(a, b):
@@ -186,8 +186,8 @@ def test_member_eval_bf16_vs_fp32_with_reference_noise(stack, dev, golden, case,
         assert worst[k] <= b, (k, worst[k], b, report)
     if case == "s1":   # member signal >> bf16 noise: the fitness order must be the reference's
         assert report["rank_exact"] and report["kendall_tau"] == 1.0, report
-    else:              # |dS| ~ member spread at sigma 1e-2 on random weights: rank agreement is partial
-        assert report["kendall_tau"] >= 0.6, report
+    else:              # one seed's 8 members: a single swapped close pair reads 0.93 (pooled over seeds:
+        assert report["kendall_tau"] >= 0.85, report   # test_rank_fidelity_over_seeds)
 
 
 def test_rank_fidelity_over_seeds(stack, dev, golden):
