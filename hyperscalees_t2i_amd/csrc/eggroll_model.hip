@@ -216,182 +216,6 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 }
 
 // ------------------------------------------------------------------------------------
-// Persistent, DMA-pipelined form of the 3x3 depthwise conv (no input SiLU; GLU or plain): the same
-// tiles (8 output rows x 32 columns x 32 channels per plane) and the same per-output arithmetic
-// (fp32 bias + 9 taps in tap order, bf16 rounding, GLU as value * silu(gate)) — bit-identical to
-// k_dwconv_nhwc — but each workgroup walks a sequence of tiles with its input staged by
-// buffer_load ... lds DMA into a double buffer: tile i+1's halo (and its weights, into registers)
-// is in flight while tile i is computed, so a CU streams instead of alternating load -> compute ->
-// store per one-shot block (the one-shot kernel spent most of a block's life waiting on its loads).
-// 8 waves per workgroup: thread = (4-channel group q, column xs, half h), output rows 4h .. 4h+3.
-// LDS unit u (16 B) = [plane][ty][tx][chunk] exactly as k_dwconv_nhwc's staging, so the DMA lane
-// layout (lane l of instruction i of wave w writes unit (i * 8 + w) * 64 + l) needs no remap;
-// out-of-image halo pixels read as zeros through an out-of-range buffer offset.
-// Concurrent tiles on one XCD are consecutive in (channel slice fastest) order: neighbouring 64-B
-// channel slices of a pixel share 128-B lines in that XCD's L2.
-// ------------------------------------------------------------------------------------
-constexpr int DWP_THREADS = 512;
-typedef __attribute__((address_space(3))) void dwp_lds_void;
-
-template <bool GLU>
-__global__ __launch_bounds__(DWP_THREADS, 1) void k_dwconv3_pipe(const unsigned short* __restrict__ in,
-                                                                 const unsigned short* __restrict__ wt,
-                                                                 const unsigned short* __restrict__ bias, int B, int H,
-                                                                 int W, int Cin, int xtiles, int bands, int cslices,
-                                                                 unsigned short* __restrict__ out) {
-    constexpr int KS = 3, PLANES = GLU ? 2 : 1;
-    constexpr int TR = DW_TH + KS - 1, TC = DW_TW + KS - 1, PIXB = DW_CS * 2;
-    constexpr int UNITS = PLANES * TR * TC * 4;          // halo: 16-B units [plane][ty][tx][chunk]
-    constexpr int IN_BYTES = UNITS * 16;
-    constexpr int WUNITS = (9 + 1) * PLANES * 4;         // weights [tap][plane][chunk], then bias [plane][chunk]
-    constexpr int BUF = IN_BYTES + WUNITS * 16;
-    constexpr int NDMA = (UNITS + DWP_THREADS - 1) / DWP_THREADS;  // halo DMA instructions per wave per tile
-    static_assert(36 * PLANES <= 128, "weights: waves 0 and 1 stage them");
-    __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
-    const int Cout = GLU ? Cin / 2 : Cin;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t ntiles = (int64_t)B * bands * xtiles * cslices;
-    // tile sequence: at step i, XCD x (blocks bid % 8 == x) runs tiles [i*G + x*nbx, +nbx) (G % 8 == 0)
-    const int G = gridDim.x, nbx = G >> 3, xcd = blockIdx.x & 7, lb = blockIdx.x >> 3;
-    auto tile_at = [&](int64_t i) -> int64_t { return i * G + (int64_t)xcd * nbx + lb; };
-    struct Tile {
-        int b, y0, x0, cs;
-    };
-    auto decode = [&](int64_t t) {
-        Tile r;
-        r.cs = (int)(t % cslices);
-        t /= cslices;
-        r.x0 = (int)(t % xtiles) * DW_TW;
-        t /= xtiles;
-        r.y0 = (int)(t % bands) * DW_TH;
-        r.b = (int)(t / bands);
-        return r;
-    };
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wt, (short)0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(bias ? bias : wt), (short)0, 0x7fffffff, 0x00020000);
-    auto issue = [&](const Tile& T, char* buf) {
-        const uint64_t base = (uint64_t)(in + (int64_t)T.b * H * W * Cin);
-        const unsigned short* ib = (const unsigned short*)(
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(base >> 32)) << 32) |
-            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)ib, (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < NDMA; ++i) {
-            const int u = (i * 8 + wave) * 64 + lane;
-            const int ch = u & 3;
-            int pix = u >> 2;
-            const int pl = pix / (TR * TC);
-            pix -= pl * (TR * TC);
-            const int ty = pix / TC, tx = pix - ty * TC;
-            const int gy = T.y0 + ty - 1, gx = T.x0 + tx - 1;
-            const bool ok = u < UNITS && gy >= 0 && gy < H && gx >= 0 && gx < W;
-            const uint32_t off = ok ? (uint32_t)((((int64_t)gy * W + gx) * Cin + pl * Cout + T.cs * DW_CS + ch * 8) * 2)
-                                    : 0x80000000u;
-            if ((i * 8 + wave) * 64 < UNITS)  // wave-uniform: instructions past the tile are skipped
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (dwp_lds_void*)(buf + (i * 8 + wave) * 1024), 16, off, 0,
-                                                         0, 0);
-        }
-        // the slice's weights (waves 0-1, units IN + k, k < 36 * PLANES) and bias (wave 2) ride along
-        if (wave < 2) {
-            const int k = wave * 64 + lane;
-            const int ch = k & 3, pl = (k >> 2) % PLANES, tp = (k >> 2) / PLANES;
-            const uint32_t off = (uint32_t)(((int64_t)tp * Cin + pl * Cout + T.cs * DW_CS + ch * 8) * 2);
-            if (wave * 64 < 36 * PLANES && k < 36 * PLANES)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (dwp_lds_void*)(buf + IN_BYTES + wave * 1024), 16, off, 0, 0,
-                                                         0);
-        } else if (wave == 2) {
-            const int ch = lane & 3, pl = lane >> 2;
-            const uint32_t off = bias ? (uint32_t)((pl * Cout + T.cs * DW_CS + ch * 8) * 2) : 0x80000000u;
-            if (lane < 4 * PLANES)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (dwp_lds_void*)(buf + IN_BYTES + 36 * PLANES * 16), 16, off,
-                                                         0, 0, 0);
-        }
-    };
-    const int q = tid & 7, xs = (tid >> 3) & 31, hh = tid >> 8;
-    int64_t i = 0;
-    int64_t t = tile_at(0);
-    if (t >= ntiles) return;
-    Tile cur = decode(t);
-    issue(cur, lds);
-    for (;; ++i) {
-        const char* buf = lds + (i & 1) * BUF;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMA (and this wave's older stores)
-        __syncthreads();                                  // whole tile staged; the other buffer is free
-        const Tile T = cur;
-        const int64_t tn = tile_at(i + 1);
-        const bool more = tn < ntiles;
-        if (more) {  // next tile in flight while this one is computed
-            cur = decode(tn);
-            issue(cur, lds + ((i + 1) & 1) * BUF);
-        }
-        const int x = T.x0 + xs;
-        const int cq = T.cs * DW_CS + q * 4;
-        auto rd = [&](int pl, int ty, int tx, float (&f)[4]) {
-            const u16x4m v = *reinterpret_cast<const u16x4m*>(buf + ((pl * TR + ty) * TC + tx) * PIXB + q * 8);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) f[c] = b2f(v[c]);
-        };
-        float res[4][4];
-#pragma unroll 1
-        for (int pl = 0; pl < PLANES; ++pl) {
-            float w[9][4], bs[4];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const u16x4m wv = *reinterpret_cast<const u16x4m*>(buf + IN_BYTES + (k * PLANES + pl) * 64 + q * 8);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) w[k][c] = b2f(wv[c]);
-            }
-            {
-                const u16x4m bv = *reinterpret_cast<const u16x4m*>(buf + IN_BYTES + (9 * PLANES + pl) * 64 + q * 8);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) bs[c] = bias ? b2f(bv[c]) : 0.0f;
-            }
-            float win[3][3][4];
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx) rd(pl, hh * 4 + r, xs + dx, win[r][dx]);
-#pragma unroll
-            for (int o = 0; o < 4; ++o) {
-                const int oy = hh * 4 + o;
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx) rd(pl, oy + 2, xs + dx, win[2][dx]);
-                float acc[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[c] = bs[c];
-#pragma unroll
-                for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) acc[c] += win[dy][dx][c] * w[dy * 3 + dx][c];
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        win[0][dx][c] = win[1][dx][c];
-                        win[1][dx][c] = win[2][dx][c];
-                    }
-                if (GLU && pl == 0) {
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) res[o][c] = acc[c];
-                } else {
-                    const int y = T.y0 + oy;
-                    if (y < H && x < W) {
-                        u16x4m ov;
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) ov[c] = f2b(GLU ? res[o][c] * silu(acc[c]) : acc[c]);
-                        *reinterpret_cast<u16x4m*>(out + (((int64_t)T.b * H + y) * W + x) * Cout + cq) = ov;
-                    }
-                }
-            }
-        }
-        if (!more) break;
-    }
-}
-
-// ------------------------------------------------------------------------------------
 // Fused row normalisation over the channel (last) dim of a [rows, C] bf16 tensor:
 //   y = norm(x)                      RMS (x / sqrt(mean x^2 + eps)) or LayerNorm (centred)
 //   y = y * w[c] (opt) * (1 + mscale[g, c]) (opt) + mshift[g, c] (opt) + b[c] (opt)
@@ -1302,11 +1126,8 @@ extern "C" int eggroll_gated_residual(void* x, const void* y, const void* gate, 
     return EGGROLL_OK;
 }
 
-extern "C" int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
-                                       int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
-                                       int32_t kernel, void* stream) {
-    EGG_CHECK_ARG(kernel >= 0 && kernel <= 2, "dwconv: kernel %d unsupported (0 auto, 1 one-shot, 2 pipelined)", kernel);
-    EGG_CHECK_ARG(kernel != 2 || (ks == 3 && !pre_silu), "dwconv: the pipelined kernel runs ks 3 without input SiLU");
+extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H, int64_t W,
+                                   int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out, void* stream) {
     EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && C > 0, "dwconv: bad sizes");
     const int64_t cout = glu ? C / 2 : C;
     EGG_CHECK_ARG((!glu || C % 2 == 0) && cout % DW_CS == 0, "dwconv: output channels must be a multiple of %d", DW_CS);
@@ -1325,27 +1146,6 @@ extern "C" int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const vo
     auto* w = (const unsigned short*)w_t;
     auto* bb = (const unsigned short*)bias;
     auto* o = (unsigned short*)out;
-    const int sel = kernel ? kernel : ((ks == 3 && !pre_silu) ? 2 : 1);
-    if (sel == 2) {
-        EGG_CHECK_ARG(B * H * W * C < (1ll << 31), "dwconv: batch too large for the pipelined kernel");
-        EGG_CHECK_ARG(bias == nullptr || ((uintptr_t)bias & 7) == 0, "dwconv: bias must be 8-byte aligned");
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                     hipSuccess)
-            cus = 256;
-        int64_t g = ((nblk + 7) / 8) * 8;
-        const int64_t resident = (int64_t)cus * (glu ? 1 : 2);  // 8-wave workgroups per CU (LDS / VGPRs)
-        if (g > resident) g = (resident / 8) * 8;
-        if (g < 8) g = 8;
-        if (glu)
-            hipLaunchKernelGGL((k_dwconv3_pipe<true>), dim3((unsigned)g), dim3(DWP_THREADS), 0, st, i, w, bb, (int)B, (int)H,
-                               (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o);
-        else
-            hipLaunchKernelGGL((k_dwconv3_pipe<false>), dim3((unsigned)g), dim3(DWP_THREADS), 0, st, i, w, bb, (int)B,
-                               (int)H, (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o);
-        EGG_CHECK_LAUNCH("dwconv_nhwc(pipelined)");
-        return EGGROLL_OK;
-    }
 #define EGG_DW(KS_, PS_, GL_)                                                                                 \
     hipLaunchKernelGGL((k_dwconv_nhwc<KS_, PS_, GL_>), grid, dim3(256), 0, st, i, w, bb, (int)H, (int)W, (int)C,  \
                        (int)xtiles, (int)bands, (int)cslices, o)
@@ -1360,11 +1160,6 @@ extern "C" int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const vo
 #undef EGG_DW
     EGG_CHECK_LAUNCH("dwconv_nhwc");
     return EGGROLL_OK;
-}
-
-extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H, int64_t W,
-                                   int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out, void* stream) {
-    return eggroll_dwconv_nhwc_sel(in, w_t, bias, B, H, W, C, ks, pre_silu, glu, out, 0, stream);
 }
 
 extern "C" int eggroll_dwconv_pw_nhwc(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H, int64_t W,

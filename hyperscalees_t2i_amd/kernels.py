@@ -478,9 +478,8 @@ class OpTimer:
 
 
 def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], ks: int, pre_silu: bool,
-                glu: bool, out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
-    """x [B,H,W,C] bf16 contiguous; w_t [ks*ks, C] bf16; returns [B,H,W,C or C/2].  kernel: 0 auto, 1 the
-    one-shot LDS-tiled kernel, 2 the persistent DMA-pipelined one (ks 3, no input SiLU; bit-identical)."""
+                glu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [B,H,W,C] bf16 contiguous; w_t [ks*ks, C] bf16; returns [B,H,W,C or C/2]."""
     _dev(x, "dwconv(x)", torch.bfloat16)
     _dev(w_t, "dwconv(w_t)", torch.bfloat16)
     B, H, W, C = x.shape
@@ -492,8 +491,8 @@ def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor]
     if out is None:
         out = torch.empty((B, H, W, co), dtype=torch.bfloat16, device=x.device)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_dwconv_nhwc_sel", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu),
-              int(glu), out.data_ptr(), int(kernel), _stream(x.device))
+    _lib.call("eggroll_dwconv_nhwc", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu), int(glu),
+              out.data_ptr(), _stream(x.device))
     OpTimer.end(e0, f"dwconv_nhwc<{ks},{int(pre_silu)},{int(glu)}>", 2.0 * B * H * W * (C + co), f"{B}x{H}x{W}x{C}")
     return out
 

@@ -216,12 +216,6 @@ int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta
 int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
                         int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
                         void* stream);
-/* The same conv with an explicit kernel choice (per call, for A/B measurement): 0 auto, 1 the one-shot
- * LDS-tiled kernel (one block per 8 x 32 x 32 tile), 2 the persistent DMA-pipelined kernel (ks 3 without
- * input SiLU only; bit-identical to 1).  Auto picks 2 where it applies.                          */
-int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
-                            int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
-                            int32_t kernel, void* stream);
 /* The DC-AE multi-scale aggregation (diffusers SanaMultiscaleAttentionProjection: depthwise ks x ks
  * conv, no bias, then a grouped 1x1 conv with groups of 32 channels) in one pass:
  *   d = bf16(dwconv(in, w_t)),  out[.., 32g + o] = bf16(sum_c pw[g][o][c] * d[.., 32g + c])

@@ -301,26 +301,6 @@ def test_dwconv_nhwc_vs_torch(dev, B, H, W, C, ks, pre, glu):
     assert (err <= 1e-2 * y.abs() + 2e-2).all(), float(err.max())
 
 
-@pytest.mark.parametrize("B,H,W,C,glu,bias", [(4, 32, 32, 11200, True, True), (2, 20, 40, 128, True, False),
-                                             (3, 7, 5, 64, False, True), (1, 64, 64, 256, False, False),
-                                             (9, 8, 32, 64, True, True)])
-def test_dwconv_pipelined_bitexact_vs_oneshot(dev, B, H, W, C, glu, bias):
-    """The persistent DMA-pipelined 3x3 depthwise conv (kernel 2: tile sequence per workgroup, halo and
-    weights staged by buffer_load ... lds one tile ahead) equals the one-shot LDS-tiled kernel (kernel 1)
-    bit for bit: ragged bands / columns, GLU and plain, with and without bias, grids with idle blocks."""
-    g = torch.Generator().manual_seed(C + H)
-    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(dev)
-    w = (torch.randn(9, C, generator=g) / 3).to(torch.bfloat16).to(dev)
-    b = torch.randn(C, generator=g).to(torch.bfloat16).to(dev) if bias else None
-    one = K.dwconv_nhwc(x, w, b, 3, False, glu, kernel=1)
-    pipe = K.dwconv_nhwc(x, w, b, 3, False, glu, kernel=2)
-    auto = K.dwconv_nhwc(x, w, b, 3, False, glu)
-    torch.cuda.synchronize()
-    assert torch.equal(one, pipe) and torch.equal(pipe, auto)
-    with pytest.raises(K._lib.EggrollError, match="pipelined"):
-        K.dwconv_nhwc(x, w, b, 3, True, glu, kernel=2)     # input SiLU: one-shot kernel only
-
-
 def test_dwconv_rejects_unsupported_channels(dev):
     from hyperscalees_t2i_amd import _lib
     x = torch.zeros(1, 4, 4, 48, dtype=torch.bfloat16, device=dev)
