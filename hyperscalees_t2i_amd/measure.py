@@ -88,6 +88,17 @@ def aux_kernel_rooflines(layout: ThetaLayout, pop: int, member_lo: int, member_h
     # the same update without caps: one launch (k_update only), i.e. the HBM-bound kernel by itself
     sec = _time(lambda: K.update(theta, fac, fit, layout, pop, antithetic, lr, 0.0, 0.0, out=newt, workspace=ws), it)
     out["update_nocaps"] = _entry(sec, 4.0 * (nb * F + 2 * D))
+    out["update_nocaps"]["note"] = "the update kernel alone (no caps): the HBM-bound launch"
+    out["update_caps_pass"] = {"us": max(out["update"]["us"] - out["update_nocaps"]["us"], 0.0),
+                               "note": "the caps pass: a fixed-order reduction of n_tiles x 32 B of norm partials "
+                                       "plus one dependent launch; latency-bound (rescales only if a cap fires)"}
+    # empirical write / copy floors on this box for the same byte counts (torch's fill and copy kernels):
+    # the noise kernel writes nb * F floats and also runs Philox4x32-10 + Box-Muller per 4 of them, so it is
+    # priced against both the HBM peak (frac) and the plain-store floor (frac_of_store_floor)
+    sec_fill = _time(lambda: fac.zero_(), it)
+    fill_gbps = 4.0 * nb * layout.factor_ld / sec_fill / 1e9
+    out["noise_factors"]["store_floor_GBps"] = fill_gbps
+    out["noise_factors"]["frac_of_store_floor"] = out["noise_factors"]["GBps"] / fill_gbps
     out["sizes"] = {"pop": pop, "members": [member_lo, member_hi], "n_base": nb, "D": D,
                     "factor_len": F, "n_tiles": layout.n_tiles}
     return out

@@ -57,6 +57,17 @@ for st in "$@"; do
       done
       python3 tools/pmc_summary.py gpurun_out/${tag}_pmc1 gpurun_out/${tag}_pmc2 2 --l2 gpurun_out/${tag}_pmc3 \
           --ea gpurun_out/${tag}_pmc4 --out gpurun_out/${tag}_pmc_lora_gemm.json | tail -20 ;;
+    pmc:*)
+      # pmc:<kernel regex>:<tools script + args, ',' for spaces> -> FETCH / WRITE / L2 hit passes
+      spec=${st#pmc:}; rx=${spec%%:*}; args=${spec#*:}; args=${args//,/ }
+      i=0
+      for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+        i=$((i+1)); say "pmc $rx pass $i: $grp"
+        timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "$rx" -d gpurun_out/${tag}_kpmc$i -o run \
+            --output-format csv -- python3 tools/$args > gpurun_out/${tag}_kpmc$i.log 2>&1 \
+            || { tail -20 gpurun_out/${tag}_kpmc$i.log; exit 1; }
+      done
+      python3 tools/pmc_kernels.py gpurun_out/${tag}_kpmc1 gpurun_out/${tag}_kpmc2 gpurun_out/${tag}_kpmc3 | tail -30 ;;
     counters)
       say counters
       timeout -k 10 120 rocprofv3 -L > gpurun_out/${tag}_counters.txt 2>&1 || { tail -20 gpurun_out/${tag}_counters.txt; exit 1; }
