@@ -692,13 +692,17 @@ __global__ __launch_bounds__(256) void k_update(const float* __restrict__ theta,
     const eggroll_tile_t tl = tiles[blockIdx.x];
     const eggroll_mat_t mt = mats[tl.mat];
     const int nf = (int)stats[1];
+    // the unpaired last member (odd pop) is read at an index clamped into [0, pop): its address is
+    // uniform, so the compiler issues it as a scalar load, which runs even when no lane takes the
+    // branch — at even pop an unclamped fit[2h] read one float past the fitness vector (a fault
+    // when that vector ends a mapped segment)
+    const int64_t h = pop / 2, lastk = (2 * h < pop) ? 2 * h : pop - 1;
     for (int64_t j = tid; j < n_base; j += blockDim.x) {
         float c;
         if (!antithetic) {
             c = fit[j];
         } else {
-            const int64_t h = pop / 2;
-            c = (j < h) ? fit[j] - fit[j + h] : fit[2 * h];
+            c = (j < h) ? fit[j] - fit[j + h] : fit[lastk];
         }
         s_c[j] = c;
     }

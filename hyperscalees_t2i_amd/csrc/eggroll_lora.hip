@@ -2201,6 +2201,286 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
     EGG_STAMP_RT(7);
 }
 
+// ------------------------------------------------------------------------------------
+// Multi-tile halo conv (eggroll_conv_nhwc_sel kernel 4): one workgroup runs MT vertically stacked
+// tiles of one image column as ONE K-step stream, so the next tile's slice-0 halo and first D weight
+// K-steps stream in during the current tile's last slice exactly as a middle slice streams slice s+1
+// — the per-tile prologue (the first halo + weights, ~11 % of a 128-channel tile) is paid once per
+// MT tiles.  What that needs:
+//   * the C tile goes out through a DEDICATED wave-private 4-KiB staging region, 32 rows at a time
+//     (after the ring: nothing the in-flight DMAs write), so the epilogue overlaps them;
+//   * the next tile's halo offsets / buffer base are recomputed in place right before the last slice
+//     (the current tile's are dead by then): no extra state is carried through the MFMA loop;
+//   * the first two counted waits of the next tile target weights issued BEFORE the epilogue, so
+//     they add the epilogue's 16 C-tile stores (a lower bound of its vector-memory ops: waiting for
+//     fewer younger ops than exist only over-waits) instead of draining the stores.
+// Same MFMA sequence per tile, same epilogue arithmetic: bit-identical to kernel 2.
+// ------------------------------------------------------------------------------------
+constexpr int HMT_EPI_STORES = 16;  // store_tile_rows_c32: 4 passes x 4 16-B stores per lane
+
+template <int ACT, class RowOf, bool RES = false>
+__device__ __forceinline__ void store_tile_rows_c32(f32x4 (&acc)[8][4], char* ctile, int lane, int rbase, int col0,
+                                                    unsigned short* __restrict__ Y, int64_t ldy, RowOf row_of,
+                                                    const u16x8 (&rv)[RES ? 16 : 1]) {
+    constexpr int ROWB = 128, SLOTS = 8;
+    const int r_l = lane & 15, c_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+            const int rr = ii * 16 + r_l;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int cc = j * 16 + c_l;
+                const int slot = (cc >> 3) ^ (rr & (SLOTS - 1));
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; e += 2) {
+                    f32x2 v = {acc[2 * p + ii][j][e], acc[2 * p + ii][j][e + 1]};
+                    if constexpr (ACT == 1) v = silu2(v);
+                    o[e] = f32_to_bf16(v.x);
+                    o[e + 1] = f32_to_bf16(v.y);
+                }
+                *reinterpret_cast<u16x4*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) = o;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this pass's LDS writes done
+        u16x8 v[4];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int rr = it * 8 + (lane >> 3), sl = lane & 7;
+            v[it] = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the next pass overwrites the region
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int rr = it * 8 + (lane >> 3);
+            if constexpr (RES) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    v[it][u] = f32_to_bf16(bf16_to_f32(v[it][u]) + bf16_to_f32(rv[4 * p + it][u]));
+            }
+            *reinterpret_cast<u16x8*>(Y + row_of(rbase + p * 32 + rr) * ldy + col0 + (lane & 7) * 8) = v[it];
+        }
+    }
+}
+
+template <class G, bool NORM>
+constexpr int halo_mt_smem_bytes() {
+    return G::LDS + G::NW * 4096 + (NORM ? G::BM * G::WN_ * 4 : 0);
+}
+
+template <int ACT, bool NORM, int WMW, int WNW>
+__global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const unsigned short* __restrict__ X,
+                                                                      const unsigned short* __restrict__ Wt,
+                                                                      const unsigned short* __restrict__ bias, int H,
+                                                                      int W, int Cin, int N, int tiles_n, int mt,
+                                                                      unsigned short* __restrict__ Y, float eps = 0.0f,
+                                                                      const unsigned short* __restrict__ nw = nullptr,
+                                                                      const unsigned short* __restrict__ nb = nullptr,
+                                                                      const unsigned short* __restrict__ res = nullptr) {
+    using G = HC<WMW, WNW>;
+    static_assert(G::NW == 8, "one 8-wave workgroup per CU");
+    static_assert(halo_mt_smem_bytes<G, NORM>() <= 160 * 1024, "LDS per CU");
+    __shared__ __attribute__((aligned(16))) char smem[halo_mt_smem_bytes<G, NORM>()];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WNW, wn = wave % WNW;
+    const int grp8 = wave >> 2;
+    char* const ctile = smem + G::LDS + wave * 4096;
+    float* const red = reinterpret_cast<float*>(smem + G::LDS + G::NW * 4096);
+    // XCD-contiguous group ranges; a group = mt vertically stacked tiles of one column, horizontally
+    // neighbouring groups (sharing halo columns) adjacent, the N-tiles of one group adjacent
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+    const int grp = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+    const int gm = grp / tiles_n, tn = grp - gm * tiles_n;
+    const int n0 = tn * G::BN;
+    const int tpr = W / G::TWD, bgs = (H / G::TH) / mt;  // tiles per row band, band groups per image
+    const int xt = gm % tpr, gr = gm / tpr;
+    const int img = gr / bgs, bg = gr - img * bgs;
+    const int x0 = xt * G::TWD;
+    const int K = 9 * Cin, S = Cin / 32;
+    EGG_STAMP_RT(6);
+    EGG_STAMP(0);
+
+    // halo DMA of tile row band y0: piece i*8 + wave holds halo pixels 16p .. 16p+15; out-of-image
+    // pixels (and the pad past HP) read as zeros through an out-of-range offset
+    uint32_t hoff[G::NPW];
+    __amdgpu_buffer_rsrc_t rX;
+    auto halo_setup = [&](int y0, int ln) {
+#pragma unroll
+        for (int i = 0; i < G::NPW; ++i) {
+            const int hp = (i * G::NW + wave) * 16 + (ln >> 2);
+            const int c = (ln & 3) ^ (((hp >> 2) & 1) << 1);
+            const int hy = hp / G::HW2, hx = hp - hy * G::HW2;
+            const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+            const bool ok = hp < G::HP && y >= 0 && y < H && x >= 0 && x < W;
+            hoff[i] = ok ? (uint32_t)(((hy * W + hx) * Cin + c * 8) * 2) : 0x80000000u;
+        }
+        const int64_t pb = ((int64_t)img * H + y0 - 1) * W + (x0 - 1);  // halo pixel (0, 0)
+        const uint64_t xbu = (uint64_t)(X + pb * Cin);
+        const unsigned short* xb = (const unsigned short*)(
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(xbu >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xbu));
+        rX = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, 0x7fffffff, 0x00020000);
+    };
+    uint32_t boff[G::NBW];
+#pragma unroll
+    for (int i = 0; i < G::NBW; ++i) {
+        const int n = (i * G::NW + wave) * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ (((n >> 2) & 1) << 1);
+        boff[i] = (uint32_t)(((n0 + n) * K + c * 8) * 2);
+    }
+    // A-fragment row addresses (tap (0,0), logical halo bytes); set per tile from an opaque copy of the
+    // lane id so neither they nor anything derived from them is carried through the epilogue
+    uint32_t la[8];
+    auto make_la = [&](int ln) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const int m = wm * 128 + 16 * f + (ln & 15);
+            const int ty = m / G::TWD, tx = m % G::TWD;
+            la[f] = (uint32_t)((ty * G::HW2 + tx) * 64 + (ln >> 4) * 16);
+        }
+    };
+    const uint32_t lb = hc_swz((uint32_t)((wn * 64 + (lane & 15)) * 64 + (lane >> 4) * 16));
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
+
+    auto issue_b = [&](int sl, int tap, int slot) {
+        const int so = __builtin_amdgcn_readfirstlane((tap * Cin + sl * 32) * 2);
+        char* dst = smem + G::RB + slot * G::BSLOT;
+#pragma unroll
+        for (int i = 0; i < G::NBW; ++i) {
+            const uint32_t v = boff[i];
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(dst + (i * G::NW + wave) * 1024), 16, v, so, 0, 0);
+        }
+    };
+    auto issue_h = [&](auto I, int sl) {
+        constexpr int i = decltype(I)::value;
+        const uint32_t v = hoff[i];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(smem + (sl & 1) * G::HALO + (i * G::NW + wave) * 1024),
+                                                 16, v, sl * 64, 0, 0);
+    };
+
+    f32x4 acc[8][4];
+    bf16x8 a[4], b[4];
+    const int yb = bg * mt * G::TH;  // first tile's row band
+    // a tile's slice-0 halo + first D weight K-steps: for tile 0 here, for tile t+1 right after tile
+    // t's last MFMA (before its epilogue), into LDS the epilogue does not touch
+    auto prefetch = [&](int y0) {
+        halo_setup(y0, lane);
+        hc_static_for<0, G::NPW>([&](auto I) { issue_h(I, 0); });
+#pragma unroll
+        for (int d = 0; d < G::D; ++d) issue_b(0, d, d);
+    };
+    prefetch(yb);
+
+    // Every tile restarts the K-step count at 0 (ring slot = K-step & 3; 9 S K-steps per tile, the ring
+    // is drained at the tile boundary).  epi: an epilogue's >= HMT_EPI_STORES vector-memory ops sit
+    // between this tile's first D weight K-steps and the rest, so the waits that target K-steps 0..D-1
+    // (the tile's first wait and taps 0 .. D-2 of slice 0) count them as younger ops.
+    auto slice = [&](int s, bool epi, auto NEXT_, auto LAST_) {
+        constexpr bool NEXT = decltype(NEXT_)::value, LAST = decltype(LAST_)::value;
+        const char* hb = smem + (s & 1) * G::HALO;
+        hc_static_for<0, 9>([&](auto T_) {
+            constexpr int T = decltype(T_)::value;
+            constexpr uint32_t delta = (uint32_t)(((T / 3) * G::HW2 + (T % 3)) * 64);
+            const int k = s * 9 + T;
+            const char* bs = smem + G::RB + (k & (G::NBUF - 1)) * G::BSLOT;
+            // the 9 taps x 8 swizzled fragment addresses derived from la[] are invariant: hoisted, all 72
+            // stay live across the tile loop, through the epilogue next to the accumulators (spills).
+            // la[] made opaque per tap re-derives each where it is used (add, shift, bitop3).
+#pragma unroll
+            for (int f = 0; f < 8; ++f) asm volatile("" : "+v"(la[f]));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + lb + j * 1024);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[u] + delta));
+            if constexpr (!LAST || T + G::D < 9) {
+                if constexpr (T + G::D < 9) issue_b(s, T + G::D, (k + G::D) & (G::NBUF - 1));
+                else issue_b(s + 1, T + G::D - 9, (k + G::D) & (G::NBUF - 1));
+            }
+            P8_LGKM0_;
+            P8_BAR();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[u], acc[u][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            P8_BAR();
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[4 + u] + delta));
+            if constexpr (NEXT && T < G::NPW) issue_h(std::integral_constant<int, T>{}, s + 1);
+            if constexpr (!(LAST && T == 8)) {
+                if constexpr (NEXT && T < G::D - 1) {  // only slice 0 can follow an epilogue
+                    if (epi) wait_vmn<hc_wait_n<G, T, NEXT, LAST>() + HMT_EPI_STORES>();
+                    else wait_vmn<hc_wait_n<G, T, NEXT, LAST>()>();
+                } else {
+                    wait_vmn<hc_wait_n<G, T, NEXT, LAST>()>();
+                }
+            }
+            P8_LGKM0_;
+            P8_BAR();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[4 + u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[u], acc[4 + u][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            P8_BAR();
+        });
+    };
+
+#pragma unroll 1
+    for (int t = 0; t < mt; ++t) {
+        const int y0 = yb + t * G::TH;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        make_la(ln);
+        if (t > 0) halo_setup(y0, ln);  // this tile's halo offsets again (not kept through the epilogue)
+        if (t == 0) wait_vmn<(G::D - 1) * G::NBW>();  // halo 0 + weights of K-step 0
+        else wait_vmn<(G::D - 1) * G::NBW + HMT_EPI_STORES>();
+        P8_BAR();
+        if (t == 0) EGG_STAMP(1);
+        if (grp8 == 1) P8_BAR();  // wave-group stagger, realigned before the epilogue
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int s = 0; s < S - 1; ++s) slice(s, t > 0 && s == 0, std::true_type{}, std::false_type{});
+        slice(S - 1, false, std::false_type{}, std::true_type{});
+        if (grp8 == 0) P8_BAR();
+        if (t == 0) EGG_STAMP(2);
+        if (t + 1 < mt) {
+            // every wave has passed its last fragment read of this tile (the barrier above): halo
+            // buffer 0 and the ring are free for the next tile
+            prefetch(y0 + G::TH);
+        }
+        const int64_t prow = ((int64_t)img * H + y0) * W + x0;  // output pixel of tile row 0
+        auto row_of = [&](int r) -> int64_t { return prow + (int64_t)(r / G::TWD) * W + (r % G::TWD); };
+        if (bias)
+            lora_mfma_addend<0>(acc, lane, 0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, 1 << 30,
+                                N);
+        if constexpr (NORM) {
+            u16x8 rv[16];
+            load_res_rows<0, 8>(rv, res, lane, wm * 128, n0 + wn * 64, N, row_of);
+            conv_rmsnorm_epilogue<1, WMW, WNW>(acc, red, wm, wn, lane, row_of, eps, nw, nb,
+                                               (const unsigned short*)nullptr);
+            load_res_rows<8, 16>(rv, res, lane, wm * 128, n0 + wn * 64, N, row_of);
+            store_tile_rows_c32<0, decltype(row_of), true>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, rv);
+        } else {
+            const u16x8 rv0[1] = {};
+            store_tile_rows_c32<ACT>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, rv0);
+        }
+        if (t == 0) EGG_STAMP(3);
+    }
+    EGG_STAMP_DRAIN();
+    EGG_STAMP(5);
+    EGG_STAMP_RT(7);
+}
+
 }  // namespace eggroll
 
 using namespace eggroll;
@@ -2407,6 +2687,25 @@ static bool halo_ok(int v, int64_t ks, int64_t px, int64_t H, int64_t W, int64_t
     return N % 256 == 0 && W % HC<2>::TWD == 0;
 }
 
+// kernel 4 (multi-tile): tiles per workgroup = the largest of 4, 2, 1 dividing the row bands H / 16
+static int halo_mt_tiles(int64_t H) {
+    const int64_t bands = H / 16;
+    return bands % 4 == 0 ? 4 : bands % 2 == 0 ? 2 : 1;
+}
+
+template <int ACT, bool NORM, int WMW, int WNW>
+static void launch_halo_mt_t(const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W,
+                             int64_t Cin, int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
+                             hipStream_t st) {
+    using G = HC<WMW, WNW>;
+    const int mt = halo_mt_tiles(H);
+    const int64_t groups = B * (H / 16 / mt) * (W / G::TWD), tn = N / G::BN;
+    hipLaunchKernelGGL((k_conv3x3_halo_mt<ACT, NORM, WMW, WNW>), dim3((unsigned)(groups * tn)), dim3(64 * G::NW), 0, st,
+                       (const unsigned short*)x, (const unsigned short*)w, (const unsigned short*)bias, (int)H, (int)W,
+                       (int)Cin, (int)N, (int)tn, mt, (unsigned short*)y, eps, (const unsigned short*)nw,
+                       (const unsigned short*)nb, (const unsigned short*)res);
+}
+
 template <int ACT, bool NORM, int WMW, int WNW>
 static void launch_halo_t(const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W, int64_t Cin,
                           int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
@@ -2423,6 +2722,11 @@ template <int ACT, bool NORM>
 static void launch_halo(int v, const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W,
                         int64_t Cin, int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
                         hipStream_t st) {
+    if (v == 4) {
+        if (N == 128) launch_halo_mt_t<ACT, NORM, 4, 2>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+        else launch_halo_mt_t<ACT, NORM, 2, 4>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+        return;
+    }
     if (v == 3) launch_halo_t<ACT, NORM, 2, 2>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
     else if (N == 128) launch_halo_t<ACT, NORM, 4, 2>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
     else launch_halo_t<ACT, NORM, 2, 4>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
@@ -2439,7 +2743,7 @@ int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int
 int eggroll_conv_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
                           int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, int32_t kernel,
                           void* stream) {
-    EGG_CHECK_ARG(kernel >= 0 && kernel <= 3, "conv_nhwc: kernel must be 0 (auto), 1 (tap-staged), 2 or 3 (halo)");
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 4, "conv_nhwc: kernel must be 0 (auto), 1 (tap-staged), 2, 3 or 4 (halo)");
     EGG_CHECK_ARG(ks == 2 || ks == 3, "conv_nhwc: ks must be 2 or 3 (got %d)", ks);
     EGG_CHECK_ARG(px == 1 || px == 2, "conv_nhwc: px must be 1 or 2 (got %d)", px);
     EGG_CHECK_ARG(ks == 3 || px == 1, "conv_nhwc: px 2 needs ks 3");
@@ -2509,8 +2813,8 @@ int eggroll_conv3x3_rmsnorm_nhwc(const void* x, const void* w_packed, const void
 int eggroll_conv3x3_rmsnorm_nhwc_sel(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H,
                                      int64_t W, int64_t Cin, int64_t N, int32_t px, float eps, const void* norm_w,
                                      const void* norm_b, const void* res, void* y, int32_t kernel, void* stream) {
-    EGG_CHECK_ARG(kernel >= 0 && kernel <= 3,
-                  "conv3x3_rmsnorm_nhwc: kernel must be 0 (auto), 1 (tap-staged), 2 or 3 (halo)");
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 4,
+                  "conv3x3_rmsnorm_nhwc: kernel must be 0 (auto), 1 (tap-staged), 2, 3 or 4 (halo)");
     EGG_CHECK_ARG(px == 1 || px == 2, "conv3x3_rmsnorm_nhwc: px must be 1 or 2 (got %d)", px);
     EGG_CHECK_ARG(N == 256 || (N == 128 && px == 1),
                   "conv3x3_rmsnorm_nhwc: N = px * Cout must be 256, or 128 at px 1 (got %lld, px %d)", (long long)N, px);
@@ -2526,7 +2830,7 @@ int eggroll_conv3x3_rmsnorm_nhwc_sel(const void* x, const void* w_packed, const 
     EGG_CHECK_ARG(((uintptr_t)res & 7) == 0, "conv3x3_rmsnorm_nhwc: res must be 8-byte aligned");
     EGG_CHECK_ARG(res != y && x != y, "conv3x3_rmsnorm_nhwc: y may not alias x or res");
     const int hv = kernel == 0 ? 2 : kernel;
-    const bool hok = halo_ok(hv, 3, px, H, W, Cin, N) && (hv == 2 || N == 128);  // whole pixels per tile
+    const bool hok = halo_ok(hv, 3, px, H, W, Cin, N) && (hv != 3 || N == 128);  // whole pixels per tile
     EGG_CHECK_ARG(kernel < 2 || hok, "conv3x3_rmsnorm_nhwc: halo kernel %d needs px 1, H %% 16 == 0 and W a multiple "
                   "of the tile width (see include/eggroll.h)", kernel);
     hipStream_t st = as_stream(stream);

@@ -165,6 +165,28 @@ def test_update_workspace_reuse_and_many_chunks(dev):
         np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8, err_msg=str(caps))
 
 
+@pytest.mark.parametrize("pop", [128, 7])
+def test_update_fitness_vector_at_allocation_end(dev, pop):
+    """The fitness vector as the LAST floats of a fresh 2-MiB allocation (where the bench's caching
+    allocator had put it when an unclamped fit[2h] scalar load — issued even with no lane in the odd-
+    member branch — read past it and faulted): the update reads nothing past fit[pop - 1]."""
+    shapes = [(2, 300), (260, 2), (7,)]
+    n = EggRollNoiser(shapes, sigma=0.01, lr_scale=0.1, rank=4 if pop % 2 == 0 else 1, use_antithetic=True)
+    fac = n.sample_factors(pop, dev, seed=5)
+    g = torch.Generator().manual_seed(5)
+    theta = (torch.randn(n.num_params, generator=g) * 0.02).to(dev)
+    S = (torch.randn(pop, 4, generator=g) + 20).to(dev)
+    fit = K.fitness(S, True)
+    tail = torch.full((1 << 19,), float("nan"), device=dev)   # exactly 2 MiB: its own segment
+    tail[-pop:] = fit["fitness"]
+    fit_end = dict(fit, fitness=tail[-pop:])
+    for caps in [(0.0, 0.0), (0.0, 40.0)]:
+        out = n.update_from_factors(theta, fac, fit_end, pop, max_step_norm=caps[0], theta_max_norm=caps[1])
+        torch.cuda.synchronize()
+        ref = n.update_from_factors(theta, fac, fit, pop, max_step_norm=caps[0], theta_max_norm=caps[1])
+        assert torch.equal(out, ref), caps
+
+
 def test_update_nonfinite_members(dev):
     shapes = [(2, 40), (40, 2)]
     pop = 8
@@ -654,6 +676,36 @@ def test_conv3x3_rmsnorm_halo_vs_torch(dev, B, H, W, Cin, Cout, kern):
     # roundings, as the eager bf16 graph x + norm(conv(h))): the bound covers a rounding of |zn| too
     tol = 2.0 ** -7 * (ref.abs() + zn.abs()) + 1e-3 * ref.abs().max()
     assert bool((err <= tol).all()), f"max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [
+    (2, 64, 32, 128, 128),    # 4 row bands: 4 tiles per workgroup (512 x 128 tile)
+    (1, 32, 64, 64, 128),     # 2 bands: 2 tiles per workgroup, Cin 64 (two slices: no middle slice)
+    (1, 48, 32, 256, 128),    # 3 bands: 1 tile per workgroup (the chunked epilogue alone)
+    (1, 64, 32, 256, 256),    # 256 x 256 tile, 4 tiles per workgroup
+    (2, 32, 16, 512, 512),    # N = 512: two column tiles per tile stack
+])
+def test_conv3x3_halo_multitile_bitexact(dev, B, H, W, Cin, Cout):
+    """Kernel 4 (one workgroup streams several vertically stacked tiles: the next tile's halo and first
+    weights in flight during the current tile's last slice, C tiles through a dedicated staging region)
+    runs the same MFMA sequence per tile as kernel 2: bit-identical outputs, plain / SiLU + bias /
+    RMSNorm + residual."""
+    g = torch.Generator().manual_seed(H * 7 + Cin)
+    x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)
+    b = (torch.randn(Cout, generator=g) * 0.5).to(dev, torch.bfloat16)
+    wp = K.pack_conv3x3_weight(w, 1)
+    for bias, act in [(None, None), (b, "silu")]:
+        y2 = K.conv3x3_nhwc(x, wp, bias, 1, act, kernel=2)
+        y4 = K.conv3x3_nhwc(x, wp, bias, 1, act, kernel=4)
+        assert torch.equal(y2, y4), (bias is None, act)
+    if Cout in (128, 256):
+        nw = (1 + 0.2 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
+        nb = (0.2 * torch.randn(Cout, generator=g)).to(dev, torch.bfloat16)
+        res = torch.randn(B, H, W, Cout, generator=g).to(dev, torch.bfloat16)
+        z2 = K.conv3x3_rmsnorm_nhwc(x, wp, b, 1, 1e-5, nw, nb, res, kernel=2)
+        z4 = K.conv3x3_rmsnorm_nhwc(x, wp, b, 1, 1e-5, nw, nb, res, kernel=4)
+        assert torch.equal(z2, z4)
 
 
 def test_conv3x3_halo_rejects_ragged(dev):
