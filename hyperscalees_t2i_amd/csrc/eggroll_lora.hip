@@ -1965,8 +1965,8 @@ constexpr int halo_smem_bytes() {
 
 // store_tile_t (fast path only: every conv tile is full) with tile row -> output row through row_of
 // the residual rows of a wave's 128 x 64 tile as coalesced 16-B loads (store_tile_rows' order)
-template <int I0 = 0, int I1 = 16, class RowOf>
-__device__ __forceinline__ void load_res_rows(u16x8 (&rv)[16], const unsigned short* __restrict__ res, int lane,
+template <int I0 = 0, int I1 = 16, class RowOf, int NR>
+__device__ __forceinline__ void load_res_rows(u16x8 (&rv)[NR], const unsigned short* __restrict__ res, int lane,
                                               int rbase, int col0, int64_t ldy, RowOf row_of) {
 #pragma unroll
     for (int it = I0; it < I1; ++it)
@@ -2218,14 +2218,21 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
 // ------------------------------------------------------------------------------------
 constexpr int HMT_EPI_STORES = 16;  // store_tile_rows_c32: 4 passes x 4 16-B stores per lane
 
+// RES: + the residual rows (the same 16-B row segments as the stores), streamed one pass ahead: the
+// caller loads pass 0's four rows (rv) before its norm math, pass p + 1's are issued while pass p goes
+// through LDS — 2 x 16 registers instead of all 64 next to the accumulators.
 template <int ACT, class RowOf, bool RES = false>
 __device__ __forceinline__ void store_tile_rows_c32(f32x4 (&acc)[8][4], char* ctile, int lane, int rbase, int col0,
                                                     unsigned short* __restrict__ Y, int64_t ldy, RowOf row_of,
-                                                    const u16x8 (&rv)[RES ? 16 : 1]) {
+                                                    const unsigned short* __restrict__ res, u16x8 (&rv)[4]) {
     constexpr int ROWB = 128, SLOTS = 8;
     const int r_l = lane & 15, c_l = (lane >> 4) * 4;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
+        u16x8 rn[4];
+        if constexpr (RES) {
+            if (p < 3) load_res_rows<0, 4>(rn, res, lane, rbase + (p + 1) * 32, col0, ldy, row_of);
+        }
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii) {
             const int rr = ii * 16 + r_l;
@@ -2257,10 +2264,14 @@ __device__ __forceinline__ void store_tile_rows_c32(f32x4 (&acc)[8][4], char* ct
             const int rr = it * 8 + (lane >> 3);
             if constexpr (RES) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    v[it][u] = f32_to_bf16(bf16_to_f32(v[it][u]) + bf16_to_f32(rv[4 * p + it][u]));
+                for (int u = 0; u < 8; ++u) v[it][u] = f32_to_bf16(bf16_to_f32(v[it][u]) + bf16_to_f32(rv[it][u]));
             }
             *reinterpret_cast<u16x8*>(Y + row_of(rbase + p * 32 + rr) * ldy + col0 + (lane & 7) * 8) = v[it];
+        }
+        if constexpr (RES) {
+            if (p < 3)
+#pragma unroll
+                for (int it = 0; it < 4; ++it) rv[it] = rn[it];
         }
     }
 }
@@ -2464,15 +2475,15 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
             lora_mfma_addend<0>(acc, lane, 0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, 1 << 30,
                                 N);
         if constexpr (NORM) {
-            u16x8 rv[16];
-            load_res_rows<0, 8>(rv, res, lane, wm * 128, n0 + wn * 64, N, row_of);
+            u16x8 rv[4];  // pass 0's residual rows, in flight during the norm math
+            load_res_rows<0, 4>(rv, res, lane, wm * 128, n0 + wn * 64, N, row_of);
             conv_rmsnorm_epilogue<1, WMW, WNW>(acc, red, wm, wn, lane, row_of, eps, nw, nb,
                                                (const unsigned short*)nullptr);
-            load_res_rows<8, 16>(rv, res, lane, wm * 128, n0 + wn * 64, N, row_of);
-            store_tile_rows_c32<0, decltype(row_of), true>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, rv);
+            store_tile_rows_c32<0, decltype(row_of), true>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, res,
+                                                          rv);
         } else {
-            const u16x8 rv0[1] = {};
-            store_tile_rows_c32<ACT>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, rv0);
+            u16x8 rv0[4];
+            store_tile_rows_c32<ACT>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, nullptr, rv0);
         }
         if (t == 0) EGG_STAMP(3);
     }
