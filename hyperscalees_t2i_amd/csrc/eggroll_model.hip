@@ -37,6 +37,7 @@ __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcp
 constexpr int DW_CS = 32;  // channels per plane per block (64 B per pixel: adjacent blocks share lines)
 constexpr int DW_TW = 32;  // output columns per block
 constexpr int DW_TH = 8;   // output rows per block
+constexpr int DW_ORDER_AUTO = 0;  // block order of kernel 0 (eggroll_dwconv_nhwc_sel: 1 = order 0, 2 = order 1)
 
 typedef __attribute__((ext_vector_type(4))) unsigned short u16x4m;
 
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
                                                      const unsigned short* __restrict__ bias, // [Cin] or null
                                                      int H, int W, int Cin, int xtiles, int bands, int cslices,
                                                      unsigned short* __restrict__ out,
-                                                     const unsigned short* __restrict__ pw = nullptr) {
+                                                     const unsigned short* __restrict__ pw = nullptr, int ord = 0) {
     static_assert(!PW || (!GLU && DW_CS == 32 && DW_TH * DW_TW == 256), "PW: one 32-channel group per block");
     constexpr int PLANES = GLU ? 2 : 1;
     constexpr int HALO = KS / 2;
@@ -65,13 +66,32 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
     auto swz = [](uint32_t L) { return L ^ ((L >> 3) & 32u); };
     const int Cout = GLU ? Cin / 2 : Cin;
     const int tid = threadIdx.x;
-    int bid = xcd_remap(blockIdx.x, gridDim.x);  // adjacent channel slices share 128-B lines: same L2
-    const int cs = bid % cslices;
-    bid /= cslices;
-    const int xt = bid % xtiles;
-    bid /= xtiles;
-    const int band = bid % bands;
-    const int b = bid / bands;
+    // Block order on each XCD (xcd_remap: an XCD walks a contiguous range of ids, ~96 blocks in flight).
+    // ord 0: channel slice fastest — adjacent slices share 128-B lines, but a band's vertical neighbour
+    // (whose rows overlap its halo) is cslices ids away.  ord 1: column sweep — a pair of slices (one
+    // 128-B line per pixel), then all bands of the column, then the tile column: both the shared lines
+    // and the overlapping halo rows are read within a few neighbouring ids (L2 hits).
+    int bid = xcd_remap(blockIdx.x, gridDim.x);
+    int cs, xt, band;
+    if (ord == 0) {
+        cs = bid % cslices;
+        bid /= cslices;
+        xt = bid % xtiles;
+        bid /= xtiles;
+        band = bid % bands;
+        bid /= bands;
+    } else {
+        const int cp = (cslices & 1) ? 1 : 2, chi = cslices / cp;
+        const int clo = bid % cp;
+        bid /= cp;
+        band = bid % bands;
+        bid /= bands;
+        xt = bid % xtiles;
+        bid /= xtiles;
+        cs = (bid % chi) * cp + clo;
+        bid /= chi;
+    }
+    const int b = bid;
     const int y0 = band * DW_TH, x0 = xt * DW_TW, c0 = cs * DW_CS;
     const unsigned short* img = in + (int64_t)b * H * W * Cin;
     // stage: 16-byte units [plane][ty][tx][4 chunks]; every load of the thread is issued before the
@@ -1126,8 +1146,19 @@ extern "C" int eggroll_gated_residual(void* x, const void* y, const void* gate, 
     return EGGROLL_OK;
 }
 
+// block order (kernel argument `ord`, see k_dwconv_nhwc) for the automatic choice
+static int dw_order(int kernel) { return kernel == 0 ? DW_ORDER_AUTO : kernel - 1; }
+
 extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H, int64_t W,
                                    int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out, void* stream) {
+    return eggroll_dwconv_nhwc_sel(in, w_t, bias, B, H, W, C, ks, pre_silu, glu, out, 0, stream);
+}
+
+extern "C" int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
+                                       int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
+                                       int32_t kernel, void* stream) {
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 2, "dwconv: kernel must be 0 (auto), 1 (channel-fastest) or 2 (column "
+                  "sweep) (got %d)", kernel);
     EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && C > 0, "dwconv: bad sizes");
     const int64_t cout = glu ? C / 2 : C;
     EGG_CHECK_ARG((!glu || C % 2 == 0) && cout % DW_CS == 0, "dwconv: output channels must be a multiple of %d", DW_CS);
@@ -1148,7 +1179,7 @@ extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* 
     auto* o = (unsigned short*)out;
 #define EGG_DW(KS_, PS_, GL_)                                                                                 \
     hipLaunchKernelGGL((k_dwconv_nhwc<KS_, PS_, GL_>), grid, dim3(256), 0, st, i, w, bb, (int)H, (int)W, (int)C,  \
-                       (int)xtiles, (int)bands, (int)cslices, o)
+                       (int)xtiles, (int)bands, (int)cslices, o, nullptr, dw_order(kernel))
     if (ks == 3 && pre_silu && glu) EGG_DW(3, true, true);
     else if (ks == 3 && !pre_silu && glu) EGG_DW(3, false, true);
     else if (ks == 3 && pre_silu && !glu) EGG_DW(3, true, false);
@@ -1164,6 +1195,12 @@ extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* 
 
 extern "C" int eggroll_dwconv_pw_nhwc(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H, int64_t W,
                                       int64_t C, int32_t ks, void* out, void* stream) {
+    return eggroll_dwconv_pw_nhwc_sel(in, w_t, pw, B, H, W, C, ks, out, 0, stream);
+}
+
+extern "C" int eggroll_dwconv_pw_nhwc_sel(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H,
+                                          int64_t W, int64_t C, int32_t ks, void* out, int32_t kernel, void* stream) {
+    EGG_CHECK_ARG(kernel >= 0 && kernel <= 2, "dwconv_pw: kernel must be 0 (auto), 1 or 2 (got %d)", kernel);
     EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && C > 0 && C % DW_CS == 0, "dwconv_pw: C must be a multiple of %d", DW_CS);
     EGG_CHECK_ARG(ks == 3 || ks == 5, "dwconv_pw: ks=%d unsupported (3, 5)", ks);
     EGG_CHECK_ARG(((uintptr_t)in & 15) == 0 && ((uintptr_t)w_t & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
@@ -1182,10 +1219,10 @@ extern "C" int eggroll_dwconv_pw_nhwc(const void* in, const void* w_t, const voi
     hipStream_t st = as_stream(stream);
     if (ks == 5)
         hipLaunchKernelGGL((k_dwconv_nhwc<5, false, false, true>), dim3((unsigned)nblk), dim3(256), 0, st, i, w, nullptr,
-                           (int)H, (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o, p);
+                           (int)H, (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o, p, dw_order(kernel));
     else
         hipLaunchKernelGGL((k_dwconv_nhwc<3, false, false, true>), dim3((unsigned)nblk), dim3(256), 0, st, i, w, nullptr,
-                           (int)H, (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o, p);
+                           (int)H, (int)W, (int)C, (int)xtiles, (int)bands, (int)cslices, o, p, dw_order(kernel));
     EGG_CHECK_LAUNCH("dwconv_pw_nhwc");
     return EGGROLL_OK;
 }

@@ -478,8 +478,9 @@ class OpTimer:
 
 
 def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], ks: int, pre_silu: bool,
-                glu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """x [B,H,W,C] bf16 contiguous; w_t [ks*ks, C] bf16; returns [B,H,W,C or C/2]."""
+                glu: bool, out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
+    """x [B,H,W,C] bf16 contiguous; w_t [ks*ks, C] bf16; returns [B,H,W,C or C/2].
+    kernel: block order, 0 auto, 1 channel-fastest, 2 column sweep (eggroll_dwconv_nhwc_sel)."""
     _dev(x, "dwconv(x)", torch.bfloat16)
     _dev(w_t, "dwconv(w_t)", torch.bfloat16)
     B, H, W, C = x.shape
@@ -491,14 +492,14 @@ def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor]
     if out is None:
         out = torch.empty((B, H, W, co), dtype=torch.bfloat16, device=x.device)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_dwconv_nhwc", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu), int(glu),
-              out.data_ptr(), _stream(x.device))
+    _lib.call("eggroll_dwconv_nhwc_sel", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu),
+              int(glu), out.data_ptr(), int(kernel), _stream(x.device))
     OpTimer.end(e0, f"dwconv_nhwc<{ks},{int(pre_silu)},{int(glu)}>", 2.0 * B * H * W * (C + co), f"{B}x{H}x{W}x{C}")
     return out
 
 
 def dwconv_pw_nhwc(x: torch.Tensor, w_t: torch.Tensor, pw: torch.Tensor, ks: int,
-                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
     """Depthwise ks x ks conv (no bias) then grouped 1x1 conv (groups of 32): x [B,H,W,C] bf16,
     w_t [ks*ks, C], pw [C/32, 32, 32] ([group][out][in]) -> [B,H,W,C] (eggroll_dwconv_pw_nhwc)."""
     _dev(x, "dwconv_pw(x)", torch.bfloat16)
@@ -511,8 +512,8 @@ def dwconv_pw_nhwc(x: torch.Tensor, w_t: torch.Tensor, pw: torch.Tensor, ks: int
     if out is None:
         out = torch.empty_like(x)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_dwconv_pw_nhwc", x.data_ptr(), w_t.data_ptr(), pw.data_ptr(), B, H, W, C, ks, out.data_ptr(),
-              _stream(x.device))
+    _lib.call("eggroll_dwconv_pw_nhwc_sel", x.data_ptr(), w_t.data_ptr(), pw.data_ptr(), B, H, W, C, ks,
+              out.data_ptr(), int(kernel), _stream(x.device))
     OpTimer.end(e0, f"dwconv_pw_nhwc<{ks}>", 4.0 * B * H * W * C, f"{B}x{H}x{W}x{C}")
     return out
 

@@ -222,6 +222,15 @@ int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* bias, int64
  * in / out [B,H,W,C] bf16 (C % 32 == 0, out may not alias in), pw [C/32][32][32] bf16.          */
 int eggroll_dwconv_pw_nhwc(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H,
                            int64_t W, int64_t C, int32_t ks, void* out, void* stream);
+/* The two depthwise entries with an explicit block order (per call, for A/B measurement):
+ * 0 = automatic, 1 = channel slice fastest, 2 = column sweep (a pair of 32-channel slices, then
+ * every row band of the tile column: the halo rows and 128-B lines shared by neighbouring blocks
+ * are read by blocks a few ids apart).                                                            */
+int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
+                            int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
+                            int32_t kernel, void* stream);
+int eggroll_dwconv_pw_nhwc_sel(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H,
+                               int64_t W, int64_t C, int32_t ks, void* out, int32_t kernel, void* stream);
 
 /* Model-side fused row normalisation of x [rows, C] bf16 (C % 8 == 0, C <= 4096):
  *   y = (x - mean·layer) * rsqrt(var + eps) [* w] [* (1 + mscale[g])] [+ mshift[g]] [+ b];

@@ -323,6 +323,23 @@ def test_dwconv_nhwc_vs_torch(dev, B, H, W, C, ks, pre, glu):
     assert (err <= 1e-2 * y.abs() + 2e-2).all(), float(err.max())
 
 
+@pytest.mark.parametrize("B,H,W,C,ks,pre,glu", [(2, 32, 32, 64, 3, True, True), (3, 7, 5, 64, 3, False, False),
+                                                (1, 40, 70, 96, 5, False, False), (2, 24, 64, 192, 3, False, True)])
+def test_dwconv_block_orders_bitexact(dev, B, H, W, C, ks, pre, glu):
+    """The two block orders (1: channel slice fastest, 2: column sweep, incl. an odd slice count and
+    ragged bands / tile columns) compute every block identically: bitwise equal outputs, for the
+    depthwise conv and the fused depthwise + grouped 1x1."""
+    g = torch.Generator().manual_seed(C + H)
+    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(ks * ks, C, generator=g) / ks).to(torch.bfloat16).to(dev)
+    b = torch.randn(C, generator=g).to(torch.bfloat16).to(dev)
+    y = [K.dwconv_nhwc(x, w, b, ks, pre, glu, kernel=k) for k in (0, 1, 2)]
+    assert torch.equal(y[0], y[1]) and torch.equal(y[1], y[2])
+    pw = (torch.randn(C // 32, 32, 32, generator=g) / 6).to(torch.bfloat16).to(dev)
+    z = [K.dwconv_pw_nhwc(x, w, pw, ks, kernel=k) for k in (0, 1, 2)]
+    assert torch.equal(z[0], z[1]) and torch.equal(z[1], z[2])
+
+
 def test_dwconv_rejects_unsupported_channels(dev):
     from hyperscalees_t2i_amd import _lib
     x = torch.zeros(1, 4, 4, 48, dtype=torch.bfloat16, device=dev)
