@@ -46,6 +46,16 @@ __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float& z0, 
 // workgroups), so one quad per thread stays.
 constexpr int NOISE_QPT = 1;
 
+// The factor rows are a write-once stream (read back by perturb for the local members and by the update
+// at the end of the epoch): non-temporal 16-B stores, 29.7 -> 27.2 us at one GPU's share of configs[2]
+// and 500 -> 448 us at configs[3] (same process, tools/es_nt_probe.py).  (The same stores made perturb's
+// theta_pop rows 8-26 % slower: those stay default-policy.)
+__device__ __forceinline__ void st4_nt(float* __restrict__ p, float4 v) {
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    const f32x4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4v*>(p));
+}
+
 __global__ __launch_bounds__(256) void k_noise(uint32_t k0, uint32_t k1, int64_t base_lo,
                                                int64_t factor_len, int64_t ld, float* __restrict__ out) {
     const int64_t quads = (factor_len + 3) / 4;
@@ -68,7 +78,7 @@ __global__ __launch_bounds__(256) void k_noise(uint32_t k0, uint32_t k1, int64_t
         const int64_t g0 = q * 4;
         float* dst = row + g0;
         if (g0 + 4 <= factor_len) {
-            *reinterpret_cast<float4*>(dst) = v[u];
+            st4_nt(dst, v[u]);
         } else {
             const float t[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
             for (int i = 0; i < 4 && g0 + i < factor_len; ++i) dst[i] = t[i];
