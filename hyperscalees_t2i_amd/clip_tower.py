@@ -29,10 +29,14 @@ ACT = {"gelu": lambda x: F.gelu(x), "quick_gelu": lambda x: x * torch.sigmoid(1.
 
 
 class CLIPVisionTower:
-    def __init__(self, model, pad_head_dim: bool = False, use_kernel: bool = True, fp32_residual: bool = True):
+    def __init__(self, model, pad_head_dim: bool = False, use_kernel: bool = True, fp32_residual: bool = True,
+                 fused_residual_ln: bool = True):
         vm = model.vision_model
         self.pad_head_dim = pad_head_dim
         self.fp32_residual = fp32_residual
+        # fp32 stream: each residual add + the next LayerNorm as one libeggroll pass (eggroll_resid_layernorm)
+        # instead of torch's bf16->fp32 copy, add, layer_norm and bf16 cast; False keeps the torch ops (A/B)
+        self.fused_residual_ln = fused_residual_ln
         self.use_kernel = use_kernel   # libeggroll's MFMA attention (eggroll_cross_attention, k = v = own tokens)
         cfg = model.config.vision_config
         self.C, self.heads = cfg.hidden_size, cfg.num_attention_heads
@@ -90,8 +94,11 @@ class CLIPVisionTower:
         kernel = self.use_kernel and hd in (64, 80, 112) and T <= 320
         from . import kernels as K
         last = len(self.layers) - 1
+        fused = self.fused_residual_ln and dt == torch.bfloat16 and C % 8 == 0
+        ln_k = lambda mod, h_, add: K.resid_layernorm_(h_, add, mod.weight, mod.bias, mod.eps)  # noqa: E731
+        y_next = ln_k(self.layers[0]["ln1"], h, None) if fused else None
         for i, L in enumerate(self.layers):
-            y = self._ln32(L["ln1"], h, dt)
+            y = y_next if fused else self._ln32(L["ln1"], h, dt)
             last_i = i == last
             if kernel:
                 qkv = F.linear(y, L["wqkv"], L["bqkv"]).view(n * T, 3 * C)
@@ -105,10 +112,20 @@ class CLIPVisionTower:
                 o = F.scaled_dot_product_attention(q, k, v, scale=L["scale"]).transpose(1, 2).reshape(n, -1, C)
             if last_i:       # only the [CLS] row is read by get_image_features
                 h = h[:, :1]
+            if fused:        # h += out_proj(o); y = LN2(h)  (h: [n, T, C], or the [CLS] rows [n, 1, C] strided)
+                h2 = h.view(n * T, C) if not last_i else h[:, 0]
+                y = ln_k(L["ln2"], h2, F.linear(o.reshape(-1, C), L["wo"], L["bo"]))
+                m = F.linear(self.act(F.linear(y, L["w1"], L["b1"])), L["w2"], L["b2"])
+                if not last_i:   # h += mlp(y); the next layer's LN1 in the same pass
+                    y_next = ln_k(self.layers[i + 1]["ln1"], h2, m)
+                else:
+                    h = h2 + m.float()
+                continue
             h = h + F.linear(o, L["wo"], L["bo"]).float()
             y = self._ln32(L["ln2"], h, dt)
             h = h + F.linear(self.act(F.linear(y, L["w1"], L["b1"])), L["w2"], L["b2"]).float()
-        pooled = F.layer_norm(h[:, 0], self.post.normalized_shape, self.post.weight.float(), self.post.bias.float(),
+        hc = h if h.dim() == 2 else h[:, 0]
+        pooled = F.layer_norm(hc, self.post.normalized_shape, self.post.weight.float(), self.post.bias.float(),
                               self.post.eps)
         return pooled @ self.proj32.t()
 

@@ -337,6 +337,76 @@ __global__ __launch_bounds__(256) void k_rownorm(const unsigned short* __restric
     }
 }
 
+// ------------------------------------------------------------------------------------
+// fp32 residual stream + LayerNorm of the CLIP reward towers (clip_tower.py, fp32_residual):
+//   h[r] += float(y[r])           (y bf16, optional: the block output just computed by a GEMM)
+//   out[r] = bf16(LN(h[r]) * w + b) with fp32 statistics (mean, then the centred second moment)
+// One 64-lane wave per row (h held in registers between the passes), 8 channels per lane-chunk.
+// Replaces, per residual point, torch's bf16->fp32 copy, fp32 add, fp32 layer_norm and the bf16
+// cast of its output (four passes over the row, three of them over the fp32 stream).
+// ------------------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void k_resid_layernorm(float* __restrict__ h, int64_t ldh,
+                                                         const unsigned short* __restrict__ y, int64_t ldy,
+                                                         int64_t rows, int C, float eps,
+                                                         const unsigned short* __restrict__ w,
+                                                         const unsigned short* __restrict__ b,
+                                                         unsigned short* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (row >= rows) return;  // whole waves: a row is one wave
+    const int nchunks = C >> 3;
+    float* hr = h + row * ldh;
+    const unsigned short* yr = y ? y + row * ldy : nullptr;
+    float v[NCH][8];
+    float s1 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {
+        const int ci = lane + t * 64;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[t][i] = 0.f;
+        if (ci < nchunks) {
+            const float4 a0 = *reinterpret_cast<const float4*>(hr + ci * 8);
+            const float4 a1 = *reinterpret_cast<const float4*>(hr + ci * 8 + 4);
+            v[t][0] = a0.x; v[t][1] = a0.y; v[t][2] = a0.z; v[t][3] = a0.w;
+            v[t][4] = a1.x; v[t][5] = a1.y; v[t][6] = a1.z; v[t][7] = a1.w;
+            if (yr) {
+                const u16x8m q = *reinterpret_cast<const u16x8m*>(yr + ci * 8);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[t][i] += b2f(q[i]);
+                *reinterpret_cast<float4*>(hr + ci * 8) = float4{v[t][0], v[t][1], v[t][2], v[t][3]};
+                *reinterpret_cast<float4*>(hr + ci * 8 + 4) = float4{v[t][4], v[t][5], v[t][6], v[t][7]};
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s1 += v[t][i];
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s1 += __shfl_xor(s1, o, 64);
+    const float mean = s1 / C;
+    float s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {
+        if (lane + t * 64 < nchunks)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { const float d = v[t][i] - mean; s2 += d * d; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    const float rstd = rsqrtf(s2 / C + eps);
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {
+        const int ci = lane + t * 64;
+        if (ci >= nchunks) continue;
+        const u16x8m qw = *reinterpret_cast<const u16x8m*>(w + ci * 8);
+        const u16x8m qb = *reinterpret_cast<const u16x8m*>(b + ci * 8);
+        u16x8m o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = f2b((v[t][i] - mean) * rstd * b2f(qw[i]) + b2f(qb[i]));
+        *reinterpret_cast<u16x8m*>(out + row * C + ci * 8) = o;
+    }
+}
+
 // x[r, c] += gate[g, c] * y[r, c]   (bf16, in place; g = r / rows_per_group)
 __global__ __launch_bounds__(256) void k_gated_residual(unsigned short* __restrict__ x, const unsigned short* __restrict__ y,
                                                         const unsigned short* __restrict__ gate, int64_t gstride,
@@ -1130,6 +1200,36 @@ extern "C" int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps
     else if (nch <= 320) launch_rownorm<64, 5>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
     else launch_rownorm<64, 8>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
     EGG_CHECK_LAUNCH("rownorm");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_resid_layernorm(float* h, int64_t ldh, const void* y, int64_t ldy, int64_t rows, int64_t C,
+                                       float eps, const void* w, const void* b, void* out, void* stream) {
+    EGG_CHECK_ARG(rows >= 0 && C > 0 && C % 8 == 0 && C <= 4096, "resid_layernorm: need C %% 8 == 0, C <= 4096");
+    EGG_CHECK_ARG(ldh >= C && ldh % 4 == 0 && (!y || (ldy >= C && ldy % 8 == 0)),
+                  "resid_layernorm: row strides must cover C and keep 16-byte rows");
+    EGG_CHECK_ARG(((uintptr_t)h & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                      ((uintptr_t)w & 15) == 0 && ((uintptr_t)b & 15) == 0,
+                  "resid_layernorm: pointers must be 16-byte aligned");
+    if (rows == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(h && w && b && out, "resid_layernorm: NULL pointer");
+    EGG_CHECK_ARG(rows < (1ll << 31) / 4, "resid_layernorm: too many rows");
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    const int nch = (int)(C / 8);
+    auto* yy = (const unsigned short*)y;
+    auto* ww = (const unsigned short*)w;
+    auto* bb = (const unsigned short*)b;
+    auto* oo = (unsigned short*)out;
+#define EGG_RLN(N_) hipLaunchKernelGGL(k_resid_layernorm<N_>, grid, dim3(256), 0, st, h, ldh, yy, ldy, rows, (int)C, eps, \
+                                       ww, bb, oo)
+    if (nch <= 64) EGG_RLN(1);
+    else if (nch <= 128) EGG_RLN(2);
+    else if (nch <= 192) EGG_RLN(3);   // CLIP-H: C = 1280 (160 chunks)
+    else if (nch <= 256) EGG_RLN(4);
+    else EGG_RLN(8);
+#undef EGG_RLN
+    EGG_CHECK_LAUNCH("resid_layernorm");
     return EGGROLL_OK;
 }
 

@@ -569,6 +569,36 @@ def gated_residual_(x: torch.Tensor, y: torch.Tensor, gate: torch.Tensor, rows_p
     return x
 
 
+def resid_layernorm_(h: torch.Tensor, y: Optional[torch.Tensor], w: torch.Tensor, b: torch.Tensor, eps: float,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """h [..., C] fp32 (rows may be strided: a [n, T, C] stream or its [:, 0] rows) += y (bf16, same row
+    count, or None) in place; returns bf16 layer_norm(h) * w + b [rows, C] (eggroll_resid_layernorm)."""
+    _dev(h, "resid_layernorm(h)", torch.float32)
+    C = h.shape[-1]
+    h2 = h if h.dim() == 2 else h.view(-1, C)   # a view: the in-place add must land in h
+    if h2.stride(1) != 1:
+        raise ValueError(f"resid_layernorm: h must be rows of C unit-stride channels, got {tuple(h.shape)} {h.stride()}")
+    rows = h2.shape[0]
+    ldy = 0
+    if y is not None:
+        _dev(y, "resid_layernorm(y)", torch.bfloat16)
+        y2 = y.reshape(-1, C)
+        if y2.shape[0] != rows or y2.stride(1) != 1:
+            raise ValueError(f"resid_layernorm: y {tuple(y.shape)} does not match h rows {rows}")
+        ldy = y2.stride(0)
+    _dev(w, "resid_layernorm(w)", torch.bfloat16)
+    _dev(b, "resid_layernorm(b)", torch.bfloat16)
+    if w.numel() != C or b.numel() != C:
+        raise ValueError("resid_layernorm: w / b must have C entries")
+    if out is None:
+        out = torch.empty((rows, C), dtype=torch.bfloat16, device=h.device)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_resid_layernorm", h2.data_ptr(), h2.stride(0), _p(y2 if y is not None else None), ldy, rows, C,
+              float(eps), w.data_ptr(), b.data_ptr(), out.data_ptr(), _stream(h.device))
+    OpTimer.end(e0, "resid_layernorm", float(rows) * C * ((8 if y is not None else 4) + 2 + 2))
+    return out
+
+
 def upshortcut_add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """y [B,2H,2W,Cout] += pixel_shuffle(repeat_interleave(x [B,H,W,Cin])) in place (NHWC)."""
     _dev(y, "upshortcut(y)", torch.bfloat16)

@@ -243,6 +243,14 @@ int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps, int32_t l
 /* x[r, :] += gate[r / rows_per_group, :] * y[r, :]  (bf16, in place; gate rows gstride apart). */
 int eggroll_gated_residual(void* x, const void* y, const void* gate, int64_t gstride, int64_t rows,
                            int64_t C, int64_t rows_per_group, void* stream);
+/* fp32 residual stream + LayerNorm of the CLIP reward towers (one pass per residual point):
+ *   h[r, :] += float(y[r, :])  (y bf16, rows ldy apart; y == NULL: no add, h is only read)
+ *   out[r, :] = bf16(layer_norm(h[r, :]) * w + b)   fp32 statistics, w / b bf16 [C], out [rows, C]
+ * h fp32 rows ldh apart (ldh % 4 == 0), C % 8 == 0, C <= 4096, 16-byte aligned pointers.
+ * Replaces `h = h + linear(...).float(); F.layer_norm(h, ..., w.float(), b.float()).to(bf16)` of
+ * transformers' CLIPEncoderLayer pre-norm residual (rewards.py:66-158 scorers).                   */
+int eggroll_resid_layernorm(float* h, int64_t ldh, const void* y, int64_t ldy, int64_t rows, int64_t C,
+                            float eps, const void* w, const void* b, void* out, void* stream);
 /* DC-AE up-block shortcut, NHWC: y[b,2h+i,2w+j,c] += x[b,h,w,(4c+2i+j)/(4*Cout/Cin)]
  * (pixel_shuffle(repeat_interleave(x)) without materialising it).                            */
 int eggroll_upshortcut_add(void* y, const void* x, int64_t B, int64_t H, int64_t W, int64_t Cin,

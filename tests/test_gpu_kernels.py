@@ -349,6 +349,29 @@ def test_dwconv_rejects_unsupported_channels(dev):
 
 
 # ---------------------------------------------------------------------------------- fused row ops (model)
+@pytest.mark.parametrize("rows,C,strided,add", [(257 * 3, 1280, False, True), (50 * 5, 768, False, True),
+                                                (7, 1280, True, True), (33, 64, False, False), (5, 4096, False, True)])
+def test_resid_layernorm_vs_torch(dev, rows, C, strided, add):
+    """fp32 residual add + LayerNorm -> bf16 (the CLIP towers' pre-norm residual points) vs torch's
+    h + y.float(); F.layer_norm(h, w.float(), b.float()).to(bf16): the stream h bit-exact (one fp32 add
+    per element), the normalised output within one bf16 rounding (fp32 statistics, summation order
+    differs); strided rows = the last layer's [CLS] rows of a [n, T, C] stream."""
+    g = torch.Generator().manual_seed(rows + C)
+    T = 5 if strided else 1
+    base = (torch.randn(rows, T, C, generator=g) * 3 + 0.5).to(dev)
+    h = base[:, 0] if strided else base.view(rows, C)
+    y = torch.randn(rows, C, generator=g).to(torch.bfloat16).to(dev) if add else None
+    w = (1 + 0.3 * torch.randn(C, generator=g)).to(torch.bfloat16).to(dev)
+    b = (0.2 * torch.randn(C, generator=g)).to(torch.bfloat16).to(dev)
+    h_ref = h + y.float() if add else h.clone()
+    ref = torch.nn.functional.layer_norm(h_ref, (C,), w.float(), b.float(), 1e-5)
+    out = K.resid_layernorm_(h, y, w, b, 1e-5)
+    assert torch.equal(h, h_ref)
+    if strided:   # the other rows of the stream are untouched
+        assert torch.equal(base[:, 1:], (torch.randn(rows, T, C, generator=torch.Generator().manual_seed(rows + C)) * 3
+                                         + 0.5).to(dev)[:, 1:])
+    err = (out.float() - ref).abs()
+    assert bool((err <= 2.0 ** -8 * ref.abs() + 1e-5).all()), float(err.max())
 @pytest.mark.parametrize("C", [32, 128, 256, 512, 1024, 2240, 2560, 4096])
 @pytest.mark.parametrize("mode", ["rms_w_b_res", "rms_relu", "layer_adaln"])
 def test_rownorm_vs_torch(dev, C, mode):
