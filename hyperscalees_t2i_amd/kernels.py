@@ -18,13 +18,13 @@ from . import _lib
 CHUNK = 1024  # EGGROLL_CHUNK in include/eggroll.h
 
 
-def _dev(t: torch.Tensor, what: str, dtype=None) -> torch.Tensor:
+def _dev(t: torch.Tensor, what: str, dtype=None, contiguous: bool = True) -> torch.Tensor:
     if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
         raise _lib.EggrollError(f"{what}: expected a ROCm device tensor, got "
                                 f"{getattr(t, 'device', type(t))} (no CPU fallback)")
     if dtype is not None and t.dtype != dtype:
         raise _lib.EggrollError(f"{what}: expected dtype {dtype}, got {t.dtype}")
-    if not t.is_contiguous():
+    if contiguous and not t.is_contiguous():
         raise _lib.EggrollError(f"{what}: tensor must be contiguous")
     return t
 
@@ -573,7 +573,7 @@ def resid_layernorm_(h: torch.Tensor, y: Optional[torch.Tensor], w: torch.Tensor
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """h [..., C] fp32 (rows may be strided: a [n, T, C] stream or its [:, 0] rows) += y (bf16, same row
     count, or None) in place; returns bf16 layer_norm(h) * w + b [rows, C] (eggroll_resid_layernorm)."""
-    _dev(h, "resid_layernorm(h)", torch.float32)
+    _dev(h, "resid_layernorm(h)", torch.float32, contiguous=False)   # rows may be strided (row stride passed)
     C = h.shape[-1]
     h2 = h if h.dim() == 2 else h.view(-1, C)   # a view: the in-place add must land in h
     if h2.stride(1) != 1:
