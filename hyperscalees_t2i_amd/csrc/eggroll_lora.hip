@@ -1916,12 +1916,18 @@ __device__ __forceinline__ void wait_vmn() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WMW, int WNW = 8 / WMW>
+// PAD: halo rows HS = HW2 rounded up to 8 pixels (the pad columns are zero-filled, never read).  The
+// fragment swizzle keys on bit 2 of the halo pixel index; with HS % 8 == 0 a tap's row shift dy (HS
+// pixels) leaves that bit alone, so a fragment needs one swizzled address per column shift dx and the
+// row shift is the ds_read immediate (3 addresses per fragment instead of 9: 24 VGPRs instead of 72).
+template <int WMW, int WNW = 8 / WMW, bool PAD = true>
 struct HC {
     static constexpr int WM_ = WMW, WN_ = WNW;
     static constexpr int NW = WMW * WNW, BM = WMW * 128, BN = WNW * 64;  // waves, tile
     static constexpr int TH = 16, TWD = BM / TH;                 // output pixels of a tile
-    static constexpr int HW2 = TWD + 2, HP = (TH + 2) * HW2;     // halo pixels
+    static constexpr int HW2 = TWD + 2;                          // halo pixels per row
+    static constexpr int HS = PAD ? (HW2 + 7) / 8 * 8 : HW2;     // halo row stride in LDS (pixels)
+    static constexpr int HP = (TH + 2) * HS;                     // halo pixel slots
     static constexpr int NPW = (HP + 16 * NW - 1) / (16 * NW);  // halo pieces (16 px x 64 B) per wave
     static constexpr int HALO = NPW * NW * 1024;
     static constexpr int NBW = BN / (16 * NW);                    // weight pieces per wave per K-step
@@ -2030,7 +2036,7 @@ __device__ __forceinline__ void store_tile_rows(f32x4 (&acc)[8][4], char* smem, 
 // WMW x WNW waves: (4, 2) 512 x 128 and (2, 4) 256 x 256 tiles run one 8-wave workgroup per CU
 // with the two wave groups staggered by a barrier (as the p8 kernels); (2, 2) 256 x 128 runs two
 // 4-wave workgroups per CU (80 KiB LDS each), which overlap each other's prologue and epilogue.
-template <int ACT, bool NORM, int WMW, int WNW>
+template <int ACT, bool NORM, int WMW, int WNW, bool PAD = true>
 __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_halo(const unsigned short* __restrict__ X,
                                                          const unsigned short* __restrict__ Wt,
                                                          const unsigned short* __restrict__ bias, int H, int W,
@@ -2038,7 +2044,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
                                                          float eps = 0.0f, const unsigned short* __restrict__ nw = nullptr,
                                                          const unsigned short* __restrict__ nb = nullptr,
                                                          const unsigned short* __restrict__ res = nullptr) {
-    using G = HC<WMW, WNW>;
+    using G = HC<WMW, WNW, PAD>;
     static_assert(halo_smem_bytes<G, NORM>() * (8 / G::NW) <= 160 * 1024, "LDS per CU");
     __shared__ __attribute__((aligned(16))) char smem[halo_smem_bytes<G, NORM>()];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2065,9 +2071,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
     for (int i = 0; i < G::NPW; ++i) {
         const int hp = (i * G::NW + wave) * 16 + (lane >> 2);
         const int c = (lane & 3) ^ (((hp >> 2) & 1) << 1);
-        const int hy = hp / G::HW2, hx = hp - hy * G::HW2;
+        const int hy = hp / G::HS, hx = hp - hy * G::HS;
         const int y = y0 - 1 + hy, x = x0 - 1 + hx;
-        const bool ok = hp < G::HP && y >= 0 && y < H && x >= 0 && x < W;
+        const bool ok = hp < G::HP && hx < G::HW2 && y >= 0 && y < H && x >= 0 && x < W;
         hoff[i] = ok ? (uint32_t)(((hy * W + hx) * Cin + c * 8) * 2) : 0x80000000u;
     }
     uint32_t boff[G::NBW];
@@ -2077,14 +2083,26 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
         const int c = (lane & 3) ^ (((n >> 2) & 1) << 1);
         boff[i] = (uint32_t)(((n0 + n) * K + c * 8) * 2);
     }
-    // fragment reads: A row f of the wave at tap (0,0) as a logical halo byte; B rows + j*1024
+    // fragment reads: A row f of the wave at tap (0,0) as a logical halo byte (!PAD: swizzled per tap);
+    // PAD: the swizzled byte of A row f at column shift dx (row shift dy = immediate dy * HS * 64)
     uint32_t la[8];
+    uint32_t ad[PAD ? 8 : 1][PAD ? 3 : 1];
 #pragma unroll
     for (int f = 0; f < 8; ++f) {
         const int m = wm * 128 + 16 * f + (lane & 15);
         const int ty = m / G::TWD, tx = m % G::TWD;
-        la[f] = (uint32_t)((ty * G::HW2 + tx) * 64 + (lane >> 4) * 16);
+        la[f] = (uint32_t)((ty * G::HS + tx) * 64 + (lane >> 4) * 16);
+        if constexpr (PAD)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) ad[f][dx] = hc_swz(la[f] + dx * 64);
     }
+    auto afrag = [&](const char* hb, int f, auto T_) -> bf16x8 {
+        constexpr int T = decltype(T_)::value;
+        if constexpr (PAD)
+            return *reinterpret_cast<const bf16x8*>(hb + ad[f][T % 3] + (T / 3) * G::HS * 64);
+        else
+            return *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[f] + (uint32_t)(((T / 3) * G::HS + T % 3) * 64)));
+    };
     const uint32_t lb = hc_swz((uint32_t)((wn * 64 + (lane & 15)) * 64 + (lane >> 4) * 16));
 
     const int64_t pb = ((int64_t)img * H + y0 - 1) * W + (x0 - 1);  // halo pixel (0, 0)
@@ -2131,14 +2149,13 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
         const char* hb = smem + (s & 1) * G::HALO;
         hc_static_for<0, 9>([&](auto T_) {
             constexpr int T = decltype(T_)::value;
-            constexpr uint32_t delta = (uint32_t)(((T / 3) * G::HW2 + (T % 3)) * 64);
             const int k = s * 9 + T;
             const char* bs = smem + G::RB + (k & (G::NBUF - 1)) * G::BSLOT;
             // phase 1: weights + A fragments 0-3, prefetch K-step k+D's weights
 #pragma unroll
             for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + lb + j * 1024);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[u] + delta));
+            for (int u = 0; u < 4; ++u) a[u] = afrag(hb, u, T_);
             if constexpr (!LAST || T + G::D < 9) {
                 if constexpr (T + G::D < 9) issue_b(s, T + G::D, (k + G::D) & (G::NBUF - 1));
                 else issue_b(s + 1, T + G::D - 9, (k + G::D) & (G::NBUF - 1));
@@ -2154,7 +2171,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, 8 / (WMW * WNW)) void k_conv3x3_hal
             P8_BAR();
             // phase 2: A fragments 4-7, one halo piece of slice s+1, retire K-step k+1's weights
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[4 + u] + delta));
+            for (int u = 0; u < 4; ++u) a[u] = afrag(hb, 4 + u, T_);
             if constexpr (NEXT && T < G::NPW) issue_h(std::integral_constant<int, T>{}, s + 1);
             if constexpr (!(LAST && T == 8)) wait_vmn<hc_wait_n<G, T, NEXT, LAST>()>();
             P8_LGKM0_;
@@ -2278,7 +2295,8 @@ __device__ __forceinline__ void store_tile_rows_c32(f32x4 (&acc)[8][4], char* ct
 
 template <class G, bool NORM>
 constexpr int halo_mt_smem_bytes() {
-    return G::LDS + G::NW * 4096 + (NORM ? G::BM * G::WN_ * 4 : 0);
+    static_assert(!NORM || G::BM * G::WN_ * 4 <= G::HALO, "RMSNorm row sums go to halo buffer 1");
+    return G::LDS + G::NW * 4096;
 }
 
 template <int ACT, bool NORM, int WMW, int WNW>
@@ -2298,7 +2316,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
     const int wm = wave / WNW, wn = wave % WNW;
     const int grp8 = wave >> 2;
     char* const ctile = smem + G::LDS + wave * 4096;
-    float* const red = reinterpret_cast<float*>(smem + G::LDS + G::NW * 4096);
+    // RMSNorm row sums: halo buffer 1 (slice S-1's, S even), free between a tile's last MFMA and the next
+    // tile's first slice-1 halo DMA (the prefetch only writes buffer 0 and ring slots 0..D-1)
+    float* const red = reinterpret_cast<float*>(smem + G::HALO);
     // XCD-contiguous group ranges; a group = mt vertically stacked tiles of one column, horizontally
     // neighbouring groups (sharing halo columns) adjacent, the N-tiles of one group adjacent
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -2323,9 +2343,9 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
         for (int i = 0; i < G::NPW; ++i) {
             const int hp = (i * G::NW + wave) * 16 + (ln >> 2);
             const int c = (ln & 3) ^ (((hp >> 2) & 1) << 1);
-            const int hy = hp / G::HW2, hx = hp - hy * G::HW2;
+            const int hy = hp / G::HS, hx = hp - hy * G::HS;
             const int y = y0 - 1 + hy, x = x0 - 1 + hx;
-            const bool ok = hp < G::HP && y >= 0 && y < H && x >= 0 && x < W;
+            const bool ok = hp < G::HP && hx < G::HW2 && y >= 0 && y < H && x >= 0 && x < W;
             hoff[i] = ok ? (uint32_t)(((hy * W + hx) * Cin + c * 8) * 2) : 0x80000000u;
         }
         const int64_t pb = ((int64_t)img * H + y0 - 1) * W + (x0 - 1);  // halo pixel (0, 0)
@@ -2342,15 +2362,18 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
         const int c = (lane & 3) ^ (((n >> 2) & 1) << 1);
         boff[i] = (uint32_t)(((n0 + n) * K + c * 8) * 2);
     }
-    // A-fragment row addresses (tap (0,0), logical halo bytes); set per tile from an opaque copy of the
-    // lane id so neither they nor anything derived from them is carried through the epilogue
-    uint32_t la[8];
+    // A-fragment addresses (HC PAD layout: one swizzled byte per fragment and column shift dx, the row
+    // shift is the ds_read immediate); set per tile from an opaque copy of the lane id so nothing derived
+    // from them is carried through the epilogue
+    uint32_t ad[8][3];
     auto make_la = [&](int ln) {
 #pragma unroll
         for (int f = 0; f < 8; ++f) {
             const int m = wm * 128 + 16 * f + (ln & 15);
             const int ty = m / G::TWD, tx = m % G::TWD;
-            la[f] = (uint32_t)((ty * G::HW2 + tx) * 64 + (ln >> 4) * 16);
+            const uint32_t L = (uint32_t)((ty * G::HS + tx) * 64 + (ln >> 4) * 16);
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) ad[f][dx] = hc_swz(L + dx * 64);
         }
     };
     const uint32_t lb = hc_swz((uint32_t)((wn * 64 + (lane & 15)) * 64 + (lane >> 4) * 16));
@@ -2394,18 +2417,13 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
         const char* hb = smem + (s & 1) * G::HALO;
         hc_static_for<0, 9>([&](auto T_) {
             constexpr int T = decltype(T_)::value;
-            constexpr uint32_t delta = (uint32_t)(((T / 3) * G::HW2 + (T % 3)) * 64);
+            constexpr int DY = (T / 3) * G::HS * 64;
             const int k = s * 9 + T;
             const char* bs = smem + G::RB + (k & (G::NBUF - 1)) * G::BSLOT;
-            // the 9 taps x 8 swizzled fragment addresses derived from la[] are invariant: hoisted, all 72
-            // stay live across the tile loop, through the epilogue next to the accumulators (spills).
-            // la[] made opaque per tap re-derives each where it is used (add, shift, bitop3).
-#pragma unroll
-            for (int f = 0; f < 8; ++f) asm volatile("" : "+v"(la[f]));
 #pragma unroll
             for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + lb + j * 1024);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[u] + delta));
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + ad[u][T % 3] + DY);
             if constexpr (!LAST || T + G::D < 9) {
                 if constexpr (T + G::D < 9) issue_b(s, T + G::D, (k + G::D) & (G::NBUF - 1));
                 else issue_b(s + 1, T + G::D - 9, (k + G::D) & (G::NBUF - 1));
@@ -2420,7 +2438,7 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
             __builtin_amdgcn_s_setprio(0);
             P8_BAR();
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + hc_swz(la[4 + u] + delta));
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const bf16x8*>(hb + ad[4 + u][T % 3] + DY);
             if constexpr (NEXT && T < G::NPW) issue_h(std::integral_constant<int, T>{}, s + 1);
             if constexpr (!(LAST && T == 8)) {
                 if constexpr (NEXT && T < G::D - 1) {  // only slice 0 can follow an epilogue
@@ -2688,12 +2706,12 @@ int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t l
 }  // extern "C"
 
 // The halo-staged kernel takes 3x3 px-1 convs whose tiles are all full: H % 16 == 0, W % TWD == 0
-// (TWD = 32 for the 512 x 128 tile, 16 for 256 x 256 and 256 x 128), N % BN == 0.  Variant v:
-// 2 = 512 x 128 (N == 128) or 256 x 256 (N % 256 == 0), one 8-wave workgroup per CU;
-// 3 = 256 x 128 (N % 128 == 0), two 4-wave workgroups per CU.
+// (TWD = 32 for the 512 x 128 tile, 16 for 256 x 256), N % BN == 0: 512 x 128 (N == 128) or 256 x 256
+// (N % 256 == 0), one 8-wave workgroup per CU.  Variant v: 2 = padded halo rows (HC PAD), 3 = the
+// round-2 unpadded layout (A/B), 4 = multi-tile (padded).
 static bool halo_ok(int v, int64_t ks, int64_t px, int64_t H, int64_t W, int64_t Cin, int64_t N) {
+    (void)v;
     if (ks != 3 || px != 1 || H % 16 || 18 * (W + 2) * Cin * 2 >= (1ll << 31)) return false;  // 32-bit halo offsets
-    if (v == 3) return N % 128 == 0 && W % HC<2, 2>::TWD == 0;
     if (N == 128) return W % HC<4>::TWD == 0;
     return N % 256 == 0 && W % HC<2>::TWD == 0;
 }
@@ -2717,13 +2735,13 @@ static void launch_halo_mt_t(const void* x, const void* w, const void* bias, int
                        (const unsigned short*)nb, (const unsigned short*)res);
 }
 
-template <int ACT, bool NORM, int WMW, int WNW>
+template <int ACT, bool NORM, int WMW, int WNW, bool PAD>
 static void launch_halo_t(const void* x, const void* w, const void* bias, int64_t B, int64_t H, int64_t W, int64_t Cin,
                           int64_t N, void* y, float eps, const void* nw, const void* nb, const void* res,
                           hipStream_t st) {
-    using G = HC<WMW, WNW>;
+    using G = HC<WMW, WNW, PAD>;
     const int64_t tiles = B * (H / 16) * (W / G::TWD), tn = N / G::BN;
-    hipLaunchKernelGGL((k_conv3x3_halo<ACT, NORM, WMW, WNW>), dim3((unsigned)(tiles * tn)), dim3(64 * G::NW), 0, st,
+    hipLaunchKernelGGL((k_conv3x3_halo<ACT, NORM, WMW, WNW, PAD>), dim3((unsigned)(tiles * tn)), dim3(64 * G::NW), 0, st,
                        (const unsigned short*)x, (const unsigned short*)w, (const unsigned short*)bias, (int)H, (int)W,
                        (int)Cin, (int)N, (int)tn, (unsigned short*)y, eps, (const unsigned short*)nw,
                        (const unsigned short*)nb, (const unsigned short*)res);
@@ -2738,9 +2756,10 @@ static void launch_halo(int v, const void* x, const void* w, const void* bias, i
         else launch_halo_mt_t<ACT, NORM, 2, 4>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
         return;
     }
-    if (v == 3) launch_halo_t<ACT, NORM, 2, 2>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
-    else if (N == 128) launch_halo_t<ACT, NORM, 4, 2>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
-    else launch_halo_t<ACT, NORM, 2, 4>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+    if (v == 3 && N == 128) launch_halo_t<ACT, NORM, 4, 2, false>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+    else if (v == 3) launch_halo_t<ACT, NORM, 2, 4, false>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+    else if (N == 128) launch_halo_t<ACT, NORM, 4, 2, true>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
+    else launch_halo_t<ACT, NORM, 2, 4, true>(x, w, bias, B, H, W, Cin, N, y, eps, nw, nb, res, st);
 }
 
 extern "C" {
@@ -2841,7 +2860,7 @@ int eggroll_conv3x3_rmsnorm_nhwc_sel(const void* x, const void* w_packed, const 
     EGG_CHECK_ARG(((uintptr_t)res & 7) == 0, "conv3x3_rmsnorm_nhwc: res must be 8-byte aligned");
     EGG_CHECK_ARG(res != y && x != y, "conv3x3_rmsnorm_nhwc: y may not alias x or res");
     const int hv = kernel == 0 ? 2 : kernel;
-    const bool hok = halo_ok(hv, 3, px, H, W, Cin, N) && (hv != 3 || N == 128);  // whole pixels per tile
+    const bool hok = halo_ok(hv, 3, px, H, W, Cin, N);
     EGG_CHECK_ARG(kernel < 2 || hok, "conv3x3_rmsnorm_nhwc: halo kernel %d needs px 1, H %% 16 == 0 and W a multiple "
                   "of the tile width (see include/eggroll.h)", kernel);
     hipStream_t st = as_stream(stream);

@@ -673,9 +673,10 @@ def test_conv3x3_rmsnorm_nhwc_vs_torch(dev, B, H, W, Cin, px, Cout):
 ])
 @pytest.mark.parametrize("kern", [2, 3])
 def test_conv3x3_halo_vs_torch(dev, B, H, W, Cin, Cout, bias, act, kern):
-    """Halo-staged conv (kernel 2: 512x128 / 256x256 tiles, one 8-wave workgroup per CU; kernel 3:
-    256x128 tiles, two 4-wave workgroups per CU) vs torch fp32 on the same bf16 inputs (same bound
-    as the tap-staged kernel), and vs the tap-staged kernel (1): both round an fp32 sum once."""
+    """Halo-staged conv (512x128 / 256x256 tiles, one 8-wave workgroup per CU; kernel 2: halo rows padded
+    to 8 pixels, kernel 3: the unpadded layout) vs torch fp32 on the same bf16 inputs (same bound as the
+    tap-staged kernel), vs the tap-staged kernel (1) — both round an fp32 sum once — and kernel 2 == 3
+    bitwise (same MFMA sequence, only the LDS layout differs)."""
     g = torch.Generator().manual_seed(B * 100 + H + Cin)
     x = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
     w = (torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)).to(dev, torch.bfloat16)
@@ -692,11 +693,12 @@ def test_conv3x3_halo_vs_torch(dev, B, H, W, Cin, Cout, bias, act, kern):
     assert bool((err <= tol).all()), f"max err {err.max().item():.3e} (ref max {ref.abs().max().item():.3e})"
     d = (y.float() - y1.float()).abs()
     assert bool((d <= 2.0 ** -7 * ref.abs() + 1e-3 * ref.abs().max()).all())
+    assert torch.equal(y, K.conv3x3_nhwc(x, wp, b, 1, act, kernel=5 - kern))
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,kern", [(2, 16, 32, 128, 128, 2), (1, 32, 64, 64, 128, 2),
                                                   (1, 32, 32, 256, 256, 2), (2, 16, 32, 128, 128, 3),
-                                                  (1, 32, 48, 256, 128, 3)])
+                                                  (1, 32, 64, 256, 128, 3), (1, 16, 48, 512, 256, 3)])
 def test_conv3x3_rmsnorm_halo_vs_torch(dev, B, H, W, Cin, Cout, kern):
     """conv -> RMSNorm -> + res on the halo kernel (2-D tile rows mapped to NHWC pixels)."""
     g = torch.Generator().manual_seed(3 + W)

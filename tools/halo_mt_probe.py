@@ -1,5 +1,6 @@
-"""Same-process A/B of the halo-staged 3x3 conv: kernel 2 (one tile per workgroup) vs kernel 4 (one
-workgroup streams a stack of tiles, the next tile's halo + weights prefetched during the epilogue) at
+"""Same-process A/B of the halo-staged 3x3 conv: kernel 2 (one tile per workgroup, halo rows padded to 8
+pixels), kernel 3 (the same, unpadded round-2 layout) and kernel 4 (one workgroup streams a stack of
+tiles, the next tile's halo + weights prefetched during the epilogue) at
 the DC-AE decoder's ResBlock shapes (8 images), plain / bias+SiLU / RMSNorm+residual; interleaved
 rounds, median ms; bitwise equality of the two kernels checked on every shape.
 usage: python tools/halo_mt_probe.py [rounds]"""
@@ -42,6 +43,7 @@ for B, C, hw in [(8, 128, 1024), (8, 256, 512), (8, 512, 256)]:
     wp = K.pack_conv3x3_weight(w, 1)
     fl = 2.0 * B * hw * hw * C * C * 9
     o2, o4 = torch.empty_like(x), torch.empty_like(x)
+    ks = (2, 3, 4)   # padded one-tile, unpadded one-tile (round 2), multi-tile
     cases = {
         "plain": lambda o, k: K.conv3x3_nhwc(x, wp, None, 1, None, out=o, kernel=k),
         "bias_silu": lambda o, k: K.conv3x3_nhwc(x, wp, b, 1, "silu", out=o, kernel=k),
@@ -50,18 +52,17 @@ for B, C, hw in [(8, 128, 1024), (8, 256, 512), (8, 512, 256)]:
         cases["rmsnorm_res"] = lambda o, k: K.conv3x3_rmsnorm_nhwc(x, wp, b, 1, 1e-5, nw, nb, res, kernel=k)
     row = {}
     for name, fn in cases.items():
-        y2 = fn(o2, 2).clone()
-        y4 = fn(o4, 4)
+        ys = {k: fn(o2 if k == 2 else o4, k).clone() for k in ks}
         torch.cuda.synchronize()
-        same = bool(torch.equal(y2, y4))
-        del y2, y4
-        ms = {2: [], 4: []}
+        same = all(bool(torch.equal(ys[2], ys[k])) for k in ks)
+        del ys
+        ms = {k: [] for k in ks}
         for _ in range(rounds):
-            for k in (2, 4):
+            for k in ks:
                 ms[k].append(t(lambda: fn(o2 if k == 2 else o4, k)))
-        m2, m4 = statistics.median(ms[2]), statistics.median(ms[4])
-        row[name] = {"k2_ms": round(m2, 4), "k4_ms": round(m4, 4), "k2_tflops": round(fl / m2 / 1e9, 1),
-                     "k4_tflops": round(fl / m4 / 1e9, 1), "speedup": round(m2 / m4, 4), "bitexact": same}
+        med = {k: statistics.median(v) for k, v in ms.items()}
+        row[name] = {**{f"k{k}_ms": round(med[k], 4) for k in ks}, **{f"k{k}_tflops": round(fl / med[k] / 1e9, 1) for k in ks},
+                     "bitexact": same}
         print(f"[halo-mt] {B}x{hw}x{hw}x{C} {name}: {row[name]}", flush=True)
     out[f"{B}x{hw}x{hw}x{C}"] = row
 print(json.dumps(out))
