@@ -2400,13 +2400,13 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
     const int yb = bg * mt * G::TH;  // first tile's row band
     // a tile's slice-0 halo + first D weight K-steps: for tile 0 here, for tile t+1 right after tile
     // t's last MFMA (before its epilogue), into LDS the epilogue does not touch
-    auto prefetch = [&](int y0) {
-        halo_setup(y0, lane);
+    auto prefetch = [&](int y0, int ln) {
+        halo_setup(y0, ln);
         hc_static_for<0, G::NPW>([&](auto I) { issue_h(I, 0); });
 #pragma unroll
         for (int d = 0; d < G::D; ++d) issue_b(0, d, d);
     };
-    prefetch(yb);
+    prefetch(yb, lane);
 
     // Every tile restarts the K-step count at 0 (ring slot = K-step & 3; 9 S K-steps per tile, the ring
     // is drained at the tile boundary).  epi: an epilogue's >= HMT_EPI_STORES vector-memory ops sit
@@ -2482,26 +2482,31 @@ __global__ __launch_bounds__(64 * WMW * WNW, 1) void k_conv3x3_halo_mt(const uns
         slice(S - 1, false, std::false_type{}, std::true_type{});
         if (grp8 == 0) P8_BAR();
         if (t == 0) EGG_STAMP(2);
+        // everything lane-derived that the prefetch and the epilogue need is re-derived here from an opaque
+        // copy of the lane id: hoisted out of the tile loop it would be spilled, and a scratch reload
+        // waits vmcnt(0) — behind the next tile's prefetch DMAs, i.e. it serialises the two
+        int lne = lane;
+        asm volatile("" : "+v"(lne));
         if (t + 1 < mt) {
             // every wave has passed its last fragment read of this tile (the barrier above): halo
             // buffer 0 and the ring are free for the next tile
-            prefetch(y0 + G::TH);
+            prefetch(y0 + G::TH, lne);
         }
         const int64_t prow = ((int64_t)img * H + y0) * W + x0;  // output pixel of tile row 0
         auto row_of = [&](int r) -> int64_t { return prow + (int64_t)(r / G::TWD) * W + (r % G::TWD); };
         if (bias)
-            lora_mfma_addend<0>(acc, lane, 0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, 1 << 30,
+            lora_mfma_addend<0>(acc, lne, 0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, 1 << 30,
                                 N);
         if constexpr (NORM) {
             u16x8 rv[4];  // pass 0's residual rows, in flight during the norm math
-            load_res_rows<0, 4>(rv, res, lane, wm * 128, n0 + wn * 64, N, row_of);
-            conv_rmsnorm_epilogue<1, WMW, WNW>(acc, red, wm, wn, lane, row_of, eps, nw, nb,
+            load_res_rows<0, 4>(rv, res, lne, wm * 128, n0 + wn * 64, N, row_of);
+            conv_rmsnorm_epilogue<1, WMW, WNW>(acc, red, wm, wn, lne, row_of, eps, nw, nb,
                                                (const unsigned short*)nullptr);
-            store_tile_rows_c32<0, decltype(row_of), true>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, res,
+            store_tile_rows_c32<0, decltype(row_of), true>(acc, ctile, lne, wm * 128, n0 + wn * 64, Y, N, row_of, res,
                                                           rv);
         } else {
             u16x8 rv0[4];
-            store_tile_rows_c32<ACT>(acc, ctile, lane, wm * 128, n0 + wn * 64, Y, N, row_of, nullptr, rv0);
+            store_tile_rows_c32<ACT>(acc, ctile, lne, wm * 128, n0 + wn * 64, Y, N, row_of, nullptr, rv0);
         }
         if (t == 0) EGG_STAMP(3);
     }
