@@ -1002,6 +1002,10 @@ __device__ __forceinline__ void epi_prefetch(char* ep, int wave, int lane, int m
 }
 
 // lora_mfma_addend with every operand read from the prefetched LDS block (same k-slot layout).
+// Branch-free: every lane reads its candidate operands (all inside the LDS block) back to back under
+// one lgkmcnt wait, and a lane whose k-slot block is not its row's / column's member keeps zeros by
+// select — divergent ifs around the reads serialised eight LDS round trips.  A row's member offset is
+// one compare against the tile-local start of the next member (the tile spans at most two).
 template <int R>
 __device__ __forceinline__ void lora_mfma_addend_lds(f32x4 (&acc)[8][4], int lane, int m0, int rbase, int cbase,
                                                      const char* ep, bool has_bias, float scale, int rows_per_member,
@@ -1010,44 +1014,57 @@ __device__ __forceinline__ void lora_mfma_addend_lds(f32x4 (&acc)[8][4], int lan
     const int ma = m0 / rows_per_member;
     const int last = (m0 + 255 < M ? m0 + 255 : M - 1);
     const bool straddle = last / rows_per_member != ma;
+    const int bnd = (ma + 1) * rows_per_member - m0;  // tile-local first row of member a + 1
     const float* Tl = reinterpret_cast<const float*>(ep + epi::T);
     const unsigned short* bl = reinterpret_cast<const unsigned short*>(ep + epi::BIAS);
-    bf16x8 rf[4];
+    const float* Bk = reinterpret_cast<const float*>(ep + (h == 1 ? epi::B1 : epi::B0));
+    const bool con = h == 0 || (h == 1 && straddle);
+    float bv[4][R > 0 ? R : 1], tv[8][R > 0 ? R : 1];
+    unsigned short bb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int c = cbase + j * 16 + l16;  // tile-local column
-        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (h == 0 || (h == 1 && straddle)) {
-            const float* Bk = reinterpret_cast<const float*>(ep + (h ? epi::B1 : epi::B0));
 #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                const float sb = scale * Bk[c * R + q];
-                const short hi = bf16_bits(sb);
-                v[q] = hi;
-                v[R + q] = hi;
-                v[2 * R + q] = bf16_bits(sb - bf16_to_f32((unsigned short)hi));
-            }
-            v[3 * R] = has_bias ? (short)bl[c] : (short)0;
+        for (int q = 0; q < R; ++q) bv[j][q] = Bk[c * R + q];
+        bb[j] = bl[c];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < R; ++q) tv[i][q] = Tl[(rbase + i * 16 + l16) * R + q];
+    bf16x8 rf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float sb = scale * bv[j][q];
+            const short hi = bf16_bits(sb);
+            v[q] = hi;
+            v[R + q] = hi;
+            v[2 * R + q] = bf16_bits(sb - bf16_to_f32((unsigned short)hi));
         }
+        v[3 * R] = has_bias ? (short)bb[j] : (short)0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = con ? v[e] : (short)0;
         rf[j] = *reinterpret_cast<bf16x8*>(v);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int rl = rbase + i * 16 + l16;  // tile-local row
-        int row = m0 + rl;
-        row = row < M ? row : M - 1;
+        const bool ron = h == (rl >= bnd ? 1 : 0);
         short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (h == row / rows_per_member - ma) {
 #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                const float t = Tl[rl * R + q];
-                const short th = bf16_bits(t);
-                v[q] = th;
-                v[R + q] = bf16_bits(t - bf16_to_f32((unsigned short)th));
-                v[2 * R + q] = th;
-            }
-            v[3 * R] = (short)0x3F80;  // 1.0
+        for (int q = 0; q < R; ++q) {
+            const float t = tv[i][q];
+            const short th = bf16_bits(t);
+            v[q] = th;
+            v[R + q] = bf16_bits(t - bf16_to_f32((unsigned short)th));
+            v[2 * R + q] = th;
         }
+        v[3 * R] = (short)0x3F80;  // 1.0
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ron ? v[e] : (short)0;
         const bf16x8 lf = *reinterpret_cast<bf16x8*>(v);
 #pragma unroll
         for (int j = 0; j < 4; ++j)  // transposed fragments (TR main loop): D[n][m]

@@ -1,5 +1,5 @@
 """Where a tile's time goes in the 8-phase kernels: per-workgroup s_memtime stamps from a
-diagnostic build of eggroll_lora.hip (-DEGG_STAMPS; tools/_build/libeggroll_stamps.so, built
+diagnostic build of eggroll_lora.hip (-DEGG_STAMPS; tools/_stamps/libeggroll_stamps.so, built
 here with `python tools/stamp_probe.py build`, never loaded by the package).
 
 Stamps (wave 0 of each workgroup): 0 start, 1 prologue landed (first barrier), 2 main loop done,
@@ -15,7 +15,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-OUT = ROOT / "tools" / "_build" / "libeggroll_stamps.so"
+OUT = ROOT / "tools" / "_stamps" / "libeggroll_stamps.so"  # tools/_build is not sent to the GPU box
 
 
 def build():
