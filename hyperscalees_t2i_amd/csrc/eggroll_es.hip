@@ -254,18 +254,31 @@ __device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&wb
             const float pr = KIND == T_WIDE ? w * x : x * w;  // a * b
             acc = q == 0 ? pr : acc + pr;
         }
+        // rank 4: sqrt(4) = 2 exactly, and x / 2 and x * 0.5 are the same correctly rounded value (both
+        // round the same real number, subnormals included) — one multiply instead of the ~10-instruction
+        // correctly rounded divide (bit-identical; time-neutral on its own, the rank-4 update was
+        // latency-bound: see the software pipeline in update_fast)
+        if constexpr (R == 4) return acc * 0.5f;
         return R == 1 ? acc : acc / sqrt_r;
     }
 }
 
+// k_update at rank >= 2: the next base group's long-factor loads issued before this group's math
+// (A/B knob; perturb measured 2-5 % slower with the same pipeline at rank 4, so it has none)
+#ifndef EGG_UPD_PREFETCH
+#define EGG_UPD_PREFETCH 1
+#endif
 // members / base samples whose long-factor loads are in flight together: 8 float4 loads per
 // thread whatever the rank (rank 4 at 8 samples needed 228 VGPRs and halved the occupancy)
+#ifndef EGG_UPD_PGRR  // k_update, rank >= 2: float4 loads per group (x2 with the pipeline)
+#define EGG_UPD_PGRR 4
+#endif
 #ifndef EGG_UPD_PGRP1
 #define EGG_UPD_PGRP1 8
 #endif
 template <int KIND, int R, bool UPD = false>
 struct PGrp {
-    static constexpr int value = (KIND == T_VEC4 || R == 1) ? (UPD ? EGG_UPD_PGRP1 : 8) : 8 / R;
+    static constexpr int value = (KIND == T_VEC4 || R == 1) ? (UPD ? EGG_UPD_PGRP1 : 8) : (UPD ? EGG_UPD_PGRR : 8) / R;
 };
 
 // ------------------------------------------------------------------------------------
@@ -599,14 +612,37 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
             }
             const int n = (int)((n_base - g) < 64 ? (n_base - g) : 64);
             constexpr int PG = PGrp<KIND, R, true>::value;
-            for (int j0 = 0; j0 < n; j0 += PG) {
-                float4 X[PG][NX];
+            // rank >= 2: software-pipelined — the next group's long factors are in flight while this
+            // group's eps math runs (rank 4 at configs[3]: 559 -> 432 us with one base sample per group,
+            // 3 % faster than two; a pure read of the same stream runs 367 us); rank 1 keeps one group in
+            // registers (the second set costs an occupancy step there: 24.7 -> 27.0 us at pop 64)
+            constexpr bool PF = EGG_UPD_PREFETCH && R >= 2 && KIND != T_VEC4;
+            float4 XN[PF ? PG : 1][NX];
+            auto load_grp = [&](float4 (&D)[PF ? PG : 1][NX], int j0) {
 #pragma unroll
-                for (int t = 0; t < PG; ++t)
+                for (int t = 0; t < (PF ? PG : 1); ++t)
 #pragma unroll
                     for (int c = 0; c < NX; ++c)
-                        X[t][c] = (ok && j0 + t < n) ? ld4<true>(factors + (g + j0 + t) * ld_f + xo + 4 * c)
+                        D[t][c] = (ok && j0 + t < n) ? ld4<true>(factors + (g + j0 + t) * ld_f + xo + 4 * c)
                                                      : float4{0, 0, 0, 0};
+            };
+            if constexpr (PF) load_grp(XN, 0);
+            for (int j0 = 0; j0 < n; j0 += PG) {
+                float4 X[PG][NX];
+                if constexpr (PF) {
+#pragma unroll
+                    for (int t = 0; t < PG; ++t)
+#pragma unroll
+                        for (int c = 0; c < NX; ++c) X[t][c] = XN[t % (PF ? PG : 1)][c];
+                    if (j0 + PG < n) load_grp(XN, j0 + PG);
+                } else {
+#pragma unroll
+                    for (int t = 0; t < PG; ++t)
+#pragma unroll
+                        for (int c = 0; c < NX; ++c)
+                            X[t][c] = (ok && j0 + t < n) ? ld4<true>(factors + (g + j0 + t) * ld_f + xo + 4 * c)
+                                                         : float4{0, 0, 0, 0};
+                }
 #pragma unroll
                 for (int t = 0; t < PG; ++t) {
                     if (j0 + t >= n) break;

@@ -68,6 +68,14 @@ for st in "$@"; do
             || { tail -20 gpurun_out/${tag}_kpmc$i.log; exit 1; }
       done
       python3 tools/pmc_kernels.py gpurun_out/${tag}_kpmc1 gpurun_out/${tag}_kpmc2 gpurun_out/${tag}_kpmc3 | tail -30 ;;
+    sq:*)
+      # sq:<kernel regex>:<tools script + args> -> one SQ counter pass (instruction mix, wave cycles, waits)
+      spec=${st#sq:}; rx=${spec%%:*}; args=${spec#*:}; args=${args//,/ }
+      say "sq $rx"
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES \
+          SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-include-regex "$rx" -d gpurun_out/${tag}_sq \
+          -o run --output-format csv -- python3 tools/$args > gpurun_out/${tag}_sq.log 2>&1 \
+          || { tail -20 gpurun_out/${tag}_sq.log; exit 1; } ;;
     counters)
       say counters
       timeout -k 10 120 rocprofv3 -L > gpurun_out/${tag}_counters.txt 2>&1 || { tail -20 gpurun_out/${tag}_counters.txt; exit 1; }
