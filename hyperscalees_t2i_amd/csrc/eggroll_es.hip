@@ -44,7 +44,10 @@ __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float& z0, 
 // 32x32->64 multiplies per quad, plus Box-Muller on the transcendental unit) about as much as store-
 // bound: 4 quads per thread measured 20.9 vs 20.3 us at pop 64 (interleaved chains, a quarter of the
 // workgroups), so one quad per thread stays.
-constexpr int NOISE_QPT = 1;
+#ifndef EGG_NOISE_QPT  // A/B knob
+#define EGG_NOISE_QPT 1
+#endif
+constexpr int NOISE_QPT = EGG_NOISE_QPT;
 
 // The factor rows are a write-once stream (read back by perturb for the local members and by the update
 // at the end of the epoch): non-temporal 16-B stores, 29.7 -> 27.2 us at one GPU's share of configs[2]
@@ -270,6 +273,9 @@ __device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&wb
 #endif
 // members / base samples whose long-factor loads are in flight together: 8 float4 loads per
 // thread whatever the rank (rank 4 at 8 samples needed 228 VGPRs and halved the occupancy)
+#ifndef EGG_PTB_PGRR  // k_perturb, rank >= 2: float4 loads per group (A/B knob)
+#define EGG_PTB_PGRR 8
+#endif
 #ifndef EGG_UPD_PGRR  // k_update, rank >= 2: float4 loads per group (x2 with the pipeline)
 #define EGG_UPD_PGRR 4
 #endif
@@ -278,7 +284,7 @@ __device__ __forceinline__ float fast_eps(const float4 (&X)[R], const float (&wb
 #endif
 template <int KIND, int R, bool UPD = false>
 struct PGrp {
-    static constexpr int value = (KIND == T_VEC4 || R == 1) ? (UPD ? EGG_UPD_PGRP1 : 8) : (UPD ? EGG_UPD_PGRR : 8) / R;
+    static constexpr int value = (KIND == T_VEC4 || R == 1) ? (UPD ? EGG_UPD_PGRP1 : 8) : (UPD ? EGG_UPD_PGRR : EGG_PTB_PGRR) / R;
 };
 
 // ------------------------------------------------------------------------------------
