@@ -238,8 +238,10 @@ class RewardModels:
     mix_weights: Tuple[float, ...] = (0.0, 0.0, 0.0, 1.0)  # unifed_es.py:360-363 defaults (length 3 or 4)
     image_batch: int = 256
     fp32_residual: bool = True     # towers carry their residual stream / norms in fp32 (clip_tower.py)
+    text_graphs: bool = True       # replay the per-epoch text towers as one HIP graph per prompt count
     _towers: Optional[tuple] = None
     _text32: Optional[tuple] = None
+    _tgraphs: Optional[dict] = None
 
     def towers(self):
         if self._towers is None or self._towers[0].fp32_residual != self.fp32_residual:
@@ -267,18 +269,52 @@ class RewardModels:
         pick = build_clip(CLIP_TINY if tiny else CLIP_H14, device, seed + 1)
         return cls(clip=clip, pick=pick, mix_weights=tuple(mix_weights))
 
-    @torch.no_grad()
-    def prompt_features(self, prompts: Sequence[str]) -> Dict[str, torch.Tensor]:
-        """Text features once per epoch (members share prompts: common random numbers)."""
-        dev = next(self.clip.parameters()).device
-        ids, mask = synthetic_tokenize([AESTHETIC_TEXT, NEGATIVE_TEXT] + list(prompts))
-        ids, mask = ids.to(dev), mask.to(dev)
+    def _text_eager(self, ids: torch.Tensor, mask: torch.Tensor) -> Dict[str, torch.Tensor]:
         tc_model, tp_model = self.text_models()
         t_clip = _text_features(tc_model, ids, mask)
         t_clip = t_clip / t_clip.norm(dim=-1, keepdim=True).clamp_min(1e-6)   # rewards.py:100
         t_pick = _text_features(tp_model, ids[2:], mask[2:])
         t_pick = t_pick / t_pick.norm(dim=-1, keepdim=True)                   # rewards.py:153
         return {"clip_aes": t_clip[0], "clip_neg": t_clip[1], "clip_prompt": t_clip[2:], "pick_prompt": t_pick}
+
+    def _text_graphed(self, ids: torch.Tensor, mask: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """The same kernels as _text_eager, captured once per prompt count into a HIP graph and replayed:
+        the fp32 text towers are ~690 small launches per epoch whose host-side dispatch (not their
+        7.5 ms of GPU work) set the pace.  The inputs are copied into the graph's static buffers."""
+        if self._tgraphs is None:
+            self._tgraphs = {}
+        key = tuple(ids.shape)
+        ent = self._tgraphs.get(key)
+        if ent is None:
+            sid, smask = ids.clone(), mask.clone()
+            side = torch.cuda.Stream(device=ids.device)
+            side.wait_stream(torch.cuda.current_stream(ids.device))
+            with torch.cuda.stream(side):
+                self._text_eager(sid, smask)   # warm-up off the capture (library handles, kernel selection)
+            torch.cuda.current_stream(ids.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self._text_eager(sid, smask)
+            ent = self._tgraphs[key] = (graph, sid, smask, out)
+        graph, sid, smask, out = ent
+        sid.copy_(ids)
+        smask.copy_(mask)
+        graph.replay()
+        return {k: v.clone() for k, v in out.items()}
+
+    @torch.no_grad()
+    def prompt_features(self, prompts: Sequence[str]) -> Dict[str, torch.Tensor]:
+        """Text features once per epoch (members share prompts: common random numbers)."""
+        dev = next(self.clip.parameters()).device
+        ids, mask = synthetic_tokenize([AESTHETIC_TEXT, NEGATIVE_TEXT] + list(prompts))
+        ids, mask = ids.to(dev), mask.to(dev)
+        if self.text_graphs and dev.type == "cuda":
+            try:
+                return self._text_graphed(ids, mask)
+            except RuntimeError:   # a capture-incompatible op: run the same towers eagerly from now on
+                torch.cuda.synchronize(dev)
+                self.text_graphs, self._tgraphs = False, None
+        return self._text_eager(ids, mask)
 
     @torch.no_grad()
     def score(self, images: torch.Tensor, prompt_index: torch.Tensor, feats: Dict[str, torch.Tensor],

@@ -262,3 +262,18 @@ def test_cross_attention_kernel_in_population_forward(dev):
         blk.attn2.use_kernel = True
     rel = float((outs[0] - outs[1]).norm() / outs[1].norm())
     assert rel < 2e-2, rel
+
+
+def test_prompt_features_graph_replay_matches_eager(dev):
+    """The per-epoch text towers replayed as a HIP graph (one per prompt count) give the eager path's
+    exact features, for the prompts it was captured with and for new prompts of the same count."""
+    rw = RewardModels.build(dev, tiny=True)
+    ref = RewardModels.build(dev, tiny=True)
+    ref.text_graphs = False
+    for prompts in (["a red fox", "two cats on a sofa"], ["a lighthouse at dusk", "macro shot of a bee"],
+                    ["one prompt only"]):
+        got, want = rw.prompt_features(prompts), ref.prompt_features(prompts)
+        assert rw.text_graphs, "graph capture fell back to eager"
+        for k in want:
+            assert torch.equal(got[k], want[k]), (prompts, k)
+    assert len(rw._tgraphs) == 2
