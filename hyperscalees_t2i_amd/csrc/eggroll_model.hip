@@ -689,6 +689,32 @@ __global__ __launch_bounds__(256) void k_la_reduce(const float* __restrict__ par
     }
 }
 
+// Many chunks (>= LA_RED_WIDE, DC-AE's 64^2 and 128^2 maps): one thread per element, one wave per 64
+// elements (17 waves per head), a thread's partials loaded 16 at a time and summed in the same chunk
+// order (bit-identical to k_la_reduce, which walks ~4 elements per thread one after another: 8 B x
+// 16 K x 16 heads 0.226 -> 0.214 ms for the whole attention; at 4 chunks the 17x more workgroups cost
+// more than they save)
+constexpr int LA_RED_WAVES = (LA_PART + 63) / 64;
+constexpr int LA_RED_WIDE = 16;
+__global__ __launch_bounds__(64) void k_la_reduce_e(const float* __restrict__ part, int nchunk,
+                                                    float* __restrict__ kvsum) {
+    const int64_t bh = blockIdx.x / LA_RED_WAVES;
+    const int e = (blockIdx.x % LA_RED_WAVES) * 64 + threadIdx.x;
+    if (e >= LA_PART) return;
+    const float* src = part + bh * nchunk * LA_PART + e;
+    float s = 0.f;
+    int cc = 0;
+    for (; cc + 16 <= nchunk; cc += 16) {  // 16 loads in flight, summed in chunk order
+        float p[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) p[u] = src[(int64_t)(cc + u) * LA_PART];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += p[u];
+    }
+    for (; cc < nchunk; ++cc) s += src[(int64_t)cc * LA_PART];
+    kvsum[bh * LA_PART + e] = s;
+}
+
 // Pass 3 on MFMA: out^T[i][t] = sum_j kv[i][j] relu(q[t][j]) as 16x16x32 bf16 MFMAs with kv as the A
 // operand (row i, 8 consecutive j per lane — the natural [i][j] layout) and 16 tokens' q as the B
 // operand (each lane's 16-B load is 8 consecutive features of one token), so the accumulator lane
@@ -1400,8 +1426,12 @@ extern "C" int eggroll_linear_attention(const void* q, const void* k, const void
                        (float*)workspace);
     EGG_CHECK_LAUNCH("linear_attention_kv");
     float* kvsum = (float*)workspace + blocks * LA_PART;
-    hipLaunchKernelGGL(k_la_reduce, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const float*)workspace,
-                       (int)nchunk, kvsum);
+    if (nchunk >= LA_RED_WIDE)
+        hipLaunchKernelGGL(k_la_reduce_e, dim3((unsigned)(B * heads * LA_RED_WAVES)), dim3(64), 0, st,
+                           (const float*)workspace, (int)nchunk, kvsum);
+    else
+        hipLaunchKernelGGL(k_la_reduce, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const float*)workspace,
+                           (int)nchunk, kvsum);
     EGG_CHECK_LAUNCH("linear_attention_reduce");
     hipLaunchKernelGGL(k_la_out, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)q, ld, hstride,
                        (int)heads, (int)N, (int)nchunk, relu_qk, (const float*)kvsum, (unsigned short*)out, ldo);

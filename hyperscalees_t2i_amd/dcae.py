@@ -153,25 +153,56 @@ class MultiscaleLinearAttention(nn.Module):
         self.w_out = _p(c, inner * (1 + len(scales)))
         self.norm_out = RMSNormC(c)
 
-    def _attend(self, br, out):  # br [B,H,W,3*inner]: per head group h, channels [q | k | v] of 32 each
+    def _attend(self, br, out, planar=False):
+        # br [B,H,W,3*inner]: per head group h, channels [q | k | v] of 32 each (the reference layout), or
+        # planar [Q | K | V] with head h's q / k / v at column 32h of each plane
         B, H, W, C3 = br.shape
         flat = br.reshape(B * H * W, C3)
-        hs = 3 * self.hd
-        K.linear_attention(flat, flat[:, self.hd:], flat[:, 2 * self.hd:], B, H * W, self.heads, hs,
-                           relu_qk=True, out=out)
+        inner = self.heads * self.hd
+        if planar:
+            K.linear_attention(flat, flat[:, inner:], flat[:, 2 * inner:], B, H * W, self.heads, self.hd,
+                               relu_qk=True, out=out)
+        else:
+            K.linear_attention(flat, flat[:, self.hd:], flat[:, 2 * self.hd:], B, H * W, self.heads, 3 * self.hd,
+                               relu_qk=True, out=out)
+
+    # Planar q/k/v at the largest maps: the same channels, relabelled so that a head's q, k and v each
+    # share 128-B lines with the neighbouring head's instead of with its own other two (whose bytes the
+    # pass does not read): the linear attention at 8 x 128 x 128 x 16 heads 0.226 -> 0.186 ms; at 64^2
+    # and below the reference layout is as fast (tools/la_probe.py).  w_qkv's rows, the depthwise
+    # weights' channels and the grouped 1x1's 32-channel groups are permuted alike, so every branch
+    # computes the same values in the permuted columns; the attention output layout is unchanged.
+    PLANAR_MIN_TOKENS = 8192
+
+    def _planar_weights(self):
+        key = (self.w_qkv._version, self.w_qkv.data_ptr(),
+               tuple((w._version, w.data_ptr()) for w in list(self.ms_dw) + list(self.ms_pw)))
+        if getattr(self, "_planar_key", None) != key:
+            hd, heads = self.hd, self.heads
+            inner = heads * hd
+            n = torch.arange(3 * inner, device=self.w_qkv.device)
+            perm = (n % inner) // hd * (3 * hd) + n // inner * hd + n % hd   # planar column -> reference column
+            gp = torch.arange(3 * heads, device=self.w_qkv.device)
+            gperm = gp % heads * 3 + gp // heads                              # planar group -> reference group
+            self._planar_w = (self.w_qkv[perm].contiguous(), [w[:, perm].contiguous() for w in self.ms_dw],
+                              [w[gperm].contiguous() for w in self.ms_pw])
+            self._planar_key = key
+        return self._planar_w
 
     def forward(self, x):  # NHWC
         B, H, W, C = x.shape
-        qkv = F.linear(x, self.w_qkv)                             # [B,H,W,3*inner]
+        planar = H * W >= self.PLANAR_MIN_TOKENS
+        w_qkv, ms_dw, ms_pw = self._planar_weights() if planar else (self.w_qkv, self.ms_dw, self.ms_pw)
+        qkv = F.linear(x, w_qkv)                                  # [B,H,W,3*inner]
         inner = self.heads * self.hd
         # every branch's attention output lands in its column slice of one buffer (no concat pass)
         o = torch.empty((B * H * W, inner * (1 + len(self.scales))), dtype=x.dtype, device=x.device)
-        self._attend(qkv, o[:, :inner])
-        for i, (ks, wdw, wpw) in enumerate(zip(self.scales, self.ms_dw, self.ms_pw)):
-            # depthwise ks x ks + grouped 1x1 (G = 3h + {q,k,v} groups of 32) in one kernel, output in
-            # the qkv layout, which the attention reads like the first branch
+        self._attend(qkv, o[:, :inner], planar)
+        for i, (ks, wdw, wpw) in enumerate(zip(self.scales, ms_dw, ms_pw)):
+            # depthwise ks x ks + grouped 1x1 (G = 3h + {q,k,v} groups of 32, or their planar order) in one
+            # kernel, output in the qkv layout, which the attention reads like the first branch
             pg = K.dwconv_pw_nhwc(qkv, wdw, wpw, ks).view(B * H * W, 3 * inner)
-            self._attend(pg.view(B, H, W, 3 * inner), o[:, (i + 1) * inner:(i + 2) * inner])
+            self._attend(pg.view(B, H, W, 3 * inner), o[:, (i + 1) * inner:(i + 2) * inner], planar)
         y = F.linear(o.view(B, H, W, -1), self.w_out)
         return self.norm_out(y, res=x)
 

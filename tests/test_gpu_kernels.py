@@ -499,7 +499,7 @@ def _linear_attention_ref(q, k, v, relu):
     return num / (den + 1e-15)
 
 
-@pytest.mark.parametrize("B,N,heads", [(2, 1024, 3), (3, 300, 2), (1, 17, 1), (2, 4096, 4)])
+@pytest.mark.parametrize("B,N,heads", [(2, 1024, 3), (3, 300, 2), (1, 17, 1), (2, 4096, 4), (1, 5000, 2)])
 def test_linear_attention_separate_qkv(dev, B, N, heads):
     g = torch.Generator().manual_seed(B * N + heads)
     q, k, v = (torch.randn(B, N, heads, 32, generator=g).to(torch.bfloat16).to(dev) for _ in range(3))
@@ -573,6 +573,31 @@ def test_multiscale_linear_attention_vs_literal(dev):
         ref = m.norm_out(y.to(torch.bfloat16), res=x).float()
     rel = ((got - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
+
+
+def test_multiscale_linear_attention_planar_bitexact(dev):
+    """The planar q/k/v relabelling (w_qkv rows, depthwise channels and grouped-1x1 groups permuted
+    alike, used at >= PLANAR_MIN_TOKENS tokens) computes every value as the reference layout does:
+    bit-identical outputs; the permuted weights refresh when a parameter changes."""
+    from hyperscalees_t2i_amd.dcae import MultiscaleLinearAttention
+    torch.manual_seed(8)
+    c, B, H, W = 128, 2, 16, 24
+    m = MultiscaleLinearAttention(c).to(dev)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_((torch.randn_like(p, dtype=torch.float32) * 0.1).to(p.dtype))
+    x = torch.randn(B, H, W, c, device=dev).to(torch.bfloat16)
+    with torch.no_grad():
+        m.PLANAR_MIN_TOKENS = 1 << 30
+        ref = m(x)
+        m.PLANAR_MIN_TOKENS = 1
+        got = m(x)
+        assert torch.equal(got, ref)
+        m.ms_pw[0].mul_(0.5)
+        m.PLANAR_MIN_TOKENS = 1 << 30
+        ref2 = m(x)
+        m.PLANAR_MIN_TOKENS = 1
+        assert torch.equal(m(x), ref2) and not torch.equal(ref2, ref)
 
 
 def test_bias_act_and_resblock(dev):
