@@ -119,7 +119,7 @@ def build_var(args, world, rank, device):
     from hyperscalees_t2i_amd.rewards import RewardModels
     from hyperscalees_t2i_amd.var import VARArch
 
-    cfg = VarConfig(classes_per_gen=4, batches_per_gen=4)
+    cfg = VarConfig(classes_per_gen=4, batches_per_gen=4, synthetic_if_missing=True)
     if args.small:
         cfg.arch = VARArch(depth=2, vae_ch=32)
     backend = VarBackend(device=str(device), cfg=cfg)
@@ -127,7 +127,7 @@ def build_var(args, world, rank, device):
     params, shapes = backend.collect_lora_params()
     theta = flatten_params(params).to(device=device, dtype=torch.float32)
     noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=1, use_antithetic=True)
-    rewards = RewardModels.build(device, tiny=args.small)
+    rewards = RewardModels.build(device, tiny=args.small, synthetic=True)
     pop = args.pop_per_gpu * world
     es_cfg = ESConfig(pop_size=pop, sigma=1e-2, lr_scale=1e-1, egg_rank=1, use_antithetic=True, promptnorm=True,
                       theta_max_norm=40.0, max_step_norm=0.0)
@@ -144,7 +144,7 @@ def build(args, world, rank, device):
     from hyperscalees_t2i_amd.rewards import RewardModels
     from hyperscalees_t2i_amd.sana import SanaArch
 
-    cfg = SanaConfig(width_latent=args.latent, height_latent=args.latent)
+    cfg = SanaConfig(synthetic_weights=True, width_latent=args.latent, height_latent=args.latent)
     if args.small:
         cfg.arch = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=2,
                             cross_attention_head_dim=64, caption_channels=256)
@@ -157,7 +157,7 @@ def build(args, world, rank, device):
     params, shapes = backend.collect_lora_params()
     theta = flatten_params(params).to(device=device, dtype=torch.float32)
     noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=1, use_antithetic=True)
-    rewards = RewardModels.build(device, tiny=args.small)
+    rewards = RewardModels.build(device, tiny=args.small, synthetic=True)
     pop = args.pop_per_gpu * world
     es_cfg = ESConfig(pop_size=pop, sigma=1e-2, lr_scale=1e-1, egg_rank=1, use_antithetic=True, promptnorm=True,
                       theta_max_norm=40.0, max_step_norm=0.0)

@@ -88,6 +88,9 @@ class SanaConfig:
     lora_b_std: float = 0.02          # nonzero B so the LoRA path is live
     lora_seed: int = 1234
     weight_seed: int = 0
+    # model_name must be a local diffusers directory (transformer/ + vae/, checkpoints.py); True builds
+    # `arch` with seeded synthetic weights instead (the benchmark's throughput configuration)
+    synthetic_weights: bool = False
 
 
 def synthetic_prompt_data(P: int = 4, seq: int = 300, dim: int = 2304, seed: int = 0) -> Dict[str, Any]:
@@ -141,7 +144,7 @@ class SanaBackend(ESBackend):
         c = self.cfg
         self.es_model = SanaOneStep(c.model_name, device=self.device, DTYPE=self._dtype(), sigma_data=0.5, arch=c.arch,
                                     vae_widths=c.vae_widths, vae_layers=c.vae_layers, weight_seed=c.weight_seed,
-                                    vae_chunk=c.vae_chunk)
+                                    vae_chunk=c.vae_chunk, synthetic_weights=c.synthetic_weights)
         n = attach_lora(self.es_model.transformer, c.lora_r, c.lora_alpha, c.lora_target_modules)
         if n == 0:
             raise RuntimeError("no LoRA target module matched")
@@ -278,7 +281,7 @@ class VarConfig:
     top_k: int = 900                        # models/VAR.py:276-277 generate() defaults
     top_p: float = 0.95
     labels_path: str = "imagenet_classes.txt"
-    synthetic_if_missing: bool = True       # no checkpoint offline: seeded synthetic weights
+    synthetic_if_missing: bool = False      # True: no checkpoint in ckpt_dir -> seeded synthetic weights (explicit opt-in)
     weight_seed: int = 0
     lora_seed: int = 1234
     lora_b_std: float = 0.02

@@ -1,0 +1,338 @@
+"""Local diffusers-format checkpoints for the Sana-Sprint host (transformer + DC-AE decoder).
+
+Reference: `SanaTransformer2DModel.from_pretrained(model_name, subfolder="transformer")` and
+`AutoencoderDC.from_pretrained(model_name, subfolder="vae")` (models/SanaSprint.py:35-49).  There is
+no hub access here, so `model_name` must be a LOCAL directory laid out as diffusers writes it:
+
+    <model_name>/transformer/config.json + diffusion_pytorch_model[-0000k-of-0000n].safetensors
+    <model_name>/vae/config.json         + diffusion_pytorch_model[...].safetensors
+
+This module maps diffusers' state-dict keys onto the build's modules (sana.py / dcae.py keep the
+diffusers module names for everything on the LoRA path, so PEFT adapter keys match; the convs that
+run as libeggroll kernels keep their weights in kernel layouts and are converted here):
+
+  transformer  patch_embed.proj.weight [D, C, 1, 1]          -> patch_w [D, C]
+               transformer_blocks.i.ff.conv_inverted [2h,D,1,1] -> ff.w_inv [2h, D] (+ b_inv)
+               transformer_blocks.i.ff.conv_depth [2h,1,3,3]    -> ff.w_dw [9, 2h] ([tap][channel]) (+ b_dw)
+               transformer_blocks.i.ff.conv_point [D,h,1,1]     -> ff.w_point [D, h]
+               every other key                                  -> the same name
+  vae          decoder.up_blocks.i.j.*  -> stages.(S-1-i).j.*   (the build lists stages lowest resolution first)
+               attn.to_q / to_k / to_v  -> attn.w_qkv = cat(q, k, v) [3C, C]
+               attn.to_qkv_multiscale.s.proj_in  [3C,1,k,k]  -> attn.ms_dw.s [k*k, 3C]
+               attn.to_qkv_multiscale.s.proj_out [3C,32,1,1] -> attn.ms_pw.s [3C/32, 32, 32] ([group][out][in])
+               attn.to_out.weight       -> attn.w_out;  conv_out.conv_inverted / conv_depth / conv_point as above
+               encoder.*                -> ignored (decode only)
+
+The key names and layouts are those of diffusers' sana_transformer.py / autoencoder_dc.py as
+published; diffusers is not importable in this container and no real checkpoint exists offline, so
+the mapping is pinned only by round trips through `save_sana_diffusers` (tests/test_checkpoint_load.py)
+— PARITY WITH REAL DIFFUSERS FILES IS UNPINNED.  Loading is strict: a missing key, an unexpected key
+(outside encoder.*) or a shape mismatch raises ValueError; a configuration this build does not
+implement raises NotImplementedError.  Weights are cast to bf16 (the build's compute dtype).
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+from torch import nn
+
+from .sana import SanaArch
+
+SANA_CLASS = "SanaTransformer2DModel"
+DCAE_CLASS = "AutoencoderDC"
+WEIGHTS_NAME = "diffusion_pytorch_model.safetensors"
+WEIGHTS_INDEX = "diffusion_pytorch_model.safetensors.index.json"
+
+
+# ---------------------------------------------------------------------------------------
+# safetensors directories
+# ---------------------------------------------------------------------------------------
+
+
+def read_state_dir(d: Path) -> Dict[str, torch.Tensor]:
+    """All tensors of a diffusers weights directory (single file, or sharded with an index)."""
+    from safetensors.torch import load_file
+    d = Path(d)
+    if (d / WEIGHTS_NAME).is_file():
+        return load_file(str(d / WEIGHTS_NAME))
+    if (d / WEIGHTS_INDEX).is_file():
+        index = json.loads((d / WEIGHTS_INDEX).read_text())
+        out: Dict[str, torch.Tensor] = {}
+        for shard in sorted(set(index["weight_map"].values())):
+            out.update(load_file(str(d / shard)))
+        missing = set(index["weight_map"]) - set(out)
+        if missing:
+            raise ValueError(f"{d}: index names tensors absent from its shards: {sorted(missing)[:3]}")
+        return out
+    files = sorted(d.glob("*.safetensors"))
+    if len(files) == 1:
+        return load_file(str(files[0]))
+    raise FileNotFoundError(f"{d}: no {WEIGHTS_NAME} (or index) found")
+
+
+def write_state_dir(d: Path, state: Dict[str, torch.Tensor], config: dict) -> None:
+    from safetensors.torch import save_file
+    d = Path(d)
+    d.mkdir(parents=True, exist_ok=True)
+    save_file({k: v.detach().cpu().contiguous() for k, v in state.items()}, str(d / WEIGHTS_NAME))
+    (d / "config.json").write_text(json.dumps(config, indent=2))
+
+
+def read_config(d: Path) -> dict:
+    p = Path(d) / "config.json"
+    if not p.is_file():
+        raise FileNotFoundError(f"{p} not found")
+    return json.loads(p.read_text())
+
+
+# ---------------------------------------------------------------------------------------
+# key rules: build parameter <- diffusers tensors
+# ---------------------------------------------------------------------------------------
+
+Rule = Tuple[str, List[str], Callable[[List[torch.Tensor]], torch.Tensor], Callable[[torch.Tensor], List[torch.Tensor]]]
+
+
+def _same(name: str, dkey: Optional[str] = None) -> Rule:
+    return (name, [dkey or name], lambda ts: ts[0], lambda t: [t])
+
+
+def _conv1x1(name: str, dkey: str) -> Rule:
+    return (name, [dkey], lambda ts: ts[0].reshape(ts[0].shape[0], -1),
+            lambda t: [t.reshape(t.shape[0], t.shape[1], 1, 1)])
+
+
+def _depthwise(name: str, dkey: str) -> Rule:
+    """[C, 1, k, k] depthwise conv weight <-> the build's [k*k, C] ([tap][channel])."""
+    def to_b(ts):
+        w = ts[0]
+        return w.reshape(w.shape[0], -1).t()
+
+    def from_b(t):
+        k2, C = t.shape
+        k = int(round(k2 ** 0.5))
+        return [t.t().reshape(C, 1, k, k)]
+    return (name, [dkey], to_b, from_b)
+
+
+def _grouped32(name: str, dkey: str) -> Rule:
+    """[3C, 32, 1, 1] grouped 1x1 conv (groups of 32) <-> the build's [3C/32, 32 out, 32 in]."""
+    return (name, [dkey], lambda ts: ts[0].reshape(-1, 32, 32),
+            lambda t: [t.reshape(-1, 32, 1, 1)])
+
+
+def _qkv(name: str, prefix: str) -> Rule:
+    keys = [f"{prefix}.to_q.weight", f"{prefix}.to_k.weight", f"{prefix}.to_v.weight"]
+    return (name, keys, lambda ts: torch.cat(ts, 0), lambda t: list(t.chunk(3, 0)))
+
+
+def _frozen_params(model: nn.Module) -> Dict[str, nn.Parameter]:
+    return {n: p for n, p in model.named_parameters() if not p.requires_grad}
+
+
+def sana_rules(model: nn.Module) -> List[Rule]:
+    rules: List[Rule] = []
+    for n in _frozen_params(model):
+        if n == "patch_w":
+            rules.append(_conv1x1(n, "patch_embed.proj.weight"))
+        elif n == "patch_b":
+            rules.append(_same(n, "patch_embed.proj.bias"))
+        elif ".ff." in n:
+            pre, leaf = n.rsplit(".", 1)
+            rules.append({"w_inv": lambda: _conv1x1(n, f"{pre}.conv_inverted.weight"),
+                          "b_inv": lambda: _same(n, f"{pre}.conv_inverted.bias"),
+                          "w_dw": lambda: _depthwise(n, f"{pre}.conv_depth.weight"),
+                          "b_dw": lambda: _same(n, f"{pre}.conv_depth.bias"),
+                          "w_point": lambda: _conv1x1(n, f"{pre}.conv_point.weight")}[leaf]())
+        else:
+            rules.append(_same(n))
+    return rules
+
+
+def dcae_rules(vae: nn.Module) -> List[Rule]:
+    S = len(vae.stages)
+    rules: List[Rule] = []
+    for n in _frozen_params(vae):
+        if n.startswith("stages."):
+            _, s, rest = n.split(".", 2)
+            dn = f"decoder.up_blocks.{S - 1 - int(s)}.{rest}"
+        else:
+            dn = f"decoder.{n}"
+        blk, _, leaf = dn.rpartition(".")
+        if blk.endswith(".attn") and leaf == "w_qkv":
+            rules.append(_qkv(n, blk))
+        elif blk.endswith(".attn") and leaf == "w_out":
+            rules.append(_same(n, f"{blk}.to_out.weight"))
+        elif ".attn.ms_dw." in dn:
+            pre, s_ = dn.split(".ms_dw.")
+            rules.append(_depthwise(n, f"{pre}.to_qkv_multiscale.{s_}.proj_in.weight"))
+        elif ".attn.ms_pw." in dn:
+            pre, s_ = dn.split(".ms_pw.")
+            rules.append(_grouped32(n, f"{pre}.to_qkv_multiscale.{s_}.proj_out.weight"))
+        elif blk.endswith(".conv_out") and leaf in ("w_inv", "b_inv", "w_dw", "b_dw", "w_point"):
+            rules.append({"w_inv": lambda: _conv1x1(n, f"{blk}.conv_inverted.weight"),
+                          "b_inv": lambda: _same(n, f"{blk}.conv_inverted.bias"),
+                          "w_dw": lambda: _depthwise(n, f"{blk}.conv_depth.weight"),
+                          "b_dw": lambda: _same(n, f"{blk}.conv_depth.bias"),
+                          "w_point": lambda: _conv1x1(n, f"{blk}.conv_point.weight")}[leaf]())
+        else:
+            rules.append(_same(n, dn))
+    return rules
+
+
+def state_from_build(model: nn.Module, rules: Sequence[Rule]) -> Dict[str, torch.Tensor]:
+    params = _frozen_params(model)
+    out: Dict[str, torch.Tensor] = {}
+    for name, dkeys, _, from_b in rules:
+        for k, t in zip(dkeys, from_b(params[name].detach())):
+            out[k] = t.contiguous()
+    return out
+
+
+@torch.no_grad()
+def load_into(model: nn.Module, rules: Sequence[Rule], state: Dict[str, torch.Tensor], what: str,
+              ignore_prefixes: Sequence[str] = ()) -> None:
+    """Strict: every build parameter from its diffusers tensors (shape-checked, cast to the
+    parameter's dtype); any checkpoint key no rule reads raises (except ignore_prefixes)."""
+    params = _frozen_params(model)
+    used = set()
+    missing = [k for _, dk, _, _ in rules for k in dk if k not in state]
+    if missing:
+        raise ValueError(f"{what}: checkpoint lacks {len(missing)} keys, e.g. {missing[:4]}")
+    for name, dkeys, to_b, _ in rules:
+        t = to_b([state[k] for k in dkeys])
+        p = params[name]
+        if tuple(t.shape) != tuple(p.shape):
+            raise ValueError(f"{what}: {dkeys[0]} gives {tuple(t.shape)} for {name} {tuple(p.shape)}")
+        p.copy_(t.to(device=p.device, dtype=p.dtype))
+        used.update(dkeys)
+    extra = sorted(k for k in state if k not in used and not k.startswith(tuple(ignore_prefixes)))
+    if extra:
+        raise ValueError(f"{what}: {len(extra)} checkpoint keys are not used by this build, e.g. {extra[:4]}")
+
+
+# ---------------------------------------------------------------------------------------
+# configs
+# ---------------------------------------------------------------------------------------
+
+
+def sana_arch_from_config(cfg: dict) -> SanaArch:
+    """diffusers SanaTransformer2DModel config.json -> SanaArch; refuses what sana.py does not build."""
+    if cfg.get("_class_name", SANA_CLASS) != SANA_CLASS:
+        raise NotImplementedError(f"transformer class {cfg.get('_class_name')!r} (expected {SANA_CLASS})")
+    need = {"patch_size": 1, "guidance_embeds": True, "qk_norm": "rms_norm_across_heads", "attention_bias": False,
+            "norm_elementwise_affine": False, "interpolation_scale": None}
+    for k, v in need.items():
+        if k in cfg and cfg[k] != v:
+            raise NotImplementedError(f"transformer config {k}={cfg[k]!r}: this build implements {v!r}")
+    if float(cfg.get("timestep_scale", 1.0) or 1.0) != 1.0 or float(cfg.get("dropout", 0.0) or 0.0) != 0.0:
+        raise NotImplementedError("transformer config: timestep_scale != 1 / dropout != 0 are not implemented")
+    a = SanaArch(in_channels=int(cfg.get("in_channels", 32)),
+                 out_channels=int(cfg.get("out_channels") or cfg.get("in_channels", 32)),
+                 num_attention_heads=int(cfg.get("num_attention_heads", 70)),
+                 attention_head_dim=int(cfg.get("attention_head_dim", 32)),
+                 num_layers=int(cfg.get("num_layers", 20)),
+                 num_cross_attention_heads=int(cfg.get("num_cross_attention_heads", 20)),
+                 cross_attention_head_dim=int(cfg.get("cross_attention_head_dim", 112)),
+                 caption_channels=int(cfg.get("caption_channels", 2304)),
+                 mlp_ratio=float(cfg.get("mlp_ratio", 2.5)),
+                 norm_eps=float(cfg.get("norm_eps", 1e-6)),
+                 guidance_embeds_scale=float(cfg.get("guidance_embeds_scale", 0.1)),
+                 sample_size=int(cfg.get("sample_size", 32)))
+    if int(cfg.get("cross_attention_dim", a.inner_dim)) != a.inner_dim:
+        raise NotImplementedError("transformer config: cross_attention_dim != inner dim")
+    return a
+
+
+def sana_config_from_arch(a: SanaArch) -> dict:
+    return {"_class_name": SANA_CLASS, "in_channels": a.in_channels, "out_channels": a.out_channels,
+            "num_attention_heads": a.num_attention_heads, "attention_head_dim": a.attention_head_dim,
+            "num_layers": a.num_layers, "num_cross_attention_heads": a.num_cross_attention_heads,
+            "cross_attention_head_dim": a.cross_attention_head_dim, "cross_attention_dim": a.inner_dim,
+            "caption_channels": a.caption_channels, "mlp_ratio": a.mlp_ratio, "dropout": 0.0,
+            "attention_bias": False, "sample_size": a.sample_size, "patch_size": 1,
+            "norm_elementwise_affine": False, "norm_eps": a.norm_eps, "interpolation_scale": None,
+            "guidance_embeds": True, "guidance_embeds_scale": a.guidance_embeds_scale,
+            "qk_norm": "rms_norm_across_heads", "timestep_scale": 1.0}
+
+
+def dcae_build_kwargs(cfg: dict) -> dict:
+    """diffusers AutoencoderDC config.json -> DCAEDecoder kwargs (decoder side only)."""
+    if cfg.get("_class_name", DCAE_CLASS) != DCAE_CLASS:
+        raise NotImplementedError(f"vae class {cfg.get('_class_name')!r} (expected {DCAE_CLASS})")
+    widths = [int(w) for w in cfg["decoder_block_out_channels"]]
+    layers = [int(x) for x in cfg["decoder_layers_per_block"]]
+    n = len(widths)
+
+    def per_stage(v, default):
+        v = cfg.get(v, default)
+        return [v] * n if isinstance(v, str) or not isinstance(v, (list, tuple)) else list(v)
+    types = per_stage("decoder_block_types", "ResBlock")
+    norms = per_stage("decoder_norm_types", "rms_norm")
+    acts = per_stage("decoder_act_fns", "silu")
+    ms = cfg.get("decoder_qkv_multiscales", [[]] * n)
+    vit_from = next((i for i, t in enumerate(types) if t == "EfficientViTBlock"), n)
+    ok = (all(t == ("ResBlock" if i < vit_from else "EfficientViTBlock") for i, t in enumerate(types))
+          and all(x == "rms_norm" for x in norms) and all(x == "silu" for x in acts[:vit_from])
+          and all(list(ms[i]) == ([5] if i >= vit_from else []) for i in range(n))
+          and cfg.get("upsample_block_type", "interpolate") == "interpolate"
+          and int(cfg.get("attention_head_dim", 32)) == 32 and int(cfg.get("in_channels", 3)) == 3
+          and layers[0] > 0 and all(x > 0 for x in layers))
+    if not ok:
+        raise NotImplementedError("vae config: this build implements the DC-AE f32c32 decoder family only "
+                                  "(ResBlocks then EfficientViT blocks with multiscale (5,), rms_norm, silu, "
+                                  "interpolate up-blocks, head dim 32)")
+    return dict(latent_channels=int(cfg.get("latent_channels", 32)), widths=tuple(widths), layers=tuple(layers),
+                vit_from=vit_from, scaling_factor=float(cfg.get("scaling_factor", 0.41407)))
+
+
+def dcae_config_from_build(vae: nn.Module) -> dict:
+    widths, layers, vit_from = vae.widths, vae.layers, vae.vit_from
+    n = len(widths)
+    return {"_class_name": DCAE_CLASS, "in_channels": 3, "latent_channels": vae.latent_channels,
+            "attention_head_dim": 32, "decoder_block_out_channels": list(widths),
+            "decoder_layers_per_block": list(layers),
+            "decoder_block_types": ["ResBlock" if i < vit_from else "EfficientViTBlock" for i in range(n)],
+            "decoder_norm_types": "rms_norm", "decoder_act_fns": "silu",
+            "decoder_qkv_multiscales": [[] if i < vit_from else [5] for i in range(n)],
+            "upsample_block_type": "interpolate", "scaling_factor": vae.scaling_factor}
+
+
+# ---------------------------------------------------------------------------------------
+# whole-model load / save
+# ---------------------------------------------------------------------------------------
+
+
+def is_local_model_dir(model_name: str) -> bool:
+    p = Path(model_name)
+    return p.is_dir() and (p / "transformer").is_dir() and (p / "vae").is_dir()
+
+
+def load_sana_transformer(model, d: Path) -> None:
+    load_into(model, sana_rules(model), read_state_dir(d), f"{d} (transformer)")
+
+
+def load_dcae_decoder(vae, d: Path) -> None:
+    load_into(vae, dcae_rules(vae), read_state_dir(d), f"{d} (vae)", ignore_prefixes=("encoder.",))
+    refresh_dcae_caches(vae)
+
+
+def refresh_dcae_caches(vae) -> None:
+    """The kernel-layout copies the decoder derives from its 3x3 weights (phase / packed weights)."""
+    from .dcae import ResBlock, UpBlock
+    for m in vae.modules():
+        if isinstance(m, UpBlock):
+            m.refresh_phase_weights()
+        if isinstance(m, ResBlock):
+            m.refresh_packed_weights()
+
+
+def save_sana_diffusers(transformer, vae, out_dir: Path) -> None:
+    """Write the build's frozen weights as a diffusers model directory (transformer/ + vae/, decoder
+    keys only): the inverse of the loader, used by the round-trip tests and for exporting."""
+    out = Path(out_dir)
+    write_state_dir(out / "transformer", state_from_build(transformer, sana_rules(transformer)),
+                    sana_config_from_arch(transformer.config))
+    write_state_dir(out / "vae", state_from_build(vae, dcae_rules(vae)), dcae_config_from_build(vae))

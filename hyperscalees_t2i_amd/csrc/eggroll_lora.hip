@@ -2567,6 +2567,8 @@ int eggroll_lora_project_multi(const void* X, int64_t ldx, const float* theta_po
     EGG_CHECK_ARG(rows_per_member > 0 && ld_theta % 4 == 0, "lora_project_multi: bad rows_per_member / ld_theta");
     if (M == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(X && theta_pop && T && offA_host, "lora_project_multi: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)X & 15) == 0 && ((uintptr_t)theta_pop & 15) == 0,
+                  "lora_project_multi: X and theta_pop must be 16-byte aligned (16-byte vector loads)");
     int64_t off[4] = {0, 0, 0, 0};
     for (int l = 0; l < n_lin; ++l) {
         off[l] = offA_host[l];

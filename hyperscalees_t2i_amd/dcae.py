@@ -276,6 +276,7 @@ class DCAEDecoder(nn.Module):
         super().__init__()
         self.scaling_factor = scaling_factor
         self.latent_channels = latent_channels
+        self.widths, self.layers, self.vit_from = tuple(widths), tuple(layers), vit_from
         self.conv_in = Conv3x3(latent_channels, widths[-1])
         self.in_repeats = widths[-1] // latent_channels
         stages = []

@@ -223,8 +223,8 @@ def shared_projection(mods: Sequence[LoRALinear], x: torch.Tensor) -> List[Optio
             or Kd % 32 or Kd > 4096):
         return none
     x2 = x.reshape(-1, Kd)
-    if x2.dtype != torch.bfloat16 or not x2.is_contiguous():
-        return none
+    if x2.dtype != torch.bfloat16 or not x2.is_contiguous() or x2.data_ptr() % 16 or ctx.theta_pop.data_ptr() % 16:
+        return none   # the multi-projection kernel issues 16-byte vector loads of X and theta_pop
     M = x2.shape[0]
     if M % ctx.n_members:
         raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")

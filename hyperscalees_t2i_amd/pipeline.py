@@ -15,6 +15,7 @@ Common random numbers: every member uses the same latents (seed = epoch) and pro
 from __future__ import annotations
 
 import math
+from pathlib import Path
 from typing import Any, List, Optional
 
 import torch
@@ -43,17 +44,43 @@ class ESBaseModel:
 
 
 class SanaOneStep(ESBaseModel):
+    """models/SanaSprint.py:10-60.  Weights: `model_name` is a LOCAL diffusers-format directory
+    (transformer/ + vae/, loaded by checkpoints.py; the architecture comes from its config.json files,
+    `arch` / `vae_*` are ignored), or — only with synthetic_weights=True — anything, in which case
+    the given architecture is built with seeded synthetic weights (throughput runs).
+    Anything else raises FileNotFoundError: there is no hub access, and silently substituting random
+    weights for a named checkpoint would produce plausible-looking but meaningless numbers."""
+
     def __init__(self, model_name: str = "Efficient-Large-Model/Sana_Sprint_1.6B_1024px_diffusers",
                  device: str = "cuda:0", DTYPE: torch.dtype = torch.float16, sigma_data: float = 0.5,
                  arch: SanaArch = SANA_SPRINT_1_6B, vae_widths=(128, 256, 512, 512, 1024, 1024),
-                 vae_layers=(3, 3, 3, 3, 3, 3), weight_seed: int = 0, vae_chunk: int = 8):
+                 vae_layers=(3, 3, 3, 3, 3, 3), weight_seed: int = 0, vae_chunk: int = 8,
+                 synthetic_weights: bool = False):
+        from . import checkpoints as C
         super().__init__(model_name, device, DTYPE, sigma_data)
         dev = torch.device(device)
-        with torch.device(dev):
-            self.transformer = SanaTransformer2DModel(arch)
-            self.vae = DCAEDecoder(arch.in_channels, widths=vae_widths, layers=vae_layers)
-        self.transformer.init_weights(weight_seed)
-        self.vae.init_weights(weight_seed + 1)
+        root = Path(str(model_name))
+        if C.is_local_model_dir(str(model_name)):
+            arch = C.sana_arch_from_config(C.read_config(root / "transformer"))
+            vkw = C.dcae_build_kwargs(C.read_config(root / "vae"))
+            with torch.device(dev):
+                self.transformer = SanaTransformer2DModel(arch)
+                self.vae = DCAEDecoder(**vkw)
+            C.load_sana_transformer(self.transformer, root / "transformer")
+            C.load_dcae_decoder(self.vae, root / "vae")
+            self.weights_source = str(root)
+        elif synthetic_weights:
+            with torch.device(dev):
+                self.transformer = SanaTransformer2DModel(arch)
+                self.vae = DCAEDecoder(arch.in_channels, widths=vae_widths, layers=vae_layers)
+            self.transformer.init_weights(weight_seed)
+            self.vae.init_weights(weight_seed + 1)
+            self.weights_source = f"synthetic(seed={weight_seed})"
+        else:
+            why = ("exists but lacks transformer/ or vae/" if root.exists()
+                   else "is not a local directory (no hub downloads offline)")
+            raise FileNotFoundError(f"SanaOneStep: model_name {str(model_name)!r} {why}; pass a local diffusers "
+                                    f"model directory, or synthetic_weights=True for seeded random weights")
         self.transformer_config = arch
         self.vae_chunk = vae_chunk
         self.ctx = PopulationContext()

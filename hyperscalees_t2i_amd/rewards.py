@@ -14,18 +14,25 @@ processor (PIL backend): Pillow's fixed-point bicubic resize of the shortest edg
 crop -> /255 -> CLIP mean/std normalisation.  Done here as tensor ops on the device, bit-exact
 with Pillow's resampling (tests/test_checkpoint_rewards.py).
 
-Weights: the hub checkpoints (openai/clip-vit-base-patch32, yuvalkirstain/PickScore_v1) are not
-available offline, so both models are built from their published configs with seeded random
-init (architecture- and FLOP-exact, scores meaningless); tokenisation is a deterministic
-synthetic word hash (no CLIP BPE vocab offline).  Reward-value parity is therefore UNPINNED;
-the reward *contract* (dict keys, per-image scalars, combination, S aggregation) is exact.
+Weights (rewards.py:32-60 loads openai/clip-vit-base-patch32 and yuvalkirstain/PickScore_v1 + the
+laion CLIP-ViT-H-14 processor by hub name): `RewardModels.build(clip_path=..., pickscore_path=...)`
+loads LOCAL copies of those repos with transformers (`CLIPModel.from_pretrained(local_files_only)`,
+the CLIP BPE tokenizer from the directory's vocab.json / merges.txt or tokenizer.json, and its
+preprocessor_config.json, checked against what the device preprocessing implements).  Without
+local weights (none exist in this container) `synthetic=True` builds both models from their
+published configs with seeded random init (architecture- and FLOP-exact, scores meaningless) and
+tokenises with a deterministic word hash; anything else raises FileNotFoundError.  Reward-value
+parity is UNPINNED (no real weights here); the reward *contract* (dict keys, per-image scalars,
+combination, S aggregation) is exact.
 """
 from __future__ import annotations
 
 import ctypes
+import json
 import zlib
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence, Tuple
+from pathlib import Path
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -169,7 +176,8 @@ def pil_tap_table(in_size: int, out_size: int, device) -> Tuple[torch.Tensor, in
     return _TAP_CACHE[key]
 
 
-def clip_pixels(images: torch.Tensor, pil_mode: int = 0, size: int = 224) -> torch.Tensor:
+def clip_pixels(images: torch.Tensor, pil_mode: int = 0, size: int = 224, mean: Sequence[float] = CLIP_MEAN,
+                std: Sequence[float] = CLIP_STD) -> torch.Tensor:
     """Decoder images [n,3,H,W] (bf16, any strides) -> CLIP pixel values [n,3,size,size] fp32 on the
     HIP path (eggroll_clip_preprocess): the uint8 PIL conversion of the backend (pil_mode 0: PixArt
     postprocess, rounding; 1: the VAR PIL path, fp16 + truncation), Pillow's bicubic resize of the
@@ -187,13 +195,78 @@ def clip_pixels(images: torch.Tensor, pil_mode: int = 0, size: int = 224) -> tor
     th, kth = pil_tap_table(h, nh, images.device)
     out = torch.empty((n, 3, size, size), dtype=torch.float32, device=images.device)
     tmp = torch.empty((max(n * 3 * h * size, 1),), dtype=torch.uint8, device=images.device)
-    mean = (ctypes.c_float * 3)(*CLIP_MEAN)
-    std = (ctypes.c_float * 3)(*CLIP_STD)
+    mean = (ctypes.c_float * 3)(*mean)
+    std = (ctypes.c_float * 3)(*std)
     sn, sc, sh, sw = images.stride()
     _lib.call("eggroll_clip_preprocess", images.data_ptr(), n, h, w, sn, sc, sh, sw, int(pil_mode), tw.data_ptr(),
               th.data_ptr(), ktw, kth, nw, nh, size, ctypes.cast(mean, ctypes.c_void_p),
               ctypes.cast(std, ctypes.c_void_p), tmp.data_ptr(), out.data_ptr(), _stream(images.device))
     return out
+
+
+class ClipTokenizer:
+    """The CLIP BPE tokenizer of a local model / processor directory (vocab.json + merges.txt or
+    tokenizer.json), called as the reference's processors are (rewards.py:87, 131-137: truncation at
+    77 tokens) but always padded to 77: the text towers are causal and read the [EOS] position, so
+    padding past it does not change the features, and a fixed shape lets the text graph replay."""
+
+    def __init__(self, path, max_length: int = 77):
+        from transformers import AutoTokenizer
+        p = Path(path)
+        if not ((p / "vocab.json").is_file() and (p / "merges.txt").is_file()) and not (p / "tokenizer.json").is_file():
+            raise FileNotFoundError(f"{p}: no CLIP tokenizer files (vocab.json + merges.txt or tokenizer.json)")
+        self.tok = AutoTokenizer.from_pretrained(str(p), local_files_only=True)
+        self.max_length = max_length
+        self.path = str(p)
+
+    def __call__(self, texts: Sequence[str]) -> Tuple[torch.Tensor, torch.Tensor]:
+        enc = self.tok(list(texts), padding="max_length", truncation=True, max_length=self.max_length,
+                       return_tensors="pt")
+        return enc["input_ids"].long(), enc["attention_mask"].long()
+
+
+@dataclass(frozen=True)
+class PixelSpec:
+    """What eggroll_clip_preprocess does for one reward model: short edge -> size (Pillow bicubic),
+    center crop size x size, /255, (x - mean) / std."""
+    size: int = 224
+    mean: Tuple[float, float, float] = CLIP_MEAN
+    std: Tuple[float, float, float] = CLIP_STD
+
+
+def pixel_spec_from_processor(path) -> PixelSpec:
+    """A CLIPImageProcessor preprocessor_config.json -> PixelSpec; NotImplementedError for anything
+    the device preprocessing does not restate (it is bit-exact for exactly this pipeline)."""
+    p = Path(path) / "preprocessor_config.json"
+    if not p.is_file():
+        raise FileNotFoundError(f"{p} not found")
+    c = json.loads(p.read_text())
+    size = c.get("size", {})
+    short = size.get("shortest_edge") if isinstance(size, dict) else size
+    crop = c.get("crop_size", short)
+    crop = (crop.get("height"), crop.get("width")) if isinstance(crop, dict) else (crop, crop)
+    ok = (c.get("do_resize", True) and c.get("do_center_crop", True) and c.get("do_rescale", True)
+          and c.get("do_normalize", True) and int(c.get("resample", 3)) == 3 and short is not None
+          and crop == (short, short) and abs(float(c.get("rescale_factor", 1 / 255)) - 1 / 255) < 1e-12)
+    if not ok:
+        raise NotImplementedError(f"{p}: only the CLIP pipeline (bicubic short-edge resize, square center crop "
+                                  f"of the same size, /255, mean/std) is implemented on the device")
+    return PixelSpec(int(short), tuple(float(x) for x in c.get("image_mean", CLIP_MEAN)),
+                     tuple(float(x) for x in c.get("image_std", CLIP_STD)))
+
+
+def load_clip(path, device, dtype=torch.bfloat16):
+    """A local transformers CLIPModel directory (openai/clip-vit-base-patch32, yuvalkirstain/PickScore_v1
+    layouts) -> (model in `dtype`, fp32 _TextOnly copy of its text tower taken BEFORE the cast)."""
+    import copy
+    from transformers import CLIPModel
+    p = Path(path)
+    if not (p / "config.json").is_file():
+        raise FileNotFoundError(f"{p}: not a local CLIPModel directory (config.json missing; no hub downloads)")
+    m32 = CLIPModel.from_pretrained(str(p), local_files_only=True, dtype=torch.float32)
+    text32 = _TextOnly(copy.deepcopy(m32.text_model).to(device).eval().requires_grad_(False),
+                       copy.deepcopy(m32.text_projection).to(device).eval().requires_grad_(False))
+    return m32.to(device=device, dtype=dtype).eval().requires_grad_(False), text32
 
 
 def build_clip(cfg: dict, device, seed: int, dtype=torch.bfloat16):
@@ -239,6 +312,11 @@ class RewardModels:
     image_batch: int = 256
     fp32_residual: bool = True     # towers carry their residual stream / norms in fp32 (clip_tower.py)
     text_graphs: bool = True       # replay the per-epoch text towers as one HIP graph per prompt count
+    clip_tok: Optional[Callable] = None   # texts -> (ids, mask); None: synthetic_tokenize (synthetic models)
+    pick_tok: Optional[Callable] = None
+    clip_px: PixelSpec = PixelSpec()
+    pick_px: PixelSpec = PixelSpec()
+    source: str = "synthetic"
     _towers: Optional[tuple] = None
     _text32: Optional[tuple] = None
     _tgraphs: Optional[dict] = None
@@ -253,7 +331,7 @@ class RewardModels:
     def text_models(self):
         """The text towers + projections the prompt features come from: fp32 copies (once per epoch
         for a handful of prompts, so the reference's fp32 precision costs nothing) unless the towers
-        run in plain bf16."""
+        run in plain bf16.  Loaded checkpoints keep the fp32 copies taken before the bf16 cast."""
         if not self.fp32_residual:
             return self.clip, self.pick
         if self._text32 is None:
@@ -263,42 +341,86 @@ class RewardModels:
         return self._text32
 
     @classmethod
-    def build(cls, device, mix_weights=(0.0, 0.0, 0.0, 1.0), tiny: bool = False, seed: int = 7):
+    def build(cls, device, mix_weights=(0.0, 0.0, 0.0, 1.0), tiny: bool = False, seed: int = 7,
+              clip_path: Optional[str] = None, pickscore_path: Optional[str] = None,
+              pickscore_processor_path: Optional[str] = None, synthetic: bool = False):
+        """rewards.py:32-60.  clip_path / pickscore_path: local copies of openai/clip-vit-base-patch32 and
+        yuvalkirstain/PickScore_v1 (CLIPModel directories); pickscore_processor_path: the local
+        laion/CLIP-ViT-H-14-laion2B-s32B-b79K processor (tokenizer + preprocessor_config) the reference
+        pairs with PickScore — default: the PickScore directory's own files, else the CLIP-B/32
+        tokenizer (the same BPE vocabulary).  Without local weights, synthetic=True (or tiny=True, the
+        test-size config) builds seeded random towers; otherwise FileNotFoundError."""
         split_mix_weights(mix_weights)
+        if clip_path is not None or pickscore_path is not None:
+            if clip_path is None or pickscore_path is None:
+                raise ValueError("RewardModels.build: pass both clip_path and pickscore_path")
+            clip, t_clip = load_clip(clip_path, device)
+            pick, t_pick = load_clip(pickscore_path, device)
+            clip_tok = ClipTokenizer(clip_path)
+            proc = pickscore_processor_path or pickscore_path
+            try:
+                pick_tok = ClipTokenizer(proc)
+            except FileNotFoundError:
+                if pickscore_processor_path is not None:
+                    raise
+                pick_tok = clip_tok
+            pick_px_dir = proc if (Path(proc) / "preprocessor_config.json").is_file() else clip_path
+            rm = cls(clip=clip, pick=pick, mix_weights=tuple(mix_weights), clip_tok=clip_tok, pick_tok=pick_tok,
+                     clip_px=pixel_spec_from_processor(clip_path), pick_px=pixel_spec_from_processor(pick_px_dir),
+                     source=f"local({clip_path}, {pickscore_path})")
+            rm._text32 = (t_clip, t_pick)
+            return rm
+        if not (synthetic or tiny):
+            raise FileNotFoundError("RewardModels.build: no local CLIP / PickScore weights given (clip_path, "
+                                    "pickscore_path; no hub downloads offline) — pass synthetic=True for seeded "
+                                    "random towers")
         clip = build_clip(CLIP_TINY if tiny else CLIP_B32, device, seed)
         pick = build_clip(CLIP_TINY if tiny else CLIP_H14, device, seed + 1)
-        return cls(clip=clip, pick=pick, mix_weights=tuple(mix_weights))
+        return cls(clip=clip, pick=pick, mix_weights=tuple(mix_weights), source=f"synthetic(seed={seed})")
 
-    def _text_eager(self, ids: torch.Tensor, mask: torch.Tensor) -> Dict[str, torch.Tensor]:
+    def tokenize(self, prompts: Sequence[str]):
+        """(clip ids, clip mask) of [AESTHETIC, NEGATIVE, *prompts] and (pick ids, pick mask) of prompts."""
+        texts = [AESTHETIC_TEXT, NEGATIVE_TEXT] + list(prompts)
+        if self.clip_tok is None:
+            ids, mask = synthetic_tokenize(texts)
+            return ids, mask, ids[2:], mask[2:]
+        ids_c, mask_c = self.clip_tok(texts)
+        ids_p, mask_p = self.pick_tok(list(prompts))
+        return ids_c, mask_c, ids_p, mask_p
+
+    def _text_eager(self, ids_c, mask_c, ids_p, mask_p) -> Dict[str, torch.Tensor]:
         tc_model, tp_model = self.text_models()
-        t_clip = _text_features(tc_model, ids, mask)
+        t_clip = _text_features(tc_model, ids_c, mask_c)
         t_clip = t_clip / t_clip.norm(dim=-1, keepdim=True).clamp_min(1e-6)   # rewards.py:100
-        t_pick = _text_features(tp_model, ids[2:], mask[2:])
+        t_pick = _text_features(tp_model, ids_p, mask_p)
         t_pick = t_pick / t_pick.norm(dim=-1, keepdim=True)                   # rewards.py:153
         return {"clip_aes": t_clip[0], "clip_neg": t_clip[1], "clip_prompt": t_clip[2:], "pick_prompt": t_pick}
 
-    def _text_graphed(self, ids: torch.Tensor, mask: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """The same kernels as _text_eager, captured once per prompt count into a HIP graph and replayed:
-        the fp32 text towers are ~690 small launches per epoch whose host-side dispatch (not their
-        7.5 ms of GPU work) set the pace.  The inputs are copied into the graph's static buffers."""
+    def _text_graphed(self, *toks) -> Dict[str, torch.Tensor]:
+        """The same kernels as _text_eager, captured once per (token shapes, tower precision) into a HIP
+        graph and replayed: the fp32 text towers are ~690 small launches per epoch whose host-side
+        dispatch (not their 7.5 ms of GPU work) set the pace.  The inputs are copied into the graph's
+        static buffers.  The key includes fp32_residual: a graph captured on the fp32 text towers must
+        not be replayed after a switch to the bf16 ones."""
         if self._tgraphs is None:
             self._tgraphs = {}
-        key = tuple(ids.shape)
+        key = (tuple(tuple(t.shape) for t in toks), bool(self.fp32_residual))
         ent = self._tgraphs.get(key)
+        dev = toks[0].device
         if ent is None:
-            sid, smask = ids.clone(), mask.clone()
-            side = torch.cuda.Stream(device=ids.device)
-            side.wait_stream(torch.cuda.current_stream(ids.device))
+            static = [t.clone() for t in toks]
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
-                self._text_eager(sid, smask)   # warm-up off the capture (library handles, kernel selection)
-            torch.cuda.current_stream(ids.device).wait_stream(side)
+                self._text_eager(*static)   # warm-up off the capture (library handles, kernel selection)
+            torch.cuda.current_stream(dev).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                out = self._text_eager(sid, smask)
-            ent = self._tgraphs[key] = (graph, sid, smask, out)
-        graph, sid, smask, out = ent
-        sid.copy_(ids)
-        smask.copy_(mask)
+                out = self._text_eager(*static)
+            ent = self._tgraphs[key] = (graph, static, out)
+        graph, static, out = ent
+        for dst, src in zip(static, toks):
+            dst.copy_(src)
         graph.replay()
         return {k: v.clone() for k, v in out.items()}
 
@@ -306,15 +428,14 @@ class RewardModels:
     def prompt_features(self, prompts: Sequence[str]) -> Dict[str, torch.Tensor]:
         """Text features once per epoch (members share prompts: common random numbers)."""
         dev = next(self.clip.parameters()).device
-        ids, mask = synthetic_tokenize([AESTHETIC_TEXT, NEGATIVE_TEXT] + list(prompts))
-        ids, mask = ids.to(dev), mask.to(dev)
+        toks = [t.to(dev) for t in self.tokenize(prompts)]
         if self.text_graphs and dev.type == "cuda":
             try:
-                return self._text_graphed(ids, mask)
+                return self._text_graphed(*toks)
             except RuntimeError:   # a capture-incompatible op: run the same towers eagerly from now on
                 torch.cuda.synchronize(dev)
                 self.text_graphs, self._tgraphs = False, None
-        return self._text_eager(ids, mask)
+        return self._text_eager(*toks)
 
     @torch.no_grad()
     def score(self, images: torch.Tensor, prompt_index: torch.Tensor, feats: Dict[str, torch.Tensor],
@@ -325,10 +446,14 @@ class RewardModels:
         compute_all_rewards keys."""
         n = images.shape[0]
         t_clip, t_pick = self.towers()
+        same_px = self.clip_px == self.pick_px
         e_clip, e_pick = [], []
         for s in range(0, n, self.image_batch):
-            px = clip_pixels(images[s:s + self.image_batch].to(torch.bfloat16), pil_mode)
+            im = images[s:s + self.image_batch].to(torch.bfloat16)
+            px = clip_pixels(im, pil_mode, self.clip_px.size, self.clip_px.mean, self.clip_px.std)
             e_clip.append(t_clip(px))
+            if not same_px:
+                px = clip_pixels(im, pil_mode, self.pick_px.size, self.pick_px.mean, self.pick_px.std)
             e_pick.append(t_pick(px))
         ic = torch.cat(e_clip)
         ic = ic / ic.norm(dim=-1, keepdim=True).clamp_min(1e-6)  # rewards.py:99

@@ -196,10 +196,12 @@ int eggroll_lora_project(const void* X, int64_t ldx, const float* theta_pop, int
 /* T = X A^T for n_lin LoRA linears that read the same X (Sana attn1 to_q/to_k/to_v, attn2 to_k/to_v:
  * the PEFT lora_A products of es_backend.py:193-200 sharing one input), X read from HBM once:
  *   T[l*M*r + row*r + q] = sum_k X[row,k] * A_{k,l}[q,k],  A_{k,l} = theta_pop[kl*ld_theta + offA_host[l]]
- * as [r][K] (kl = row / rows_per_member).  MFMA with A split into bf16 hi + lo (|error| <= ~2^-16
- * relative per product, fp32 accumulation), so T agrees with eggroll_lora_project to fp32 rounding,
- * not bit for bit.  offA_host: HOST array of n_lin offsets (multiples of 4).  1 <= n_lin <= 4,
- * n_lin * r <= 8, K % 32 == 0, K <= 4096, ldx % 8 == 0.                                        */
+ * as [r][K] (kl = row / rows_per_member).  MFMA with A split into bf16 hi + lo: each product carries
+ * ~2^-16 relative error (the lo part's rounding; fp32 accumulation), so T agrees with the fp32 VALU
+ * eggroll_lora_project to ~2^-16 * sum|x||a| per element, not to fp32 rounding and not bit for bit
+ * (this is the default projection of the Sana attn1 q/k/v and attn2 k/v linears).
+ * offA_host: HOST array of n_lin offsets (multiples of 4).  1 <= n_lin <= 4, n_lin * r <= 8,
+ * K % 32 == 0, K <= 4096, ldx % 8 == 0, X and theta_pop 16-byte aligned (16-byte vector loads). */
 int eggroll_lora_project_multi(const void* X, int64_t ldx, const float* theta_pop, int64_t ld_theta,
                                const int64_t* offA_host, int32_t n_lin, int32_t r, int64_t rows_per_member,
                                int64_t M, int64_t K, float* T, void* stream);

@@ -268,16 +268,15 @@ class Rewards32:
         self.clip = copy.deepcopy(rewards.clip).float()
         self.pick = copy.deepcopy(rewards.pick).float()
         self.mix_weights = rewards.mix_weights
+        self.tokenize = rewards.tokenize    # the same token ids as the build (synthetic or the local BPE)
 
     @torch.no_grad()
     def prompt_features(self, prompts: List[str]) -> Dict[str, torch.Tensor]:
-        from hyperscalees_t2i_amd.rewards import AESTHETIC_TEXT, NEGATIVE_TEXT, synthetic_tokenize
         dev = next(self.clip.parameters()).device
-        ids, mask = synthetic_tokenize([AESTHETIC_TEXT, NEGATIVE_TEXT] + list(prompts))
-        ids, mask = ids.to(dev), mask.to(dev)
-        tc = self.clip.text_projection(self.clip.text_model(input_ids=ids, attention_mask=mask).pooler_output)
+        ids_c, mask_c, ids_p, mask_p = (t.to(dev) for t in self.tokenize(prompts))
+        tc = self.clip.text_projection(self.clip.text_model(input_ids=ids_c, attention_mask=mask_c).pooler_output)
         tc = tc / tc.norm(dim=-1, keepdim=True).clamp_min(1e-6)
-        tp = self.pick.text_projection(self.pick.text_model(input_ids=ids[2:], attention_mask=mask[2:]).pooler_output)
+        tp = self.pick.text_projection(self.pick.text_model(input_ids=ids_p, attention_mask=mask_p).pooler_output)
         tp = tp / tp.norm(dim=-1, keepdim=True)
         return {"clip_aes": tc[0], "clip_neg": tc[1], "clip_prompt": tc[2:], "pick_prompt": tp}
 

@@ -19,7 +19,7 @@ def build_tiny(dev):
     from hyperscalees_t2i_amd.sana import SanaArch
     arch = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=2,
                     cross_attention_head_dim=64, caption_channels=2304)
-    cfg = SanaConfig(width_latent=4, height_latent=4, batches_per_gen=2, arch=arch,
+    cfg = SanaConfig(synthetic_weights=True, width_latent=4, height_latent=4, batches_per_gen=2, arch=arch,
                      vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
     be = SanaBackend(str(dev), cfg)
     be.init_and_attach_lora()

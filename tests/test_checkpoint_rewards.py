@@ -31,7 +31,7 @@ TINY = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_
 
 @pytest.fixture(scope="module")
 def backend_cpu():
-    cfg = SanaConfig(width_latent=4, height_latent=4, arch=TINY, vae_widths=(16, 32, 32, 64, 64, 64),
+    cfg = SanaConfig(synthetic_weights=True, width_latent=4, height_latent=4, arch=TINY, vae_widths=(16, 32, 32, 64, 64, 64),
                      vae_layers=(1, 1, 1, 1, 1, 1))
     be = SanaBackend("cpu", cfg)
     be.init_and_attach_lora()
@@ -153,7 +153,7 @@ def test_var_checkpoint_roundtrip(tmp_path):
     from safetensors.torch import load_file
     from hyperscalees_t2i_amd.backend import VarBackend, VarConfig
     from hyperscalees_t2i_amd.var import VARArch
-    be = VarBackend("cpu", VarConfig(arch=VARArch(depth=2, vae_ch=32), ckpt_dir="/nonexistent"))
+    be = VarBackend("cpu", VarConfig(arch=VARArch(depth=2, vae_ch=32), ckpt_dir="/nonexistent", synthetic_if_missing=True))
     be.init_and_attach_lora()
     params, shapes = be.collect_lora_params()
     theta = torch.randn(sum(p.numel() for p in params), generator=torch.Generator().manual_seed(5))

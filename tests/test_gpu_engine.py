@@ -19,7 +19,7 @@ TINY = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_
 
 @pytest.fixture(scope="module")
 def setup(dev):
-    cfg = SanaConfig(width_latent=4, height_latent=4, batches_per_gen=2, arch=TINY,
+    cfg = SanaConfig(synthetic_weights=True, width_latent=4, height_latent=4, batches_per_gen=2, arch=TINY,
                      vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
     be = SanaBackend(str(dev), cfg)
     be.init_and_attach_lora()
@@ -219,7 +219,7 @@ def test_fused_epilogues_population_forward(dev):
     128x128 GEMM tile while the fused one always runs the 8-phase kernel, so the summation order
     differs: close, not bitwise (the op-level tests in test_gpu_kernels.py are bitwise at one kernel)."""
     from hyperscalees_t2i_amd import lora
-    cfg = SanaConfig(width_latent=8, height_latent=8, batches_per_gen=2, arch=TINY,
+    cfg = SanaConfig(synthetic_weights=True, width_latent=8, height_latent=8, batches_per_gen=2, arch=TINY,
                      vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
     be = SanaBackend(str(dev), cfg)
     be.init_and_attach_lora()
@@ -243,7 +243,7 @@ def test_cross_attention_kernel_in_population_forward(dev):
     an additive bias) vs the SDPA path on gathered k / v, inside the population forward."""
     arch = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=4,
                     cross_attention_head_dim=112, caption_channels=2304)   # inner 448 = 7 x 64 (GEMM K)
-    cfg = SanaConfig(width_latent=4, height_latent=4, batches_per_gen=2, arch=arch,
+    cfg = SanaConfig(synthetic_weights=True, width_latent=4, height_latent=4, batches_per_gen=2, arch=arch,
                      vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
     be = SanaBackend(str(dev), cfg)
     be.init_and_attach_lora()
@@ -277,3 +277,10 @@ def test_prompt_features_graph_replay_matches_eager(dev):
         for k in want:
             assert torch.equal(got[k], want[k]), (prompts, k)
     assert len(rw._tgraphs) == 2
+    # switching the tower precision must not replay the graph captured on the fp32 text towers
+    rw.fp32_residual = ref.fp32_residual = False
+    prompts = ["a red fox", "two cats on a sofa"]
+    got, want = rw.prompt_features(prompts), ref.prompt_features(prompts)
+    for k in want:
+        assert torch.equal(got[k], want[k]), ("bf16 towers", k)
+    assert len(rw._tgraphs) == 3

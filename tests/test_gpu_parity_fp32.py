@@ -69,7 +69,7 @@ def rel(a, b):
 
 @pytest.fixture(scope="module")
 def stack(dev):
-    cfg = SanaConfig(width_latent=4, height_latent=4, batches_per_gen=2, arch=TINY,
+    cfg = SanaConfig(synthetic_weights=True, width_latent=4, height_latent=4, batches_per_gen=2, arch=TINY,
                      vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
     be = SanaBackend(str(dev), cfg)
     be.init_and_attach_lora()

@@ -35,7 +35,7 @@ def test_product_sample_indices_match_reference(golden):
 
 
 def _backend(P, k, R, L, prompts):
-    be = SanaBackend("cpu", SanaConfig(prompts_per_gen=k, batches_per_gen=R, max_log_batches=L))
+    be = SanaBackend("cpu", SanaConfig(synthetic_weights=True, prompts_per_gen=k, batches_per_gen=R, max_log_batches=L))
     be.base_prompt_embeds = torch.zeros(P, 1, 1)
     be.prompts_list = prompts
     return be

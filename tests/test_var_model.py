@@ -174,7 +174,7 @@ def test_var_es_epoch_matches_oracle(dev):
     from hyperscalees_t2i_amd.es_step import ESConfig, ESEngine
     from hyperscalees_t2i_amd.rewards import RewardModels
     from oracle import eggroll_oracle as O
-    be = VarBackend(str(dev), VarConfig(arch=ARCH, classes_per_gen=2, batches_per_gen=2, ckpt_dir="/nonexistent"))
+    be = VarBackend(str(dev), VarConfig(arch=ARCH, classes_per_gen=2, batches_per_gen=2, ckpt_dir="/nonexistent", synthetic_if_missing=True))
     be.init_and_attach_lora()
     params, shapes = be.collect_lora_params()
     theta = flatten_params(params).to(dev)

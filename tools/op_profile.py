@@ -12,7 +12,7 @@ from hyperscalees_t2i_amd.backend import SanaBackend, SanaConfig  # noqa: E402
 from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params  # noqa: E402
 
 dev = torch.device("cuda:0")
-be = SanaBackend(str(dev), SanaConfig())
+be = SanaBackend(str(dev), SanaConfig(synthetic_weights=True))
 be.init_and_attach_lora()
 params, shapes = be.collect_lora_params()
 theta = flatten_params(params).to(dev)

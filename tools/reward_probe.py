@@ -35,7 +35,7 @@ def main():
     from hyperscalees_t2i_amd.rewards import (RewardModels, _image_features, clip_pixels, clip_preprocess,
                                               postprocess_uint8)
     dev = torch.device("cuda:0")
-    rm = RewardModels.build(dev)
+    rm = RewardModels.build(dev, synthetic=True)
     g = torch.Generator(device=dev).manual_seed(0)
     imgs = (torch.rand((a.n, 3, 1024, 1024), generator=g, device=dev) * 2.2 - 1.1).to(torch.bfloat16)
     imgs = imgs.contiguous(memory_format=torch.channels_last)

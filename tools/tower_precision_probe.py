@@ -18,7 +18,7 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
     dev = torch.device("cuda:0")
     torch.backends.cuda.matmul.allow_tf32 = False
-    rw = RewardModels.build(dev)
+    rw = RewardModels.build(dev, synthetic=True)
     r32 = Rewards32(rw)
     g = torch.Generator(device=dev).manual_seed(0)
     # smooth synthetic "decoder outputs" in [-1, 1]
