@@ -1178,6 +1178,365 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8(
 }
 
 // ------------------------------------------------------------------------------------
+// 256 x 320 variant of the 8-phase kernel (kernel 10): the same schedule, 8 waves (2 M x 4 N), each
+// wave a 128 x 80 sub-tile = 8 x 5 fragments of 16 x 16.  The N side of a K-tile is split into two
+// LDS regions by fragment column: B0 = n-fragments 0-2 of every wave column (192 rows, 3 DMAs per
+// wave), B1 = n-fragments 3-4 (128 rows, 2 DMAs); A0 / A1 as in k_lora_gemm8.  Quadrant order
+// (0,0) (0,1) (1,1) (1,0) = 24, 16, 16, 24 MFMAs.  Why: per 64-deep K-tile the ring moves
+// (256 + 320) x 128 B = 72 KiB for 2,560 MFMA cycles per SIMD (28.1 B/cycle/CU) instead of 64 KiB for
+// 2,048 (32 B/cycle/CU) — the 256 x 256 main loop is bound by the per-CU LDS-DMA fill rate (28-30
+// B/cycle/CU measured), so 10 % fewer fill bytes per MFMA; 2240 and 11200 (the Sana
+// widths) are multiples of 320, so the 256-wide tiling's 2.8 % of padded columns at N = 2240 go away;
+// and the per-tile prologue / addend / C tile amortise over 25 % more MFMAs.  Ring: 2 x 72 KiB.
+// vmcnt: the waits retire everything older than the last three half-tiles issued (A0, B1, A1 of
+// the next-but-one K-tile = 6 DMAs) exactly as in k_lora_gemm8; the early-first-K-tile waits in
+// phases 1 and 2 count 11 (B0 carries 3 DMAs).  Every output element accumulates the same MFMAs in
+// the same k order as k_lora_gemm8, so the two kernels are bit-identical.
+// ------------------------------------------------------------------------------------
+namespace p8n {
+constexpr int HA = 128 * 128;            // A half: 128 rows x 128 B
+constexpr int HB0 = 192 * 128;           // B0: 4 wave columns x 48 rows
+constexpr int HB1 = 128 * 128;           // B1: 4 wave columns x 32 rows
+constexpr int RA0 = 0, RA1 = HA, RB0 = 2 * HA, RB1 = 2 * HA + HB0;
+constexpr int BUF = 2 * HA + HB0 + HB1;  // 72 KiB
+constexpr int LDS = 2 * BUF;             // 144 KiB
+constexpr int BN = 320, NF = 5;
+// epilogue operand block after the ring: T rows, B_k columns (tile's members a / a+1), bias
+constexpr int ET = 0, EB0 = 2048, EB1 = 4608, EBIAS = 7168, EBYTES = 7936;
+constexpr int CROW = 176;                // C staging row: 80 bf16 (160 B) padded to 11 x 16 B
+}  // namespace p8n
+
+template <int NP>
+struct StageN {
+    uint32_t off[NP];
+};
+
+// B-side staging: region row j -> tile column (j / PER) * 80 + FIRST + (j % PER)
+template <int NP, int PER, int FIRST>
+__device__ __forceinline__ StageN<NP> make_stage_bn(int n0, int row_max, int64_t ld, int wave, int lane) {
+    StageN<NP> s;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int j = (i * 8 + wave) * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ (j & 7);
+        int gr = n0 + (j / PER) * 80 + FIRST + (j % PER);
+        gr = gr < row_max ? gr : row_max;
+        s.off[i] = ((uint32_t)gr * (uint32_t)ld + chunk * 8) * 2;
+    }
+    return s;
+}
+__device__ __forceinline__ StageN<2> as_stage(const HalfStage& h) { return StageN<2>{{h.off[0], h.off[1]}}; }
+
+// Non-template overloads: the host compilation pass rejects __amdgpu_buffer_rsrc_t in a deduced template.
+__device__ __forceinline__ void issue_n(__amdgpu_buffer_rsrc_t rs, const StageN<2>& s, int kbytes, char* region,
+                                        int wave) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(region + (i * 8 + wave) * 1024), 16, s.off[i], kbytes,
+                                                 0, 0);
+}
+__device__ __forceinline__ void issue_n(__amdgpu_buffer_rsrc_t rs, const StageN<3>& s, int kbytes, char* region,
+                                        int wave) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(region + (i * 8 + wave) * 1024), 16, s.off[i], kbytes,
+                                                 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+    static_assert(N == 6 || N == 11, "add the literal");
+    if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+}
+
+// QB = 0: n-fragments 0..2 (region B0), QB = 1: 3..4 (region B1); W is the MFMA A operand (TR)
+template <int QA, int QB>
+__device__ __forceinline__ void p8n_mma(f32x4 (&acc)[8][5], const bf16x8 (&a)[4][2], const bf16x8 (&b)[3][2]) {
+    constexpr int NB = QB ? 2 : 3, G0 = QB ? 3 : 0;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int g = 0; g < NB; ++g)
+                acc[QA * 4 + f][G0 + g] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[g][kk], a[f][kk], acc[QA * 4 + f][G0 + g], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+}
+
+template <int NB>
+__device__ __forceinline__ void p8n_read_b(bf16x8 (&b)[3][2], const char* region, const int (&off)[2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int g = 0; g < NB; ++g) b[g][kk] = *reinterpret_cast<const bf16x8*>(region + off[kk] + g * 2048);
+}
+
+// one phase: read the quadrant's fragments (RD: 0 = A+B, 1 = B only, 2 = A only), issue one half-tile
+// DMA, [early vmcnt], [vmcnt(6)], retire the reads, barrier, 24 or 16 MFMA, barrier
+template <int QA, int QB, int RD, bool VM, int EW, int NP>
+__device__ __forceinline__ void p8n_phase(f32x4 (&acc)[8][5], bf16x8 (&a)[4][2], bf16x8 (&b)[3][2], const char* buf,
+                                          const int (&oA)[2], const int (&oB0)[2], const int (&oB1)[2],
+                                          __amdgpu_buffer_rsrc_t rs, const StageN<NP>& st, int kbytes, char* dst,
+                                          int wave) {
+    if (RD != 2) {
+        if (QB) p8n_read_b<2>(b, buf + p8n::RB1, oB1);
+        else p8n_read_b<3>(b, buf + p8n::RB0, oB0);
+    }
+    if (RD != 1) p8_read_a(a, buf + (QA ? p8n::RA1 : p8n::RA0), oA);
+    issue_n(rs, st, kbytes, dst, wave);
+    if constexpr (EW > 0) wait_vm_n<EW>();
+    if (VM) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    P8_LGKM0_;
+    P8_BAR();
+    p8n_mma<QA, QB>(acc, a, b);
+    P8_BAR();
+}
+
+template <int R>
+__device__ __forceinline__ void epi_prefetch_n(char* ep, int wave, int lane, int m0, int n0, int M, int N,
+                                               const float* __restrict__ T, const float* __restrict__ theta_pop,
+                                               int64_t ld_theta, int64_t offB, const unsigned short* __restrict__ bias,
+                                               int rows_per_member) {
+    static_assert(R >= 0 && R <= 2, "MFMA addend: r <= 2");
+    const uint32_t vo = lane * 4;
+    if constexpr (R > 0) {
+        constexpr int TB = 256 * R * 4, BB = p8n::BN * R * 4;
+        if (wave * 256 < TB) {
+            const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(T + (int64_t)m0 * R), (short)0, (int)((int64_t)(M - m0) * R * 4), 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (lds_void*)(ep + p8n::ET + wave * 256), 4, vo, wave * 256, 0, 0);
+        }
+        const int ma = m0 / rows_per_member;
+        const int nrec = (N - n0) * R * 4;
+        const int last = m0 + 255 < M ? m0 + 255 : M - 1;
+        const bool straddle = last / rows_per_member != ma;
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(theta_pop + (int64_t)ma * ld_theta + offB + (int64_t)n0 * R), (short)0, nrec, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rb1 = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(theta_pop + (int64_t)(ma + 1) * ld_theta + offB + (int64_t)n0 * R), (short)0, straddle ? nrec : 0,
+            0x00020000);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int pc = wave + 8 * p;
+            if (pc * 256 < BB) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(ep + p8n::EB0 + pc * 256), 4, vo, pc * 256, 0, 0);
+                if (straddle)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb1, (lds_void*)(ep + p8n::EB1 + pc * 256), 4, vo, pc * 256,
+                                                             0, 0);
+            }
+        }
+    }
+    if (bias && wave < 3) {
+        const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(bias + n0), (short)0,
+                                                                            (N - n0) * 2, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_void*)(ep + p8n::EBIAS + wave * 256), 4, vo, wave * 256, 0, 0);
+    }
+}
+
+// lora_mfma_addend_lds over the 128 x 80 wave tile (5 n-fragments), operands from the p8n epilogue block
+template <int R>
+__device__ __forceinline__ void lora_mfma_addend_n(f32x4 (&acc)[8][5], int lane, int m0, int rbase, int cbase,
+                                                   const char* ep, bool has_bias, float scale, int rows_per_member,
+                                                   int M) {
+    const int h = lane >> 4, l16 = lane & 15;
+    const int ma = m0 / rows_per_member;
+    const int last = (m0 + 255 < M ? m0 + 255 : M - 1);
+    const bool straddle = last / rows_per_member != ma;
+    const int bnd = (ma + 1) * rows_per_member - m0;
+    const float* Tl = reinterpret_cast<const float*>(ep + p8n::ET);
+    const unsigned short* bl = reinterpret_cast<const unsigned short*>(ep + p8n::EBIAS);
+    const float* Bk = reinterpret_cast<const float*>(ep + (h == 1 ? p8n::EB1 : p8n::EB0));
+    const bool con = h == 0 || (h == 1 && straddle);
+    float bv[5][R > 0 ? R : 1], tv[8][R > 0 ? R : 1];
+    unsigned short bb[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const int c = cbase + j * 16 + l16;
+#pragma unroll
+        for (int q = 0; q < R; ++q) bv[j][q] = Bk[c * R + q];
+        bb[j] = bl[c];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < R; ++q) tv[i][q] = Tl[(rbase + i * 16 + l16) * R + q];
+    bf16x8 rf[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float sb = scale * bv[j][q];
+            const short hi = bf16_bits(sb);
+            v[q] = hi;
+            v[R + q] = hi;
+            v[2 * R + q] = bf16_bits(sb - bf16_to_f32((unsigned short)hi));
+        }
+        v[3 * R] = has_bias ? (short)bb[j] : (short)0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = con ? v[e] : (short)0;
+        rf[j] = *reinterpret_cast<bf16x8*>(v);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int rl = rbase + i * 16 + l16;
+        const bool ron = h == (rl >= bnd ? 1 : 0);
+        short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float t = tv[i][q];
+            const short th = bf16_bits(t);
+            v[q] = th;
+            v[R + q] = bf16_bits(t - bf16_to_f32((unsigned short)th));
+            v[2 * R + q] = th;
+        }
+        v[3 * R] = (short)0x3F80;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ron ? v[e] : (short)0;
+        const bf16x8 lf = *reinterpret_cast<bf16x8*>(v);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rf[j], lf, acc[i][j], 0, 0, 0);
+    }
+}
+
+// C tile of a transposed 128 x 80 wave tile in two 64-row passes through a wave-private LDS tile
+// (176-B rows: 8-B fragment writes, 16-B reads), 16-B global stores; EPI ops as store_tile_t.
+template <int EPI = EPI_NONE>
+__device__ __forceinline__ void store_tile_n(f32x4 (&acc)[8][5], char* smem, int wave, int lane, int m0, int n0,
+                                             int rbase, int cbase, int M, int N, unsigned short* __restrict__ Y,
+                                             int64_t ldy, const EpiArgs& ea = EpiArgs{}) {
+    constexpr int RB = p8n::CROW;
+    char* ctile = smem + wave * (64 * RB);
+    const int r_l = lane & 15, c_l = (lane >> 4) * 4;
+    const bool vec = (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0 &&
+                     (EPI == EPI_NONE || EPI == EPI_SILU ||
+                      ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
+                       (EPI != EPI_GATED || ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0))));
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rr = i * 16 + r_l;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = f32_to_bf16(acc[ph * 4 + i][j][e]);
+                *reinterpret_cast<u16x4*>(ctile + rr * RB + (j * 16 + c_l) * 2) = o;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+        u16x8 v[10];
+#pragma unroll
+        for (int it = 0; it < 10; ++it) {
+            const int idx = it * 64 + lane, rr = idx / 10, ch = idx - rr * 10;
+            v[it] = *reinterpret_cast<const u16x8*>(ctile + rr * RB + ch * 16);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the next pass rewrites the tile
+#pragma unroll
+        for (int it = 0; it < 10; ++it) {
+            const int idx = it * 64 + lane, rr = idx / 10, ch = idx - rr * 10;
+            const int row = m0 + rbase + ph * 64 + rr, col = n0 + cbase + ch * 8;
+            if (row >= M || col >= N) continue;
+            unsigned short* dst = Y + (int64_t)row * ldy + col;
+            if (vec && col + 8 <= N) {
+                u16x8 w = v[it];
+                if constexpr (EPI != EPI_NONE) w = epi_apply<EPI>(w, row, col, ea);
+                *reinterpret_cast<u16x8*>(dst) = w;
+            } else {
+                for (int u = 0; u < 8 && col + u < N; ++u) dst[u] = epi_apply1<EPI>(v[it][u], row, col + u, ea);
+            }
+        }
+    }
+}
+
+// MF path only (r <= 2, rows_per_member >= 256, or r = 0): bias + LoRA term as the MFMA addend
+template <int R, int EPI = EPI_NONE>
+__global__ __launch_bounds__(512, 1) void k_lora_gemm8n(
+    const unsigned short* __restrict__ X, int64_t ldx, const unsigned short* __restrict__ W, int64_t ldw,
+    const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
+    int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int M, int N, int64_t K, int tiles_n,
+    unsigned short* __restrict__ Y, int64_t ldy, EpiArgs ea = EpiArgs{}) {
+    __shared__ __attribute__((aligned(16))) char smem[p8n::LDS + p8n::EBYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+    const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+    const int tiles_m = (M + 255) / 256;
+    const int per_group = GROUP_M * tiles_n;
+    const int grp = tile / per_group, first_m = grp * GROUP_M;
+    const int gsize = (tiles_m - first_m) < GROUP_M ? (tiles_m - first_m) : GROUP_M;
+    const int in_grp = tile - grp * per_group;
+    const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
+    const int m0 = tm * 256, n0 = tn * p8n::BN;
+
+    const StageN<2> sA0 = as_stage(make_stage<true>(m0, M - 1, ldx, 0, wave, lane));
+    const StageN<2> sA1 = as_stage(make_stage<true>(m0, M - 1, ldx, 1, wave, lane));
+    const StageN<3> sB0 = make_stage_bn<3, 48, 0>(n0, N - 1, ldw, wave, lane);
+    const StageN<2> sB1 = make_stage_bn<2, 32, 48>(n0, N - 1, ldw, wave, lane);
+    char* const e_buf = smem;
+    char* const o_buf = smem + p8n::BUF;
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, 0x7fffffff, 0x00020000);
+
+    f32x4 acc[8][5];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a[4][2], b[3][2];
+    int oA[2], oB0[2], oB1[2];
+    p8_frag_offsets(oA, wm * 64 + (lane & 15), lane);
+    p8_frag_offsets(oB0, wn * 48 + (lane & 15), lane);
+    p8_frag_offsets(oB1, wn * 32 + (lane & 15), lane);
+
+    const int nk = (int)(K / BK);
+    auto kb = [nk](int t) -> int { return (t < nk ? t : nk - 1) * (BK * 2); };
+    epi_prefetch_n<R>(smem + p8n::LDS, wave, lane, m0, n0, M, N, T, theta_pop, ld_theta, offB, bias, rows_per_member);
+    issue_n(rX, sA0, 0, e_buf + p8n::RA0, wave);
+    issue_n(rW, sB0, 0, e_buf + p8n::RB0, wave);
+    issue_n(rW, sB1, 0, e_buf + p8n::RB1, wave);
+    issue_n(rX, sA1, 0, e_buf + p8n::RA1, wave);
+    issue_n(rX, sA0, kb(1), o_buf + p8n::RA0, wave);
+    issue_n(rW, sB1, kb(1), o_buf + p8n::RB1, wave);
+    issue_n(rX, sA1, kb(1), o_buf + p8n::RA1, wave);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // K-tile 0's A0 + B0 (5 younger halves x 2 DMAs)
+    P8_BAR();
+    if (wm == 1) P8_BAR();
+
+    int t0 = 0;
+    for (; t0 + 1 < nk; t0 += 2) {
+        const int k1 = kb(t0 + 1), k2 = kb(t0 + 2), k3 = kb(t0 + 3);
+        p8n_phase<0, 0, 0, false, 11>(acc, a, b, e_buf, oA, oB0, oB1, rW, sB0, k1, o_buf + p8n::RB0, wave);
+        p8n_phase<0, 1, 1, false, 11>(acc, a, b, e_buf, oA, oB0, oB1, rX, sA0, k2, e_buf + p8n::RA0, wave);
+        p8n_phase<1, 1, 2, false, 0>(acc, a, b, e_buf, oA, oB0, oB1, rW, sB1, k2, e_buf + p8n::RB1, wave);
+        p8n_phase<1, 0, 1, true, 0>(acc, a, b, e_buf, oA, oB0, oB1, rX, sA1, k2, e_buf + p8n::RA1, wave);
+        p8n_phase<0, 0, 0, false, 0>(acc, a, b, o_buf, oA, oB0, oB1, rW, sB0, k2, e_buf + p8n::RB0, wave);
+        p8n_phase<0, 1, 1, false, 0>(acc, a, b, o_buf, oA, oB0, oB1, rX, sA0, k3, o_buf + p8n::RA0, wave);
+        p8n_phase<1, 1, 2, false, 0>(acc, a, b, o_buf, oA, oB0, oB1, rW, sB1, k3, o_buf + p8n::RB1, wave);
+        p8n_phase<1, 0, 1, true, 0>(acc, a, b, o_buf, oA, oB0, oB1, rX, sA1, k3, o_buf + p8n::RA1, wave);
+    }
+    if (t0 < nk) {
+        const int k1 = kb(t0 + 1), k2 = kb(t0 + 2);
+        p8n_phase<0, 0, 0, false, 11>(acc, a, b, e_buf, oA, oB0, oB1, rW, sB0, k1, o_buf + p8n::RB0, wave);
+        p8n_phase<0, 1, 1, false, 11>(acc, a, b, e_buf, oA, oB0, oB1, rX, sA0, k2, e_buf + p8n::RA0, wave);
+        p8n_phase<1, 1, 2, false, 0>(acc, a, b, e_buf, oA, oB0, oB1, rW, sB1, k2, e_buf + p8n::RB1, wave);
+        p8n_phase<1, 0, 1, false, 0>(acc, a, b, e_buf, oA, oB0, oB1, rX, sA1, k2, e_buf + p8n::RA1, wave);
+    }
+    if (wm == 0) P8_BAR();
+    P8_VM0();
+    __syncthreads();  // every wave is past its last ring read: the epilogue reuses the ring
+
+    lora_mfma_addend_n<R>(acc, lane, m0, wm * 128, wn * 80, smem + p8n::LDS, bias != nullptr, scale, rows_per_member,
+                          M);
+    store_tile_n<EPI>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 80, M, N, Y, ldy, ea);
+}
+
+// ------------------------------------------------------------------------------------
 // Y += scale * T B_k^T   (8 bf16 per thread)
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_lora_expand(const float* __restrict__ T, const float* __restrict__ theta_pop,
@@ -1532,6 +1891,39 @@ static int launch_gemm8_epi(const void* X, int64_t ldx, const void* W, int64_t l
 #undef EGG_GEMM8E_R
 #undef EGG_GEMM8E
     EGG_CHECK_LAUNCH("lora_gemm8_epi");
+    return EGGROLL_OK;
+}
+
+// The 256 x 320 kernel (kernel 10): MFMA-addend path only (r <= 2 with rows_per_member >= 256, or r = 0).
+static bool gemm8n_ok(int32_t r, int64_t rows_per_member) { return r == 0 || (r <= 2 && rows_per_member >= 256); }
+
+static int launch_gemm8n(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                         const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                         int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, int32_t epi,
+                         const EpiArgs& ea, hipStream_t st) {
+    const int64_t tiles_m = (M + 255) / 256, tiles_n = (N + p8n::BN - 1) / p8n::BN;
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "lora_gemm: grid too large");
+    EGG_CHECK_ARG(gemm8n_ok(r, rows_per_member), "lora_gemm: kernel 10 needs r <= 2 and rows_per_member >= 256");
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+#define EGG_GEMM8N(RV, EV)                                                                                        \
+    hipLaunchKernelGGL((k_lora_gemm8n<RV, EV>), grid, dim3(512), 0, st, (const unsigned short*)X, ldx,             \
+                       (const unsigned short*)W, ldw, (const unsigned short*)bias, T, theta_pop, ld_theta, offB,  \
+                       scale, (int)rows_per_member, (int)M, (int)N, K, (int)tiles_n, (unsigned short*)Y, ldy, ea)
+#define EGG_GEMM8N_R(EV)                       \
+    switch (r) {                               \
+        case 0: EGG_GEMM8N(0, EV); break;      \
+        case 1: EGG_GEMM8N(1, EV); break;      \
+        default: EGG_GEMM8N(2, EV); break;     \
+    }
+    switch (epi) {
+        case EPI_NONE: EGG_GEMM8N_R(EPI_NONE); break;
+        case EPI_SILU: EGG_GEMM8N_R(EPI_SILU); break;
+        case EPI_RES: EGG_GEMM8N_R(EPI_RES); break;
+        default: EGG_GEMM8N_R(EPI_GATED); break;
+    }
+#undef EGG_GEMM8N_R
+#undef EGG_GEMM8N
+    EGG_CHECK_LAUNCH("lora_gemm8n");
     return EGGROLL_OK;
 }
 
@@ -2613,8 +3005,9 @@ static int lora_gemm_impl(const void* X, int64_t ldx, const void* W, int64_t ldw
                           const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
                           int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy,
                           int32_t kernel, void* stream) {
-    EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 9 || kernel == 12 || kernel == 128 || kernel == 256,
-                  "lora_gemm: kernel must be 0 (auto), 8, 9, 12, 128 or 256 (got %d)", kernel);
+    EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 9 || kernel == 10 || kernel == 12 || kernel == 128 ||
+                      kernel == 256,
+                  "lora_gemm: kernel must be 0 (auto), 8, 9, 10, 12, 128 or 256 (got %d)", kernel);
     EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0, "lora_gemm: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
                   (long long)K);
     EGG_CHECK_ARG(K % 64 == 0, "lora_gemm: K=%lld must be a multiple of 64", (long long)K);
@@ -2627,7 +3020,12 @@ static int lora_gemm_impl(const void* X, int64_t ldx, const void* W, int64_t ldw
     EGG_CHECK_ARG(r == 0 || (T && theta_pop), "lora_gemm: T / theta_pop NULL with r > 0");
     hipStream_t st = as_stream(stream);
     const int tsel = kernel ? kernel : ((M / 256) * ((N + 255) / 256) >= 512 ? 8 : 128);
-    if (tsel == 8 || tsel == 9 || tsel == 12) {
+    if (tsel == 10 && gemm8n_ok(r, rows_per_member)) {   // else: kernel 8's VALU-epilogue path, as kernel 8 does
+        EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_gemm: operand > 2 GiB");
+        return launch_gemm8n(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
+                             ldy, EPI_NONE, EpiArgs{}, st);
+    }
+    if (tsel == 8 || tsel == 9 || tsel == 10 || tsel == 12) {
         EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_gemm: operand > 2 GiB");
         const bool mf = tsel != 9 && r <= 2 && rows_per_member >= 256;
         return mf ? launch_gemm8<true>(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale,
@@ -2669,8 +3067,9 @@ int eggroll_lora_linear_pop_sel(const void* X, int64_t ldx, const void* W, int64
                                 const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
                                 float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
                                 int64_t ldy, float* T_ws, int32_t kernel, void* stream) {
-    EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 9 || kernel == 12 || kernel == 128 || kernel == 256,
-                  "lora_linear_pop: kernel must be 0 (auto), 8, 9, 12, 128 or 256 (got %d)", kernel);
+    EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 9 || kernel == 10 || kernel == 12 || kernel == 128 ||
+                      kernel == 256,
+                  "lora_linear_pop: kernel must be 0 (auto), 8, 9, 10, 12, 128 or 256 (got %d)", kernel);
     EGG_CHECK_ARG(K > 0 && K % 64 == 0, "lora_linear_pop: K=%lld must be a multiple of 64", (long long)K);
     EGG_CHECK_ARG(r >= 0 && r <= 16, "lora_linear_pop: r=%d out of range", r);
     if (M == 0) return EGGROLL_OK;
@@ -2690,14 +3089,16 @@ int eggroll_lora_linear_pop_sel(const void* X, int64_t ldx, const void* W, int64
                           ldy, kernel == 12 ? 8 : kernel, stream);
 }
 
-int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
-                                const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
-                                float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
-                                int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr, const void* gate,
-                                int64_t gstride, int64_t rows_per_group, void* stream) {
+int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                                    const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                                    float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                                    int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr,
+                                    const void* gate, int64_t gstride, int64_t rows_per_group, int32_t kernel,
+                                    void* stream) {
+    EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 10, "lora_linear_pop_epi: kernel must be 0, 8 or 10");
     if (epi == EPI_NONE)
         return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
-                                           rows_per_member, M, N, K, Y, ldy, T_ws, 0, stream);
+                                           rows_per_member, M, N, K, Y, ldy, T_ws, kernel, stream);
     EGG_CHECK_ARG(epi == EPI_SILU || epi == EPI_RES || epi == EPI_GATED, "lora_linear_pop_epi: epi=%d unknown", epi);
     EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
     EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
@@ -2715,8 +3116,22 @@ int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64
         if (rc) return rc;
     }
     const EpiArgs ea{(const unsigned short*)res, ldr, (const unsigned short*)gate, gstride, rows_per_group};
-    return launch_gemm8_epi(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale,
-                            r ? rows_per_member : (M > 0 ? M : 1), M, N, K, Y, ldy, epi, ea, as_stream(stream));
+    const int64_t rpm = r ? rows_per_member : (M > 0 ? M : 1);
+    if (kernel == 10)
+        return launch_gemm8n(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rpm, M, N, K, Y, ldy, epi,
+                             ea, as_stream(stream));
+    return launch_gemm8_epi(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rpm, M, N, K, Y, ldy, epi,
+                            ea, as_stream(stream));
+}
+
+int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                                const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                                float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                                int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr, const void* gate,
+                                int64_t gstride, int64_t rows_per_group, void* stream) {
+    return eggroll_lora_linear_pop_epi_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
+                                           rows_per_member, M, N, K, Y, ldy, T_ws, epi, res, ldr, gate, gstride,
+                                           rows_per_group, 0, stream);
 }
 
 int eggroll_lora_linear_pop(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,

@@ -308,10 +308,11 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
                         offA: int, offB: int, r: int, scale: float, rows_per_member: int, epi: str,
                         res: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
                         rows_per_group: int = 1, out: Optional[torch.Tensor] = None,
-                        T_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """lora_linear_pop with an epilogue op on the bf16 output y (eggroll_lora_linear_pop_epi):
+                        T_ws: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
+    """lora_linear_pop with an epilogue op on the bf16 output y (eggroll_lora_linear_pop_epi_sel):
     "silu": silu(y); "res": res + y; "gated": res + gate[row // rows_per_group] * y.  With res given and
-    out None the result is written into res (in place, as the residual adds it replaces)."""
+    out None the result is written into res (in place, as the residual adds it replaces).
+    kernel: 0 automatic, 8 / 10 the 256x256 / 256x320 8-phase kernels (A/B measurement)."""
     _dev(x, "lora_linear_pop_epi(x)", torch.bfloat16)
     _dev(W, "lora_linear_pop_epi(W)", torch.bfloat16)
     M, Kd = x.shape
@@ -329,10 +330,10 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
         need = lora_workspace_numel(M, Kd, r, rows_per_member)
         if T_ws is None or T_ws.numel() < need:
             T_ws = torch.empty(need, dtype=torch.float32, device=x.device)
-    _lib.call("eggroll_lora_linear_pop_epi", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
+    _lib.call("eggroll_lora_linear_pop_epi_sel", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
               _p(theta_pop) if r > 0 else None, theta_pop.stride(0) if r > 0 else 0, offA, offB, r, float(scale),
               rows_per_member, M, N, Kd, out.data_ptr(), N, _p(T_ws) if r > 0 else None, code,
-              _p(res), N if res is not None else 0, pg, gst or N, int(rows_per_group), _stream(x.device))
+              _p(res), N if res is not None else 0, pg, gst or N, int(rows_per_group), int(kernel), _stream(x.device))
     return out
 
 

@@ -149,6 +149,14 @@ int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64
                                 float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
                                 int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr, const void* gate,
                                 int64_t gstride, int64_t rows_per_group, void* stream);
+/* The same with an explicit kernel (A/B measurement): 0 = automatic, 8 = the 256x256 8-phase
+ * kernel, 10 = the 256x320 8-phase kernel (bit-identical to 8).                                   */
+int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                                    const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                                    float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                                    int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr,
+                                    const void* gate, int64_t gstride, int64_t rows_per_group, int32_t kernel,
+                                    void* stream);
 /* (2) Population-batched perturbed LoRA linear — replaces per-member
  * `unflatten_to_params` + PEFT lora.Linear.forward (peft: y = base(x) + B(A x) * alpha/r),
  * members evaluated sequentially in the reference (unifed_es.py:159-163).
@@ -179,8 +187,9 @@ int eggroll_lora_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, co
 /* The same two entry points with an explicit kernel choice (per call; no global state), for A/B
  * measurement: 0 = automatic (as above: the 8-phase 256x256 kernel when the grid fills the chip,
  * else 128x128); 8 = 8-phase with the MFMA LoRA epilogue, 9 = 8-phase with a VALU epilogue,
- * 128 / 256 = one-barrier tiles; linear_pop_sel also takes 12 = 8-phase with the projection fused
- * into the GEMM (opt-in: slower than the two-pass path at the Sana shapes).                     */
+ * 10 = 8-phase 256x320 tile with the MFMA LoRA epilogue (r <= 2 with rows_per_member >= 256, or
+ * r = 0; bit-identical to 8), 128 / 256 = one-barrier tiles; linear_pop_sel also takes 12 = 8-phase
+ * with the projection fused into the GEMM (opt-in: slower than the two-pass path at the Sana shapes). */
 int eggroll_lora_gemm_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
                           const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
                           int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,

@@ -44,7 +44,7 @@ def test_argument_errors_are_reported():
                                      None, None)  # K % 64 != 0
     assert rc == -1 and b"multiple of 64" in lib.eggroll_last_error()
     rc = lib.eggroll_lora_linear_pop_sel(None, 64, None, 64, None, None, 0, 0, 0, 2, 1.0, 10, 10, 10, 64, None, 10,
-                                         None, 10, None)  # kernel 10: the old diagnostic modes are gone
+                                         None, 11, None)  # kernel 11: not a kernel id
     assert rc == -1 and b"kernel" in lib.eggroll_last_error()
     rc = lib.eggroll_lora_gemm_sel(None, 64, None, 64, None, None, None, 0, 0, 2, 1.0, 10, 10, 10, 64, None, 10, 12,
                                    None)  # kernel 12 (fused projection) exists only in linear_pop_sel

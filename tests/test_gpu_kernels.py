@@ -236,8 +236,8 @@ def _lora_ref(x, W, b, tp, offA, offB, r, scale, rpm):
                                  scale, rpm)
 
 
-@pytest.fixture(params=[128, 256, 8, 9, 12],
-                ids=["tile128", "tile256", "tile8phase_mfma", "tile8phase_valu", "tile8phase_fused_proj"])
+@pytest.fixture(params=[128, 256, 8, 9, 10, 12],
+                ids=["tile128", "tile256", "tile8phase_mfma", "tile8phase_valu", "tile8phase_320", "tile8phase_fused_proj"])
 def gemm_tile(request):
     return request.param
 
@@ -868,6 +868,37 @@ def test_lora_linear_pop_epilogue_bitexact(dev, epi, r, M, N, Kd, rpm):
         out = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, "gated", res=res.clone(), gate=gate,
                                     rows_per_group=rpg)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("M,N,Kd,r,rpm", [(2 * 16384, 2240, 2240, 2, 16384), (3 * 1000 + 200, 2000, 256, 1, 1000),
+                                          (777, 200, 128, 0, 777), (4 * 4096, 11200, 640, 0, 4096),
+                                          (1536, 320, 64, 2, 700), (2560, 650, 192, 2, 512), (9600, 2240, 2240, 2, 1200)])
+def test_gemm_320_tile_bitexact_vs_256(dev, M, N, Kd, r, rpm):
+    """Kernel 10 (256 x 320 tile, B halves of 3 + 2 n-fragments) accumulates every output element with
+    the same MFMAs in the same k order as kernel 8 (256 x 256): bit-identical outputs, plain and with
+    each fused epilogue op; ragged M / N, tiles straddling members, 1 / odd / even K-tile counts."""
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N)
+    x = torch.randn((M, Kd), generator=g, device=dev).to(torch.bfloat16)
+    W = (torch.randn((N, Kd), generator=g, device=dev) / Kd ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=dev).to(torch.bfloat16)
+    tp = torch.randn((-(-M // rpm), Kd * r + N * r + 8), generator=g, device=dev) * 0.05 if r else None
+    offA, offB = 0, Kd * r
+    T = K.lora_project(x, tp, offA, r, rpm) if r else None
+    y8 = K.lora_gemm(x, W, bias, T, tp, offB, r, 2.0, rpm, kernel=8)
+    y10 = K.lora_gemm(x, W, bias, T, tp, offB, r, 2.0, rpm, kernel=10)
+    assert torch.equal(y8, y10)
+    res = torch.randn((M, N), generator=g, device=dev).to(torch.bfloat16)
+    gate = torch.randn((-(-M // 512), N), generator=g, device=dev).to(torch.bfloat16)
+    for epi in ("silu", "res", "gated"):
+        kw = {} if epi == "silu" else dict(res=res.clone())
+        if epi == "gated":
+            kw.update(gate=gate, rows_per_group=512)
+        o8 = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, epi, kernel=8, **kw)
+        kw = {} if epi == "silu" else dict(res=res.clone())
+        if epi == "gated":
+            kw.update(gate=gate, rows_per_group=512)
+        o10 = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, epi, kernel=10, **kw)
+        assert torch.equal(o8, o10), epi
 
 
 @pytest.mark.parametrize("B,N,H,L,U", [(4, 64, 2, 37, 2), (3, 100, 3, 300, 3), (6, 17, 1, 320, 2), (16, 1024, 20, 300, 4)])
