@@ -1203,7 +1203,6 @@ constexpr int LDS = 2 * BUF;             // 144 KiB
 constexpr int BN = 320, NF = 5;
 // epilogue operand block after the ring: T rows, B_k columns (tile's members a / a+1), bias
 constexpr int ET = 0, EB0 = 2048, EB1 = 4608, EBIAS = 7168, EBYTES = 7936;
-constexpr int CROW = 176;                // C staging row: 80 bf16 (160 B) padded to 11 x 16 B
 }  // namespace p8n
 
 template <int NP>
@@ -1402,44 +1401,48 @@ __device__ __forceinline__ void lora_mfma_addend_n(f32x4 (&acc)[8][5], int lane,
     }
 }
 
-// C tile of a transposed 128 x 80 wave tile in two 64-row passes through a wave-private LDS tile
-// (176-B rows: 8-B fragment writes, 16-B reads), 16-B global stores; EPI ops as store_tile_t.
+// C tile of the 256 x 320 workgroup tile, staged through ONE shared LDS tile (256 rows x 640 B = all
+// 160 KiB; the caller has passed a barrier after the epilogue block's last read) so that the global
+// stores write whole 128-B lines: with per-wave staging each wave's 80-column row segment (160 B)
+// straddles lines shared with the neighbouring wave and the store phase took 2x the 256 x 256
+// kernel's per byte (stamped).  16-B slots are rotated by row ((slot + row) mod 40): the
+// 8-B fragment writes are at most 2-way bank-conflicted.  After a barrier, wave w stores rows
+// [32w, 32w + 32): 40 lanes per 640-B row, 20 16-B stores per lane.  EPI ops as store_tile_t.
 template <int EPI = EPI_NONE>
-__device__ __forceinline__ void store_tile_n(f32x4 (&acc)[8][5], char* smem, int wave, int lane, int m0, int n0,
-                                             int rbase, int cbase, int M, int N, unsigned short* __restrict__ Y,
-                                             int64_t ldy, const EpiArgs& ea = EpiArgs{}) {
-    constexpr int RB = p8n::CROW;
-    char* ctile = smem + wave * (64 * RB);
+__device__ __forceinline__ void store_tile_wg(f32x4 (&acc)[8][5], char* smem, int wave, int lane, int m0, int n0,
+                                              int wm, int wn, int M, int N, unsigned short* __restrict__ Y,
+                                              int64_t ldy, const EpiArgs& ea = EpiArgs{}) {
+    constexpr int RB = 640, SL = 40;
     const int r_l = lane & 15, c_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int rr = wm * 128 + i * 16 + r_l;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = f32_to_bf16(acc[i][j][e]);
+            const int c = wn * 80 + j * 16 + c_l;  // tile column: 16-B slot c >> 3, 8-B half (c >> 2) & 1
+            *reinterpret_cast<u16x4*>(smem + rr * RB + ((c >> 3) + rr) % SL * 16 + ((c >> 2) & 1) * 8) = o;
+        }
+    }
+    __syncthreads();
     const bool vec = (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0 &&
                      (EPI == EPI_NONE || EPI == EPI_SILU ||
                       ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
                        (EPI != EPI_GATED || ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0))));
 #pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int rr = i * 16 + r_l;
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                u16x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = f32_to_bf16(acc[ph * 4 + i][j][e]);
-                *reinterpret_cast<u16x4*>(ctile + rr * RB + (j * 16 + c_l) * 2) = o;
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+    for (int h = 0; h < 20; h += 10) {
         u16x8 v[10];
 #pragma unroll
         for (int it = 0; it < 10; ++it) {
-            const int idx = it * 64 + lane, rr = idx / 10, ch = idx - rr * 10;
-            v[it] = *reinterpret_cast<const u16x8*>(ctile + rr * RB + ch * 16);
+            const int idx = (h + it) * 64 + lane, rr = wave * 32 + idx / SL, ch = idx % SL;
+            v[it] = *reinterpret_cast<const u16x8*>(smem + rr * RB + (ch + rr) % SL * 16);
         }
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the next pass rewrites the tile
 #pragma unroll
         for (int it = 0; it < 10; ++it) {
-            const int idx = it * 64 + lane, rr = idx / 10, ch = idx - rr * 10;
-            const int row = m0 + rbase + ph * 64 + rr, col = n0 + cbase + ch * 8;
+            const int idx = (h + it) * 64 + lane, rr = wave * 32 + idx / SL, ch = idx % SL;
+            const int row = m0 + rr, col = n0 + ch * 8;
             if (row >= M || col >= N) continue;
             unsigned short* dst = Y + (int64_t)row * ldy + col;
             if (vec && col + 8 <= N) {
@@ -1460,7 +1463,8 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8n(
     const unsigned short* __restrict__ bias, const float* __restrict__ T, const float* __restrict__ theta_pop,
     int64_t ld_theta, int64_t offB, float scale, int rows_per_member, int M, int N, int64_t K, int tiles_n,
     unsigned short* __restrict__ Y, int64_t ldy, EpiArgs ea = EpiArgs{}) {
-    __shared__ __attribute__((aligned(16))) char smem[p8n::LDS + p8n::EBYTES];
+    __shared__ __attribute__((aligned(16))) char smem[256 * 640];  // ring + epilogue block; the C tile: all of it
+    static_assert(p8n::LDS + p8n::EBYTES <= 256 * 640, "LDS layout");
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -1473,6 +1477,8 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8n(
     const int in_grp = tile - grp * per_group;
     const int tm = first_m + in_grp % gsize, tn = in_grp / gsize;
     const int m0 = tm * 256, n0 = tn * p8n::BN;
+    EGG_STAMP_RT(6);
+    EGG_STAMP(0);
 
     const StageN<2> sA0 = as_stage(make_stage<true>(m0, M - 1, ldx, 0, wave, lane));
     const StageN<2> sA1 = as_stage(make_stage<true>(m0, M - 1, ldx, 1, wave, lane));
@@ -1506,6 +1512,7 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8n(
     issue_n(rX, sA1, kb(1), o_buf + p8n::RA1, wave);
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // K-tile 0's A0 + B0 (5 younger halves x 2 DMAs)
     P8_BAR();
+    EGG_STAMP(1);
     if (wm == 1) P8_BAR();
 
     int t0 = 0;
@@ -1528,12 +1535,19 @@ __global__ __launch_bounds__(512, 1) void k_lora_gemm8n(
         p8n_phase<1, 0, 1, false, 0>(acc, a, b, e_buf, oA, oB0, oB1, rX, sA1, k2, e_buf + p8n::RA1, wave);
     }
     if (wm == 0) P8_BAR();
+    EGG_STAMP(2);
     P8_VM0();
     __syncthreads();  // every wave is past its last ring read: the epilogue reuses the ring
+    EGG_STAMP(3);
 
     lora_mfma_addend_n<R>(acc, lane, m0, wm * 128, wn * 80, smem + p8n::LDS, bias != nullptr, scale, rows_per_member,
                           M);
-    store_tile_n<EPI>(acc, smem, wave, lane, m0, n0, wm * 128, wn * 80, M, N, Y, ldy, ea);
+    EGG_STAMP(4);
+    __syncthreads();  // the C tile overwrites the epilogue block every wave's addend has just read
+    store_tile_wg<EPI>(acc, smem, wave, lane, m0, n0, wm, wn, M, N, Y, ldy, ea);
+    EGG_STAMP_DRAIN();
+    EGG_STAMP(5);
+    EGG_STAMP_RT(7);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1896,6 +1910,18 @@ static int launch_gemm8_epi(const void* X, int64_t ldx, const void* W, int64_t l
 
 // The 256 x 320 kernel (kernel 10): MFMA-addend path only (r <= 2 with rows_per_member >= 256, or r = 0).
 static bool gemm8n_ok(int32_t r, int64_t rows_per_member) { return r == 0 || (r <= 2 && rows_per_member >= 256); }
+
+// Automatic choice between the 8-phase tiles (256 x 256 = 8, 256 x 320 = 10): rounds of one tile per
+// CU (256 CUs) times the tile's cost, a 256 x 320 tile measured at 1.22x a 256 x 256 one (25 % more
+// MFMAs, ~2.5 % fewer cycles per output element and a slightly higher clock; tools/gemm10_probe.py,
+// DESIGN §5).  131072 x 2240: 18 vs 14 x 1.22 rounds -> 10 (+3-6 % measured); 9600 x 2240: 2 vs 2 x 1.22
+// -> 8.  The residual / gated-residual epilogues stay on 8 (their loads slow kernel 10's store phase).
+static int gemm8_auto(int64_t M, int64_t N, int32_t r, int64_t rows_per_member, int32_t epi) {
+    if (!gemm8n_ok(r, rows_per_member) || epi == EPI_RES || epi == EPI_GATED) return 8;
+    const int64_t tm = (M + 255) / 256;
+    const int64_t rounds8 = (tm * ((N + 255) / 256) + 255) / 256, rounds10 = (tm * ((N + 319) / 320) + 255) / 256;
+    return 122 * rounds10 < 100 * rounds8 ? 10 : 8;
+}
 
 static int launch_gemm8n(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
                          const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
@@ -3019,7 +3045,8 @@ static int lora_gemm_impl(const void* X, int64_t ldx, const void* W, int64_t ldw
     EGG_CHECK_ARG(X && W && Y, "lora_gemm: NULL pointer");
     EGG_CHECK_ARG(r == 0 || (T && theta_pop), "lora_gemm: T / theta_pop NULL with r > 0");
     hipStream_t st = as_stream(stream);
-    const int tsel = kernel ? kernel : ((M / 256) * ((N + 255) / 256) >= 512 ? 8 : 128);
+    const int tsel = kernel ? kernel
+                            : ((M / 256) * ((N + 255) / 256) >= 512 ? gemm8_auto(M, N, r, rows_per_member, EPI_NONE) : 128);
     if (tsel == 10 && gemm8n_ok(r, rows_per_member)) {   // else: kernel 8's VALU-epilogue path, as kernel 8 does
         EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_gemm: operand > 2 GiB");
         return launch_gemm8n(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
@@ -3117,6 +3144,7 @@ int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, i
     }
     const EpiArgs ea{(const unsigned short*)res, ldr, (const unsigned short*)gate, gstride, rows_per_group};
     const int64_t rpm = r ? rows_per_member : (M > 0 ? M : 1);
+    if (kernel == 0) kernel = gemm8_auto(M, N, r, rpm, epi);
     if (kernel == 10)
         return launch_gemm8n(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rpm, M, N, K, Y, ldy, epi,
                              ea, as_stream(stream));

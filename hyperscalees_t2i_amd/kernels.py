@@ -367,10 +367,17 @@ def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T:
     return out
 
 
-def gemm_tile_for(M: int, N: int) -> int:
-    """Kernel libeggroll's automatic choice uses for an M x N LoRA GEMM (mirrors eggroll_lora_gemm):
-    8 = the 8-phase 256x256 kernel, 128 = the 128x128 one-barrier tile."""
-    return 8 if (M // 256) * ((N + 255) // 256) >= 512 else 128
+def gemm_tile_for(M: int, N: int, r: int = 2, rows_per_member: int = 1 << 30) -> int:
+    """Kernel libeggroll's automatic choice uses for an M x N LoRA GEMM without an epilogue op (mirrors
+    lora_gemm_impl / gemm8_auto): 8 = the 8-phase 256x256 kernel, 10 = the 8-phase 256x320 kernel,
+    128 = the 128x128 one-barrier tile."""
+    if (M // 256) * ((N + 255) // 256) < 512:
+        return 128
+    if not (r == 0 or (r <= 2 and rows_per_member >= 256)):
+        return 8
+    tm = -(-M // 256)
+    rounds8, rounds10 = -(-(tm * -(-N // 256)) // 256), -(-(tm * -(-N // 320)) // 256)
+    return 10 if 122 * rounds10 < 100 * rounds8 else 8
 
 
 def lora_project(x: torch.Tensor, theta_pop: torch.Tensor, offA: int, r: int, rows_per_member: int,

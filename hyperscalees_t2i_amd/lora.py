@@ -70,14 +70,15 @@ class GemmTimer:
     @classmethod
     def summary(cls) -> Dict[str, Dict[str, float]]:
         """Per GEMM kernel variant (what rocprof names: k_lora_gemm8<r> = the 8-phase 256x256 tile,
-        k_lora_gemm<r,Tile<128>>) and "all": launches, total/avg kernel time, algorithmic FLOP =
-        2MNK (base) + 2MNr (rank-r LoRA expansion in the epilogue).  "k_lora_project<r>": the
-        projection pre-pass, algorithmic bytes = X (2MK) + T (4Mr) + the members' A rows (4 n_k r K)."""
+        k_lora_gemm8n<r> = the 8-phase 256x320 tile, k_lora_gemm<r,Tile<128>>) and "all": launches,
+        total/avg kernel time, algorithmic FLOP = 2MNK (base) + 2MNr (rank-r LoRA expansion in the
+        epilogue).  "k_lora_project<r>": the projection pre-pass, algorithmic bytes = X (2MK) + T (4Mr)
+        + the members' A rows (4 n_k r K)."""
         torch.cuda.synchronize()
         out: Dict[str, Dict[str, float]] = {}
         for e0, e1, e2, M, N, Kd, r, rpm in cls.records:
-            t = K.gemm_tile_for(M, N)
-            name = f"k_lora_gemm8<{r}>" if t == 8 else f"k_lora_gemm<{r},Tile<{t}>>"
+            t = K.gemm_tile_for(M, N, r, rpm)
+            name = {8: f"k_lora_gemm8<{r}>", 10: f"k_lora_gemm8n<{r}>"}.get(t, f"k_lora_gemm<{r},Tile<{t}>>")
             ms = e1.elapsed_time(e2)
             fl = 2.0 * M * N * Kd + 2.0 * M * N * r
             for key in (name, "all"):

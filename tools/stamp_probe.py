@@ -15,7 +15,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-OUT = ROOT / "tools" / "_stamps" / "libeggroll_stamps.so"  # tools/_build is not sent to the GPU box
+OUT = ROOT / "tools" / "_stamplib" / "libeggroll_stamps.so"  # build only for a stamp run, delete after (13 MB)
 
 
 def build():
@@ -76,15 +76,18 @@ def main():
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     T = torch.randn(M, 2, device=dev)
 
-    def gemm():
+    def gemm(kern=8):
         rc = lib.eggroll_lora_gemm_sel(ctypes.c_void_p(x.data_ptr()), ctypes.c_int64(Kd), ctypes.c_void_p(W.data_ptr()),
                                        ctypes.c_int64(Kd), ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(T.data_ptr()),
                                        ctypes.c_void_p(tp.data_ptr()), ctypes.c_int64(tp.stride(0)),
                                        ctypes.c_int64(2 * Kd), ctypes.c_int32(2), ctypes.c_float(4.0),
                                        ctypes.c_int64(rpm), ctypes.c_int64(M), ctypes.c_int64(N), ctypes.c_int64(Kd),
-                                       ctypes.c_void_p(y.data_ptr()), ctypes.c_int64(N), ctypes.c_int32(8), st)
+                                       ctypes.c_void_p(y.data_ptr()), ctypes.c_int64(N), ctypes.c_int32(kern), st)
         assert rc == 0
     report("k_lora_gemm8<2> 131072x2240x2240", 512 * 9, gemm)
+    report("k_lora_gemm8n<2> (256x320) 131072x2240x2240", 512 * 7, lambda: gemm(10))
+    if len(sys.argv) > 1 and sys.argv[1] == "gemm":
+        return
     del x, y
 
     # DC-AE ResBlock convs (8 images): 128 ch at 1024^2 (512x128 tile), 256 at 512^2, 512 at 256^2
@@ -123,6 +126,6 @@ def main():
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "build":
-        build()
+        build()   # usage: python tools/stamp_probe.py build; then [gemm] on the GPU
     else:
         main()
