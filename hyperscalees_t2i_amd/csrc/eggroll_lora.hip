@@ -775,7 +775,12 @@ __device__ __forceinline__ void lora_epilogue(f32x4 (&acc)[WTM / 16][WTN / 16], 
 //   EPI_RES   : out = bf16(res + y)                        (x = x + attn2(...))
 //   EPI_GATED : out = bf16(res + gate[row / rpg] * y)      (x += gate * attn1(...), k_gated_residual)
 // res may alias Y (each element is read and written by the same lane).
-enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3 };
+// fp32 residual stream (Sana blocks) — res is an fp32 [M, ldr] stream updated in place,
+// Y (optional, may be NULL) receives its bf16 shadow copy (the next GEMM's operand):
+//   EPI_RES32   : res = res + float(y)                     (x = x + attn2(...))
+//   EPI_GATED32 : res = fma(gate32[row / rpg], float(y), res)  (x += gate * attn1(...); gate fp32)
+// The same expressions as eggroll_gated_residual_f32, so fused == unfused bit for bit.
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3, EPI_RES32 = 4, EPI_GATED32 = 5 };
 struct EpiArgs {
     const unsigned short* res;
     int64_t ldr;
@@ -822,6 +827,44 @@ __device__ __forceinline__ u16x8 epi_apply(u16x8 v, int row, int col, const EpiA
     }
     return v;
 }
+// EPI_RES32 / EPI_GATED32 on one 8-column chunk (vector) or one element (tail)
+template <int EPI>
+__device__ __forceinline__ void epi_store32(u16x8 v, int row, int col, const EpiArgs& ea, unsigned short* Y, int64_t ldy) {
+    float* r = const_cast<float*>(reinterpret_cast<const float*>(ea.res)) + (int64_t)row * ea.ldr + col;
+    float4 a0 = *reinterpret_cast<const float4*>(r), a1 = *reinterpret_cast<const float4*>(r + 4);
+    float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    if constexpr (EPI == EPI_GATED32) {
+        const float* g = reinterpret_cast<const float*>(ea.gate) + (row / ea.rpg) * ea.gstride + col;
+        const float4 g0 = *reinterpret_cast<const float4*>(g), g1 = *reinterpret_cast<const float4*>(g + 4);
+        const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = __builtin_fmaf(gv[u], bf16_to_f32(v[u]), x[u]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = x[u] + bf16_to_f32(v[u]);
+    }
+    *reinterpret_cast<float4*>(r) = float4{x[0], x[1], x[2], x[3]};
+    *reinterpret_cast<float4*>(r + 4) = float4{x[4], x[5], x[6], x[7]};
+    if (Y) {
+        u16x8 o;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = f32_to_bf16(x[u]);
+        *reinterpret_cast<u16x8*>(Y + (int64_t)row * ldy + col) = o;
+    }
+}
+template <int EPI>
+__device__ __forceinline__ void epi_store32_1(unsigned short v, int row, int col, const EpiArgs& ea, unsigned short* Y,
+                                              int64_t ldy) {
+    float* r = const_cast<float*>(reinterpret_cast<const float*>(ea.res)) + (int64_t)row * ea.ldr + col;
+    float x = *r;
+    if constexpr (EPI == EPI_GATED32)
+        x = __builtin_fmaf(reinterpret_cast<const float*>(ea.gate)[(row / ea.rpg) * ea.gstride + col], bf16_to_f32(v), x);
+    else
+        x = x + bf16_to_f32(v);
+    *r = x;
+    if (Y) Y[(int64_t)row * ldy + col] = f32_to_bf16(x);
+}
+
 template <int EPI>
 __device__ __forceinline__ unsigned short epi_apply1(unsigned short v, int row, int col, const EpiArgs& ea) {
     if constexpr (EPI == EPI_SILU) return f32_to_bf16(epi_silu(bf16_to_f32(v)));
@@ -853,10 +896,12 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
         }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+    constexpr bool E32 = EPI == EPI_RES32 || EPI == EPI_GATED32;
     const bool full = m0 + rbase + 128 <= M && n0 + cbase + 64 <= N && (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0;
     const bool epi_vec = EPI == EPI_NONE || EPI == EPI_SILU ||
                          ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
-                          (EPI != EPI_GATED || ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0)));
+                          ((EPI != EPI_GATED && EPI != EPI_GATED32) ||
+                           ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0)));
     if (full && epi_vec) {  // interior wave tile: all 16 row reads in flight, then 16 unconditional 16-B stores
         u16x8 v[16];
 #pragma unroll
@@ -865,7 +910,12 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
             v[it] = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
         }
         const int row0 = m0 + rbase + (lane >> 3), col0 = n0 + cbase + (lane & 7) * 8;
-        if constexpr (EPI != EPI_NONE) {
+        if constexpr (E32) {
+#pragma unroll
+            for (int it = 0; it < 16; ++it) epi_store32<EPI>(v[it], row0 + it * 8, col0, ea, Y, ldy);
+            return;
+        }
+        if constexpr (EPI != EPI_NONE && !E32) {
 #pragma unroll
             for (int it = 0; it < 16; ++it) v[it] = epi_apply<EPI>(v[it], row0 + it * 8, col0, ea);
         }
@@ -881,6 +931,13 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
         const int col = n0 + cbase + sl * 8;
         if (row >= M || col >= N) continue;
         u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+        if constexpr (E32) {
+            if (col + 8 <= N && epi_vec && (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0)
+                epi_store32<EPI>(v, row, col, ea, Y, ldy);
+            else
+                for (int u = 0; u < 8 && col + u < N; ++u) epi_store32_1<EPI>(v[u], row, col + u, ea, Y, ldy);
+            continue;
+        }
         unsigned short* dst = Y + (int64_t)row * ldy + col;
         if (col + 8 <= N && (((uintptr_t)dst) & 15) == 0 && epi_vec) {
             if constexpr (EPI != EPI_NONE) v = epi_apply<EPI>(v, row, col, ea);
@@ -1900,7 +1957,9 @@ static int launch_gemm8_epi(const void* X, int64_t ldx, const void* W, int64_t l
     switch (epi) {
         case EPI_SILU: EGG_GEMM8E_R(EPI_SILU); break;
         case EPI_RES: EGG_GEMM8E_R(EPI_RES); break;
-        default: EGG_GEMM8E_R(EPI_GATED); break;
+        case EPI_GATED: EGG_GEMM8E_R(EPI_GATED); break;
+        case EPI_RES32: EGG_GEMM8E_R(EPI_RES32); break;
+        default: EGG_GEMM8E_R(EPI_GATED32); break;
     }
 #undef EGG_GEMM8E_R
 #undef EGG_GEMM8E
@@ -1917,7 +1976,7 @@ static bool gemm8n_ok(int32_t r, int64_t rows_per_member) { return r == 0 || (r 
 // DESIGN §5).  131072 x 2240: 18 vs 14 x 1.22 rounds -> 10 (+3-6 % measured); 9600 x 2240: 2 vs 2 x 1.22
 // -> 8.  The residual / gated-residual epilogues stay on 8 (their loads slow kernel 10's store phase).
 static int gemm8_auto(int64_t M, int64_t N, int32_t r, int64_t rows_per_member, int32_t epi) {
-    if (!gemm8n_ok(r, rows_per_member) || epi == EPI_RES || epi == EPI_GATED) return 8;
+    if (!gemm8n_ok(r, rows_per_member) || (epi != EPI_NONE && epi != EPI_SILU)) return 8;
     const int64_t tm = (M + 255) / 256;
     const int64_t rounds8 = (tm * ((N + 255) / 256) + 255) / 256, rounds10 = (tm * ((N + 319) / 320) + 255) / 256;
     return 122 * rounds10 < 100 * rounds8 ? 10 : 8;
@@ -3126,16 +3185,18 @@ int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, i
     if (epi == EPI_NONE)
         return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
                                            rows_per_member, M, N, K, Y, ldy, T_ws, kernel, stream);
-    EGG_CHECK_ARG(epi == EPI_SILU || epi == EPI_RES || epi == EPI_GATED, "lora_linear_pop_epi: epi=%d unknown", epi);
+    EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_GATED32, "lora_linear_pop_epi: epi=%d unknown", epi);
+    EGG_CHECK_ARG(kernel != 10 || epi <= EPI_GATED, "lora_linear_pop_epi: the fp32-stream epilogues run on kernel 8");
     EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
     EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
     EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "lora_linear_pop_epi: need K %% 64 == 0");
     EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop_epi: bad strides");
     EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_linear_pop_epi: M/N too large");
     EGG_CHECK_ARG(epi == EPI_SILU || (res && ldr >= N), "lora_linear_pop_epi: res NULL or ldr < N");
-    EGG_CHECK_ARG(epi != EPI_GATED || (gate && gstride >= N && rows_per_group > 0), "lora_linear_pop_epi: bad gate");
+    EGG_CHECK_ARG((epi != EPI_GATED && epi != EPI_GATED32) || (gate && gstride >= N && rows_per_group > 0),
+                  "lora_linear_pop_epi: bad gate");
     if (M == 0) return EGGROLL_OK;
-    EGG_CHECK_ARG(X && W && Y, "lora_linear_pop_epi: NULL pointer");
+    EGG_CHECK_ARG(X && W && (Y || epi >= EPI_RES32), "lora_linear_pop_epi: NULL pointer");
     EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_linear_pop_epi: operand > 2 GiB");
     if (r > 0) {
         EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop_epi: theta_pop / T_ws NULL with r > 0");

@@ -245,12 +245,27 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 // Covers DC-AE RMSNorm(+bias)(+residual)(+ReLU), Sana q/k/caption RMSNorm, and the Sana AdaLN
 // "layer_norm(x) * (1 + scale) + shift" of every block and of norm_out.
 // ------------------------------------------------------------------------------------
-template <int SEG, int NCH>
-__global__ __launch_bounds__(256) void k_rownorm(const unsigned short* __restrict__ x, int64_t rows, int C, float eps,
+// 8 consecutive values of a bf16 (f32 = 0) or fp32 (f32 = 1) vector as floats
+__device__ __forceinline__ void load8f(const void* p, int f32, int64_t off, float (&o)[8]) {
+    if (f32) {
+        const float4 a0 = *reinterpret_cast<const float4*>((const float*)p + off);
+        const float4 a1 = *reinterpret_cast<const float4*>((const float*)p + off + 4);
+        o[0] = a0.x; o[1] = a0.y; o[2] = a0.z; o[3] = a0.w; o[4] = a1.x; o[5] = a1.y; o[6] = a1.z; o[7] = a1.w;
+    } else {
+        const u16x8m q = *reinterpret_cast<const u16x8m*>((const unsigned short*)p + off);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = b2f(q[i]);
+    }
+}
+
+// XF: x is fp32 (the fp32 residual stream of the Sana blocks); mf32: the modulation
+// vectors mscale / mshift are fp32 (the fp32 AdaLN modulation).  Output bf16 (a GEMM operand).
+template <int SEG, int NCH, bool XF>
+__global__ __launch_bounds__(256) void k_rownorm(const void* __restrict__ x, int64_t rows, int C, float eps,
                                                  int layer, const unsigned short* __restrict__ w,
                                                  const unsigned short* __restrict__ b,
-                                                 const unsigned short* __restrict__ mscale,
-                                                 const unsigned short* __restrict__ mshift, int64_t mstride,
+                                                 const void* __restrict__ mscale,
+                                                 const void* __restrict__ mshift, int64_t mstride, int mf32,
                                                  int64_t rows_per_group, int act,
                                                  const unsigned short* __restrict__ res,
                                                  unsigned short* __restrict__ out) {
@@ -259,16 +274,16 @@ __global__ __launch_bounds__(256) void k_rownorm(const unsigned short* __restric
     const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / SEG;
     const bool live = row < rows;
     const int nchunks = C / 8;
-    const unsigned short* xr = x + (live ? row : 0) * C;
+    const int64_t xoff = (live ? row : 0) * C;
     float v[NCH][8];
     float s1 = 0.f;
 #pragma unroll
     for (int t = 0; t < NCH; ++t) {
         const int ci = seg_lane + t * SEG;
         if (live && ci < nchunks) {
-            const u16x8m q = *reinterpret_cast<const u16x8m*>(xr + ci * 8);
+            load8f(x, XF, xoff + ci * 8, v[t]);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) { v[t][i] = b2f(q[i]); s1 += v[t][i]; }
+            for (int i = 0; i < 8; ++i) s1 += v[t][i];
         } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[t][i] = 0.f;
@@ -295,28 +310,28 @@ __global__ __launch_bounds__(256) void k_rownorm(const unsigned short* __restric
         const int ci = seg_lane + t * SEG;
         if (ci >= nchunks) continue;
         const int c0 = ci * 8;
-        float y[8];
+        float y[8], q[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) y[i] = (v[t][i] - mean) * rstd;
         if (w) {
-            const u16x8m q = *reinterpret_cast<const u16x8m*>(w + c0);
+            load8f(w, 0, c0, q);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) y[i] *= b2f(q[i]);
+            for (int i = 0; i < 8; ++i) y[i] *= q[i];
         }
         if (mscale) {
-            const u16x8m q = *reinterpret_cast<const u16x8m*>(mscale + g * mstride + c0);
+            load8f(mscale, mf32, g * mstride + c0, q);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) y[i] *= 1.0f + b2f(q[i]);
+            for (int i = 0; i < 8; ++i) y[i] *= 1.0f + q[i];
         }
         if (mshift) {
-            const u16x8m q = *reinterpret_cast<const u16x8m*>(mshift + g * mstride + c0);
+            load8f(mshift, mf32, g * mstride + c0, q);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) y[i] += b2f(q[i]);
+            for (int i = 0; i < 8; ++i) y[i] += q[i];
         }
         if (b) {
-            const u16x8m q = *reinterpret_cast<const u16x8m*>(b + c0);
+            load8f(b, 0, c0, q);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) y[i] += b2f(q[i]);
+            for (int i = 0; i < 8; ++i) y[i] += q[i];
         }
         if (act == 1) {
 #pragma unroll
@@ -326,9 +341,9 @@ __global__ __launch_bounds__(256) void k_rownorm(const unsigned short* __restric
             for (int i = 0; i < 8; ++i) y[i] = silu(y[i]);
         }
         if (res) {
-            const u16x8m q = *reinterpret_cast<const u16x8m*>(res + row * C + c0);
+            load8f(res, 0, row * C + c0, q);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) y[i] += b2f(q[i]);
+            for (int i = 0; i < 8; ++i) y[i] += q[i];
         }
         u16x8m o;
 #pragma unroll
@@ -423,6 +438,40 @@ __global__ __launch_bounds__(256) void k_gated_residual(unsigned short* __restri
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = f2b(b2f(xv[k]) + b2f(gv[k]) * b2f(yv[k]));
     *reinterpret_cast<u16x8m*>(x + row * C + c0) = o;
+}
+
+// fp32 residual stream update (Sana blocks):  x[r, c] = fma(gate[g, c], y[r, c], x[r, c])
+// (x fp32 in place, y bf16, gate bf16 or fp32 (g32) or NULL = 1: x += y), optionally also writing the
+// bf16 shadow copy of x that the next GEMM reads.  The same expression as the fused GEMM epilogues
+// EPI_RES32 / EPI_GATED32 of eggroll_lora.hip, so fused == unfused bit for bit.
+__global__ __launch_bounds__(256) void k_gated_residual_f32(float* __restrict__ x, const unsigned short* __restrict__ y,
+                                                            const void* __restrict__ gate, int g32, int64_t gstride,
+                                                            int64_t rows_per_group, int C, int64_t total_chunks,
+                                                            unsigned short* __restrict__ shadow) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total_chunks) return;
+    const int nch = C / 8;
+    const int64_t row = i / nch;
+    const int c0 = (int)(i - row * nch) * 8;
+    float xv[8], yv[8], gv[8];
+    load8f(x, 1, row * C + c0, xv);
+    load8f(y, 0, row * C + c0, yv);
+    if (gate) {
+        load8f(gate, g32, (row / rows_per_group) * gstride + c0, gv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xv[k] = __builtin_fmaf(gv[k], yv[k], xv[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xv[k] = xv[k] + yv[k];
+    }
+    *reinterpret_cast<float4*>(x + row * C + c0) = float4{xv[0], xv[1], xv[2], xv[3]};
+    *reinterpret_cast<float4*>(x + row * C + c0 + 4) = float4{xv[4], xv[5], xv[6], xv[7]};
+    if (shadow) {
+        u16x8m o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = f2b(xv[k]);
+        *reinterpret_cast<u16x8m*>(shadow + row * C + c0) = o;
+    }
 }
 
 // y = act(bf16(y + bias[c])) in place (conv bias folded into the activation pass; torch's conv2d
@@ -1194,39 +1243,57 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
 }
 
 template <int SEG, int NCH>
-static void launch_rownorm(const void* x, int64_t rows, int C, float eps, int layer, const void* w, const void* b,
-                           const void* ms, const void* mh, int64_t mstride, int64_t rpg, int act, const void* res,
-                           void* out, hipStream_t st) {
+static void launch_rownorm(const void* x, int xf32, int64_t rows, int C, float eps, int layer, const void* w,
+                           const void* b, const void* ms, const void* mh, int64_t mstride, int mf32, int64_t rpg,
+                           int act, const void* res, void* out, hipStream_t st) {
     const int64_t threads = rows * SEG;
-    hipLaunchKernelGGL((k_rownorm<SEG, NCH>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
-                       (const unsigned short*)x, rows, C, eps, layer, (const unsigned short*)w,
-                       (const unsigned short*)b, (const unsigned short*)ms, (const unsigned short*)mh, mstride, rpg,
-                       act, (const unsigned short*)res, (unsigned short*)out);
+    const dim3 grid((unsigned)((threads + 255) / 256));
+    if (xf32)
+        hipLaunchKernelGGL((k_rownorm<SEG, NCH, true>), grid, dim3(256), 0, st, x, rows, C, eps, layer,
+                           (const unsigned short*)w, (const unsigned short*)b, ms, mh, mstride, mf32, rpg, act,
+                           (const unsigned short*)res, (unsigned short*)out);
+    else
+        hipLaunchKernelGGL((k_rownorm<SEG, NCH, false>), grid, dim3(256), 0, st, x, rows, C, eps, layer,
+                           (const unsigned short*)w, (const unsigned short*)b, ms, mh, mstride, mf32, rpg, act,
+                           (const unsigned short*)res, (unsigned short*)out);
+}
+
+extern "C" int eggroll_rownorm_ex(const void* x, int32_t x_f32, int64_t rows, int64_t C, float eps, int32_t layer,
+                                  const void* w, const void* b, const void* mscale, const void* mshift,
+                                  int64_t mstride, int32_t mod_f32, int64_t rows_per_group, int32_t act,
+                                  const void* res, void* out, void* stream) {
+    EGG_CHECK_ARG(rows >= 0 && C > 0 && C % 8 == 0 && C <= 8 * 64 * 8, "rownorm: need C %% 8 == 0, C <= 4096");
+    EGG_CHECK_ARG(act >= 0 && act <= 2 && rows_per_group > 0, "rownorm: bad act / rows_per_group");
+    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 && (!res || ((uintptr_t)res & 15) == 0) &&
+                      (!mscale || ((uintptr_t)mscale & 15) == 0) && (!mshift || ((uintptr_t)mshift & 15) == 0),
+                  "rownorm: pointers must be 16-byte aligned");
+    EGG_CHECK_ARG(mstride % 8 == 0, "rownorm: modulation stride must be a multiple of 8");
+    EGG_CHECK_ARG((x_f32 == 0 || x_f32 == 1) && (mod_f32 == 0 || mod_f32 == 1), "rownorm: x_f32 / mod_f32 are 0 or 1");
+    if (rows == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(x && out, "rownorm: NULL pointer");
+    hipStream_t st = as_stream(stream);
+    const int nch = (int)(C / 8);
+#define EGG_RN(S_, N_) launch_rownorm<S_, N_>(x, x_f32, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, mod_f32, \
+                                              rows_per_group, act, res, out, st)
+    if (nch <= 16) EGG_RN(16, 1);
+    else if (nch <= 32) EGG_RN(32, 1);
+    else if (nch <= 64) EGG_RN(64, 1);
+    else if (nch <= 128) EGG_RN(64, 2);
+    else if (nch <= 256) EGG_RN(64, 4);
+    // Sana's C = 2240 (280 chunks): 5 chunks per lane use 88 % of the slots (8: 55 %, 64 dead value
+    // registers); a lane sums the same chunks in the same order either way, so the bits do not change
+    else if (nch <= 320) EGG_RN(64, 5);
+    else EGG_RN(64, 8);
+#undef EGG_RN
+    EGG_CHECK_LAUNCH("rownorm");
+    return EGGROLL_OK;
 }
 
 extern "C" int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps, int32_t layer, const void* w,
                                const void* b, const void* mscale, const void* mshift, int64_t mstride,
                                int64_t rows_per_group, int32_t act, const void* res, void* out, void* stream) {
-    EGG_CHECK_ARG(rows >= 0 && C > 0 && C % 8 == 0 && C <= 8 * 64 * 8, "rownorm: need C %% 8 == 0, C <= 4096");
-    EGG_CHECK_ARG(act >= 0 && act <= 2 && rows_per_group > 0, "rownorm: bad act / rows_per_group");
-    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 && (!res || ((uintptr_t)res & 15) == 0),
-                  "rownorm: pointers must be 16-byte aligned");
-    EGG_CHECK_ARG(mstride % 8 == 0, "rownorm: modulation stride must be a multiple of 8");
-    if (rows == 0) return EGGROLL_OK;
-    EGG_CHECK_ARG(x && out, "rownorm: NULL pointer");
-    hipStream_t st = as_stream(stream);
-    const int nch = (int)(C / 8);
-    if (nch <= 16) launch_rownorm<16, 1>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
-    else if (nch <= 32) launch_rownorm<32, 1>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
-    else if (nch <= 64) launch_rownorm<64, 1>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
-    else if (nch <= 128) launch_rownorm<64, 2>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
-    else if (nch <= 256) launch_rownorm<64, 4>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
-    // Sana's C = 2240 (280 chunks): 5 chunks per lane use 88 % of the slots (8: 55 %, 64 dead value
-    // registers); a lane sums the same chunks in the same order either way, so the bits do not change
-    else if (nch <= 320) launch_rownorm<64, 5>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
-    else launch_rownorm<64, 8>(x, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, rows_per_group, act, res, out, st);
-    EGG_CHECK_LAUNCH("rownorm");
-    return EGGROLL_OK;
+    return eggroll_rownorm_ex(x, 0, rows, C, eps, layer, w, b, mscale, mshift, mstride, 0, rows_per_group, act, res,
+                              out, stream);
 }
 
 extern "C" int eggroll_resid_layernorm(float* h, int64_t ldh, const void* y, int64_t ldy, int64_t rows, int64_t C,
@@ -1269,6 +1336,24 @@ extern "C" int eggroll_gated_residual(void* x, const void* y, const void* gate, 
                        (unsigned short*)x, (const unsigned short*)y, (const unsigned short*)gate, gstride,
                        rows_per_group, (int)C, total);
     EGG_CHECK_LAUNCH("gated_residual");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_gated_residual_f32(float* x, const void* y, const void* gate, int32_t gate_f32, int64_t gstride,
+                                          int64_t rows, int64_t C, int64_t rows_per_group, void* shadow, void* stream) {
+    EGG_CHECK_ARG(rows >= 0 && C > 0 && C % 8 == 0 && gstride % 8 == 0 && rows_per_group > 0 &&
+                      (gate_f32 == 0 || gate_f32 == 1),
+                  "gated_residual_f32: bad sizes");
+    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)gate & 15) == 0 &&
+                      ((uintptr_t)shadow & 15) == 0,
+                  "gated_residual_f32: pointers must be 16-byte aligned");
+    if (rows == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(x && y, "gated_residual_f32: NULL pointer");
+    const int64_t total = rows * (C / 8);
+    hipLaunchKernelGGL(k_gated_residual_f32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream), x,
+                       (const unsigned short*)y, gate, gate_f32, gstride, rows_per_group, (int)C, total,
+                       (unsigned short*)shadow);
+    EGG_CHECK_LAUNCH("gated_residual_f32");
     return EGGROLL_OK;
 }
 

@@ -301,7 +301,7 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
     return out
 
 
-EPI = {None: 0, "silu": 1, "res": 2, "gated": 3}
+EPI = {None: 0, "silu": 1, "res": 2, "gated": 3, "res32": 4, "gated32": 5}
 
 
 def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], theta_pop: Optional[torch.Tensor],
@@ -312,6 +312,8 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
     """lora_linear_pop with an epilogue op on the bf16 output y (eggroll_lora_linear_pop_epi_sel):
     "silu": silu(y); "res": res + y; "gated": res + gate[row // rows_per_group] * y.  With res given and
     out None the result is written into res (in place, as the residual adds it replaces).
+    "res32" / "gated32": res is the fp32 residual stream, updated in place (res + y /
+    fma(gate, y, res), gate fp32); out (optional) receives its bf16 shadow; returns res.
     kernel: 0 automatic, 8 / 10 the 256x256 / 256x320 8-phase kernels (A/B measurement)."""
     _dev(x, "lora_linear_pop_epi(x)", torch.bfloat16)
     _dev(W, "lora_linear_pop_epi(W)", torch.bfloat16)
@@ -319,12 +321,17 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
     N = W.shape[0]
     code = EPI[epi]
     if res is not None:
-        _dev(res, "lora_linear_pop_epi(res)", torch.bfloat16)
+        _dev(res, "lora_linear_pop_epi(res)", torch.float32 if code >= 4 else torch.bfloat16)
         if res.shape[-1] != N or res.numel() != M * N:
             raise ValueError(f"res {tuple(res.shape)} does not match [{M}, {N}]")
-    if out is None:
+    if code >= 4:
+        if res is None or (code == 5 and (gate is None or gate.dtype != torch.float32)):
+            raise ValueError(f"lora_linear_pop_epi({epi}): needs an fp32 res (and an fp32 gate)")
+        if out is not None:
+            _dev(out, "lora_linear_pop_epi(out)", torch.bfloat16)
+    elif out is None:
         out = res if res is not None and code in (2, 3) else torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
-    pg, gst = _row_ptr(gate, "lora_linear_pop_epi(gate)", N) if gate is not None else (None, 0)
+    pg, gst = _row_ptr(gate, "lora_linear_pop_epi(gate)", N, allow_f32=code == 5) if gate is not None else (None, 0)
     if r > 0:
         _dev(theta_pop, "lora_linear_pop_epi(theta_pop)", torch.float32)
         need = lora_workspace_numel(M, Kd, r, rows_per_member)
@@ -332,9 +339,9 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
             T_ws = torch.empty(need, dtype=torch.float32, device=x.device)
     _lib.call("eggroll_lora_linear_pop_epi_sel", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
               _p(theta_pop) if r > 0 else None, theta_pop.stride(0) if r > 0 else 0, offA, offB, r, float(scale),
-              rows_per_member, M, N, Kd, out.data_ptr(), N, _p(T_ws) if r > 0 else None, code,
+              rows_per_member, M, N, Kd, _p(out), N, _p(T_ws) if r > 0 else None, code,
               _p(res), N if res is not None else 0, pg, gst or N, int(rows_per_group), int(kernel), _stream(x.device))
-    return out
+    return res if code >= 4 else out
 
 
 def lora_workspace_numel(M: int, K: int, r: int, rows_per_member: int) -> int:
@@ -526,12 +533,14 @@ def dwconv_pw_nhwc(x: torch.Tensor, w_t: torch.Tensor, pw: torch.Tensor, ks: int
     return out
 
 
-def _row_ptr(t: Optional[torch.Tensor], what: str, C: int):
-    """Pointer + row stride of a [groups, C]-shaped (possibly strided) bf16 view."""
+def _row_ptr(t: Optional[torch.Tensor], what: str, C: int, allow_f32: bool = False):
+    """Pointer + row stride of a [groups, C]-shaped (possibly strided) bf16 (or, allow_f32, fp32) view."""
     if t is None:
         return None, 0
-    if t.device.type != "cuda" or t.dtype != torch.bfloat16 or t.stride(-1) != 1:
-        raise _lib.EggrollError(f"{what}: expected a bf16 device view with unit inner stride")
+    ok = (torch.bfloat16, torch.float32) if allow_f32 else (torch.bfloat16,)
+    if t.device.type != "cuda" or t.dtype not in ok or t.stride(-1) != 1:
+        raise _lib.EggrollError(f"{what}: expected a {'bf16 / fp32' if allow_f32 else 'bf16'} device view with "
+                                f"unit inner stride")
     stride = t.stride(0) if t.dim() > 1 and t.shape[0] > 1 else C
     return t.data_ptr(), stride
 
@@ -544,23 +553,30 @@ def rownorm(x: torch.Tensor, eps: float, layer: bool = False, w: Optional[torch.
             mshift: Optional[torch.Tensor] = None, rows_per_group: int = 1, act=None,
             res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused (RMS|Layer)Norm over the last dim [+w][*(1+mscale[g])][+mshift[g]][+b][act][+res].
-    mscale / mshift: [groups, C] views (rows `mstride` apart), g = row // rows_per_group."""
-    _dev(x, "rownorm(x)", torch.bfloat16)
+    mscale / mshift: [groups, C] views (rows `mstride` apart), g = row // rows_per_group.
+    x may be fp32 (the fp32 residual stream) and mscale / mshift fp32 (the fp32 modulation); the
+    output is bf16 (eggroll_rownorm_ex)."""
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        raise _lib.EggrollError("rownorm(x): expected bf16 or fp32")
+    _dev(x, "rownorm(x)", x.dtype)
     C = x.shape[-1]
     rows = x.numel() // C
     if out is None:
-        out = torch.empty_like(x)
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
     for t, nm in ((w, "w"), (b, "b"), (res, "res")):
         if t is not None:
             _dev(t, f"rownorm({nm})", torch.bfloat16)
-    ps, st1 = _row_ptr(mscale, "rownorm(mscale)", C)
-    ph, st2 = _row_ptr(mshift, "rownorm(mshift)", C)
-    if ps is not None and ph is not None and st1 != st2:
-        raise ValueError("mscale / mshift must share a row stride")
+    ps, st1 = _row_ptr(mscale, "rownorm(mscale)", C, allow_f32=True)
+    ph, st2 = _row_ptr(mshift, "rownorm(mshift)", C, allow_f32=True)
+    if ps is not None and ph is not None and (st1 != st2 or mscale.dtype != mshift.dtype):
+        raise ValueError("mscale / mshift must share a row stride and a dtype")
+    mf32 = int(any(t is not None and t.dtype == torch.float32 for t in (mscale, mshift)))
+    xf32 = int(x.dtype == torch.float32)
     e0 = OpTimer.begin()
-    _lib.call("eggroll_rownorm", x.data_ptr(), rows, C, float(eps), int(bool(layer)), _p(w), _p(b), ps, ph,
-              st1 or st2 or C, int(rows_per_group), ACT[act], _p(res), out.data_ptr(), _stream(x.device))
-    OpTimer.end(e0, f"rownorm(C={C})", 2.0 * rows * C * (3 if res is not None else 2), f"rows{rows}")
+    _lib.call("eggroll_rownorm_ex", x.data_ptr(), xf32, rows, C, float(eps), int(bool(layer)), _p(w), _p(b), ps, ph,
+              st1 or st2 or C, mf32, int(rows_per_group), ACT[act], _p(res), out.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, f"rownorm(C={C})", (2.0 + 2 * xf32) * rows * C + 2.0 * rows * C * (2 if res is not None else 1),
+                f"rows{rows}")
     return out
 
 
@@ -576,6 +592,27 @@ def gated_residual_(x: torch.Tensor, y: torch.Tensor, gate: torch.Tensor, rows_p
     OpTimer.end(e0, "gated_residual", 6.0 * x.numel())
     return x
 
+
+
+def gated_residual_f32_(x: torch.Tensor, y: torch.Tensor, gate: Optional[torch.Tensor], rows_per_group: int = 1,
+                        shadow: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 residual stream update in place: x = fma(gate[g], y, x) (gate bf16 / fp32 [groups, C] view;
+    None: x += y), y bf16; shadow (optional bf16, x's shape) receives bf16(x)
+    (eggroll_gated_residual_f32 — the unfused form of the EPI_RES32 / EPI_GATED32 GEMM epilogues)."""
+    _dev(x, "gated_residual_f32(x)", torch.float32)
+    _dev(y, "gated_residual_f32(y)", torch.bfloat16)
+    C = x.shape[-1]
+    if y.numel() != x.numel() or y.shape[-1] != C:
+        raise ValueError(f"gated_residual_f32: y {tuple(y.shape)} does not match x {tuple(x.shape)}")
+    if shadow is not None:
+        _dev(shadow, "gated_residual_f32(shadow)", torch.bfloat16)
+    pg, st = _row_ptr(gate, "gated_residual_f32(gate)", C, allow_f32=True)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_gated_residual_f32", x.data_ptr(), y.data_ptr(), pg,
+              int(gate is not None and gate.dtype == torch.float32), st or C, x.numel() // C, C, int(rows_per_group),
+              _p(shadow), _stream(x.device))
+    OpTimer.end(e0, "gated_residual_f32", (10.0 + (2 if shadow is not None else 0)) * x.numel(), f"rows{x.numel() // C}")
+    return x
 
 def resid_layernorm_(h: torch.Tensor, y: Optional[torch.Tensor], w: torch.Tensor, b: torch.Tensor, eps: float,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:

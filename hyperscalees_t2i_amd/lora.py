@@ -139,11 +139,13 @@ class LoRALinear(nn.Module):
 
     def forward(self, x: torch.Tensor, epi: Optional[str] = None, res: Optional[torch.Tensor] = None,
                 gate: Optional[torch.Tensor] = None, rows_per_group: int = 1,
-                T: Optional[torch.Tensor] = None) -> torch.Tensor:
+                T: Optional[torch.Tensor] = None, shadow: Optional[torch.Tensor] = None) -> torch.Tensor:
         """epi (optional): an elementwise op on the output, fused into the GEMM epilogue on the
         population path (kernels.lora_linear_pop_epi): "res" -> res + y, "gated" -> res + gate[g] * y,
-        both written into `res` in place and returned.  T (optional, population path): this linear's
-        X A_k^T already computed by shared_projection — only the GEMM + LoRA epilogue run here."""
+        both written into `res` in place and returned; "res32" / "gated32": the same on an fp32 residual
+        stream `res` (gate fp32), `shadow` (optional bf16) receiving bf16(res).  T (optional, population
+        path): this linear's X A_k^T already computed by shared_projection — only the GEMM + LoRA
+        epilogue run here."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if x2.dtype != torch.bfloat16:
@@ -153,6 +155,7 @@ class LoRALinear(nn.Module):
         ctx = self.ctx
         if epi is not None:
             res2 = res.view(M, self.out_features)
+            sh2 = shadow.view(M, self.out_features) if shadow is not None else None
             if (FUSE_EPILOGUES and self.r and ctx is not None and ctx.theta_pop is not None and self.r <= 2
                     and not GemmTimer.active
                     and M % ctx.n_members == 0 and M // ctx.n_members >= 256 and self.in_features % 64 == 0):
@@ -160,13 +163,15 @@ class LoRALinear(nn.Module):
                 ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device)
                 K.lora_linear_pop_epi(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
                                       self.r, self.scale, rpm, epi, res=res2, gate=gate, rows_per_group=rows_per_group,
-                                      T_ws=ws)
+                                      T_ws=ws, out=sh2)
                 return res
             y = self.forward(x).view(M, self.out_features)   # the same ops, unfused
             if epi == "res":
                 res2.add_(y)
             elif epi == "gated":
                 K.gated_residual_(res2, y, gate, rows_per_group=rows_per_group)
+            elif epi in ("res32", "gated32"):
+                K.gated_residual_f32_(res2, y, gate if epi == "gated32" else None, rows_per_group, shadow=sh2)
             else:
                 raise ValueError(f"LoRALinear: epi {epi!r} unsupported")
             return res
@@ -203,6 +208,44 @@ class LoRALinear(nn.Module):
         else:
             y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
         return y.view(*shp[:-1], self.out_features)
+
+
+    def _weight32(self) -> torch.Tensor:
+        key = (self.weight._version, self.weight.data_ptr())
+        if getattr(self, "_w32_key", None) != key:
+            self._w32 = (self.weight.detach().float(), None if self.bias is None else self.bias.detach().float())
+            self._w32_key = key
+        return self._w32
+
+    def forward_fp32(self, x: torch.Tensor) -> torch.Tensor:
+        """The PEFT LoRA linear in fp32 (torch GEMMs on fp32 copies of the frozen weight): y = x W^T + b
+        + s (x A_k^T) B_k^T with member k's factors from the population context (rows member-major) or this
+        module's own lora_A / lora_B.  For the small-M linears whose outputs set a whole member's
+        behaviour — the time / guidance embedding and AdaLN modulation, and proj_out (the transformer
+        output the reference rounds to fp16 only): their bf16 rounding was a measured source of
+        member-differential error at sigma = 1e-2 (tools/drift_probe.py)."""
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).float()
+        M = x2.shape[0]
+        W32, b32 = self._weight32()
+        y = torch.nn.functional.linear(x2, W32, b32)
+        ctx = self.ctx
+        if self.r and ctx is not None and ctx.theta_pop is not None:
+            n = ctx.n_members
+            if M % n:
+                raise RuntimeError(f"{M} rows do not split over {n} members")
+            tp = ctx.theta_pop
+            A = tp[:, self.theta_off_A:self.theta_off_A + self.r * self.in_features].view(n, self.r, self.in_features)
+            B = tp[:, self.theta_off_B:self.theta_off_B + self.out_features * self.r].view(n, self.out_features, self.r)
+            t = torch.bmm(x2.view(n, M // n, -1), A.transpose(1, 2))
+            y = y + self.scale * torch.bmm(t, B.transpose(1, 2)).view(M, -1)
+        elif self.r:
+            A, B = self.lora_A.weight.detach(), self.lora_B.weight.detach()
+            y = y + self.scale * ((x2 @ A.t()) @ B.t())
+        y = y.view(*shp[:-1], self.out_features)
+        for hook in self._forward_hooks.values():   # forward hooks see this path like __call__ (activation capture)
+            hook(self, (x,), y)
+        return y
 
 
 # Linears that read the same input (Sana attn1 to_q / to_k / to_v, attn2 to_k / to_v) get their LoRA

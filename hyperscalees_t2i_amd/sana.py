@@ -91,7 +91,15 @@ class CombinedTimestepGuidanceEmbeddings(nn.Module):
         self.guidance_embedder = TimestepEmbedding(256, dim)
         self.linear = LoRALinear(dim, 6 * dim, lora=False)
 
-    def forward(self, timestep, guidance):
+    def forward(self, timestep, guidance, fp32: bool = False):
+        """fp32: the whole chain in fp32 (LoRALinear.forward_fp32; B rows, negligible cost) — it sets every
+        token's AdaLN modulation, and its bf16 rounding was member-differential error."""
+        if fp32:
+            lf = lambda m, v: m.forward_fp32(v)  # noqa: E731
+            t = lf(self.timestep_embedder.linear_2, F.silu(lf(self.timestep_embedder.linear_1, timestep_embedding(timestep))))
+            g = lf(self.guidance_embedder.linear_2, F.silu(lf(self.guidance_embedder.linear_1, timestep_embedding(guidance))))
+            cond = t + g
+            return lf(self.linear, F.silu(cond)), cond
         t = self.timestep_embedder(timestep_embedding(timestep).to(torch.bfloat16))
         g = self.guidance_embedder(timestep_embedding(guidance).to(torch.bfloat16))
         cond = t + g
@@ -126,9 +134,10 @@ class LinearSelfAttention(nn.Module):
         self.to_v = LoRALinear(dim, inner, bias=False, lora=False)
         self.to_out = nn.ModuleList([LoRALinear(inner, dim, bias=True, lora=False)])
 
-    def forward(self, x, res=None, gate=None):  # x [B, N, D]
+    def forward(self, x, res=None, gate=None, shadow=None):  # x [B, N, D]
         """With res / gate: returns res += gate[image] * attn1(x), the gated residual fused into
-        to_out's GEMM epilogue (the block's `x + gate_msa * attn_output`)."""
+        to_out's GEMM epilogue (the block's `x + gate_msa * attn_output`); an fp32 res is the fp32
+        residual stream (gate fp32, shadow = its bf16 copy written in the same epilogue)."""
         B, N, D = x.shape
         Tq, Tk, Tv = lora.shared_projection([self.to_q, self.to_k, self.to_v], x)   # X read once for 3 LoRAs
         q = self.norm_q(self.to_q(x, T=Tq), act="relu").view(B * N, -1)   # RMS norm + ReLU fused
@@ -136,7 +145,8 @@ class LinearSelfAttention(nn.Module):
         v = self.to_v(x, T=Tv).view(B * N, -1)
         o = K.linear_attention(q, k, v, B, N, self.heads, self.head_dim, relu_qk=False)
         if res is not None:
-            return self.to_out[0](o.view(B, N, -1), epi="gated", res=res, gate=gate, rows_per_group=N)
+            epi = "gated32" if res.dtype == torch.float32 else "gated"
+            return self.to_out[0](o.view(B, N, -1), epi=epi, res=res, gate=gate, rows_per_group=N, shadow=shadow)
         return self.to_out[0](o.view(B, N, -1))
 
 
@@ -173,7 +183,7 @@ class CrossAttention(nn.Module):
             o = K.cross_attention(q, k, v, B, N, self.heads, hd, L, hd ** -0.5, bias=mask_bias.contiguous(),
                                   enc_index=enc_index).view(B, N, -1)
             if res is not None:   # res += to_out(o): the block's residual add fused into the GEMM epilogue
-                return self.to_out[0](o, epi="res", res=res)
+                return self.to_out[0](o, epi="res32" if res.dtype == torch.float32 else "res", res=res)
             return self.to_out[0](o)
         q = self.norm_q(self.to_q(x)).view(B, N, self.heads, hd)
         k = self.norm_k(self.to_k(enc)).view(U, L, self.heads, hd)
@@ -193,7 +203,7 @@ class CrossAttention(nn.Module):
             o = o[..., :hd]
         o = o.transpose(1, 2).reshape(B, N, -1)
         if res is not None:   # res += to_out(o): the block's residual add fused into the GEMM epilogue
-            return self.to_out[0](o, epi="res", res=res)
+            return self.to_out[0](o, epi="res32" if res.dtype == torch.float32 else "res", res=res)
         return self.to_out[0](o)
 
 
@@ -232,6 +242,25 @@ class SanaBlock(nn.Module):
         self.ff = GLUMBConv(D, int(a.mlp_ratio * D))
         self.scale_shift_table = nn.Parameter(torch.randn(6, D).div(D ** 0.5).to(torch.bfloat16), requires_grad=False)
 
+    def forward_fp32(self, x32, x16, enc, mask_bias, timestep, H, W, enc_index=None):
+        """The block on the fp32 residual stream x32 (updated in place; x16 = its bf16 shadow, the
+        GEMM operand of attn2's to_q) with the fp32 AdaLN modulation: every update of x is an fp32
+        add (fused into the GEMM epilogues / eggroll_gated_residual_f32) instead of a bf16 rounding,
+        the norms read x32 directly.  DESIGN §3.2: the bf16 residual stream was the largest single
+        source of member-differential drift in the transformer at sigma = 1e-2."""
+        B, N, D = x32.shape
+        mods = self.scale_shift_table.float()[None] + timestep.view(B, 6, -1)
+        n = K.rownorm(x32, self.eps, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=N)
+        if lora.FUSE_EPILOGUES:
+            self.attn1(n, res=x32, gate=mods[:, 2], shadow=x16)    # x32 += gate_msa * attn1(n); x16 = bf16(x32)
+            self.attn2(x16, enc, mask_bias, enc_index, res=x32)    # x32 += attn2(x16)
+        else:                                                      # the same ops unfused (bit-identical)
+            K.gated_residual_f32_(x32, self.attn1(n), mods[:, 2], rows_per_group=N, shadow=x16)
+            K.gated_residual_f32_(x32, self.attn2(x16, enc, mask_bias, enc_index), None, rows_per_group=N)
+        n = K.rownorm(x32, self.eps, layer=True, mscale=mods[:, 4], mshift=mods[:, 3], rows_per_group=N)
+        K.gated_residual_f32_(x32, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
+        return x32
+
     def forward(self, x, enc, mask_bias, timestep, H, W, enc_index=None):
         B, N, D = x.shape
         # [B, 6, D]: shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp
@@ -265,6 +294,9 @@ class SanaTransformer2DModel(nn.Module):
         # opt-in (exact, see forward): off by default so the bench runs the reference's full 300-token
         # cross-attention and caption projection (measured +0.8 % epoch throughput on the synthetic prompts)
         self.trim_caption_padding = False
+        # fp32 residual stream + fp32 time embedding / modulation / output projection;
+        # False: the round-3 all-bf16 path (kept for A/B)
+        self.fp32_stream = True
 
     @torch.no_grad()
     def init_weights(self, seed: int = 0):
@@ -296,9 +328,15 @@ class SanaTransformer2DModel(nn.Module):
         row per image, as diffusers' SanaTransformer2DModel."""
         B, C, H, W = hidden_states.shape
         a = self.config
-        x = hidden_states.to(torch.bfloat16).permute(0, 2, 3, 1).reshape(B, H * W, C)
-        x = F.linear(x, self.patch_w, self.patch_b).contiguous()                      # PatchEmbed (p = 1)
-        timestep6, emb_t = self.time_embed(timestep, guidance)
+        f32 = self.fp32_stream
+        if f32:   # PatchEmbed (p = 1) in fp32 (K = 32): the fp32 residual stream starts here
+            x = F.linear(hidden_states.float().permute(0, 2, 3, 1).reshape(B, H * W, C), self.patch_w.float(),
+                         self.patch_b.float()).contiguous()
+            x16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        else:
+            x = hidden_states.to(torch.bfloat16).permute(0, 2, 3, 1).reshape(B, H * W, C)
+            x = F.linear(x, self.patch_w, self.patch_b).contiguous()                      # PatchEmbed (p = 1)
+        timestep6, emb_t = self.time_embed(timestep, guidance, fp32=f32)
         if self.trim_caption_padding and encoder_attention_mask is not None:
             # Caption columns that are padding for EVERY image carry a -10000 bias: their softmax weight
             # underflows to exactly 0, so dropping them (and their caption-projection / k / v rows) is
@@ -313,6 +351,13 @@ class SanaTransformer2DModel(nn.Module):
         enc = self.caption_projection(encoder_hidden_states.to(torch.bfloat16))
         enc = self.caption_norm(enc)
         mask_bias = (1.0 - encoder_attention_mask.to(torch.bfloat16)) * -10000.0   # [U, L], per caption row
+        if f32:
+            for blk in self.transformer_blocks:
+                blk.forward_fp32(x, x16, enc, mask_bias, timestep6, H, W, enc_index)
+            mods = self.scale_shift_table.float()[None] + emb_t[:, None]          # [B, 2, D]: shift, scale
+            n = K.rownorm(x, a.norm_eps, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=H * W)
+            x = self.proj_out.forward_fp32(n)                                      # fp32 output (the SCM math)
+            return x.view(B, H, W, a.out_channels).permute(0, 3, 1, 2)
         for blk in self.transformer_blocks:
             x = blk(x, enc, mask_bias, timestep6, H, W, enc_index)
         mods = (self.scale_shift_table[None] + emb_t[:, None]).contiguous()     # [B, 2, D]: shift, scale

@@ -142,8 +142,11 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
  *   epi 1: Y = bf16(silu(y))                       GLUMBConv 1x1 conv -> SiLU (sana.py, dcae.py)
  *   epi 2: Y = bf16(res + y)                       x = x + attn2(...) (Sana block)
  *   epi 3: Y = bf16(res + gate[row/rpg, :] * y)    x += gate_msa * attn1(...) (eggroll_gated_residual)
- * res [M, ldr] bf16 may alias Y; gate rows gstride apart.  Requires r <= 2 (and rows_per_member >=
- * 256 when r > 0) and K % 64 == 0: always the MFMA-addend 8-phase kernel.  epi 0 = linear_pop.    */
+ *   epi 4: res = res + y                           the same on the fp32 residual stream (res fp32)
+ *   epi 5: res = fma(gate[row/rpg, :], y, res)     (res fp32, gate fp32; eggroll_gated_residual_f32)
+ * res [M, ldr] bf16 may alias Y; gate rows gstride apart.  epi 4 / 5: res is an fp32 stream updated in
+ * place and Y (may be NULL) receives bf16(res).  Requires r <= 2 (and rows_per_member >= 256 when
+ * r > 0) and K % 64 == 0: always an MFMA-addend 8-phase kernel.  epi 0 = linear_pop.               */
 int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
                                 const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
                                 float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
@@ -254,6 +257,17 @@ int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps, int32_t l
 /* x[r, :] += gate[r / rows_per_group, :] * y[r, :]  (bf16, in place; gate rows gstride apart). */
 int eggroll_gated_residual(void* x, const void* y, const void* gate, int64_t gstride, int64_t rows,
                            int64_t C, int64_t rows_per_group, void* stream);
+/* The same row normalisation with an fp32 input x (x_f32 = 1: the fp32 residual stream of the Sana
+ * blocks) and / or fp32 modulation vectors (mod_f32 = 1: the fp32 AdaLN modulation); output bf16.   */
+int eggroll_rownorm_ex(const void* x, int32_t x_f32, int64_t rows, int64_t C, float eps, int32_t layer,
+                       const void* w, const void* b, const void* mscale, const void* mshift, int64_t mstride,
+                       int32_t mod_f32, int64_t rows_per_group, int32_t act, const void* res, void* out,
+                       void* stream);
+/* fp32 residual stream update: x = fma(gate[g], y, x) (gate bf16 or fp32 per gate_f32; NULL: x += y),
+ * x fp32 [rows, C] in place, y bf16; shadow (optional) receives bf16(x).  The unfused form of the
+ * EPI_RES32 / EPI_GATED32 GEMM epilogues (eggroll_lora_linear_pop_epi epi 4 / 5), bit-identical.   */
+int eggroll_gated_residual_f32(float* x, const void* y, const void* gate, int32_t gate_f32, int64_t gstride,
+                               int64_t rows, int64_t C, int64_t rows_per_group, void* shadow, void* stream);
 /* fp32 residual stream + LayerNorm of the CLIP reward towers (one pass per residual point):
  *   h[r, :] += float(y[r, :])  (y bf16, rows ldy apart; y == NULL: no add, h is only read)
  *   out[r, :] = bf16(layer_norm(h[r, :]) * w + b)   fp32 statistics, w / b bf16 [C], out [rows, C]

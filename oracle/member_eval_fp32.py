@@ -120,51 +120,64 @@ def timestep_embedding(t, dim=256, max_period=10000.0):
 
 
 def transformer_fp32(tr, theta_k, hidden_states, timestep, enc_states, enc_mask, guidance,
-                     record: Optional[list] = None):
-    """SanaTransformer2DModel.forward of the build, fp32, member k's LoRA."""
-    L = lambda m: LoraLinear32(m, theta_k)  # noqa: E731
+                     record: Optional[list] = None, rnd=()):
+    """SanaTransformer2DModel.forward of the build, fp32, member k's LoRA.
+    rnd (drift attribution, tools/drift_probe.py): classes of points rounded to bf16 as the build
+    stores them — "x" the residual stream after every update, "lin_in" every GEMM operand built from
+    activations, "lin_out" every linear's output, "norm" row-norm outputs, "attn" attention outputs,
+    "out" the transformer output, "mods" the AdaLN modulation (scale_shift_table + timestep6, a bf16 add
+    in the build), "temb" the time / guidance embedding chain.  Empty: pure fp32."""
+    bf = lambda t, c: t.to(torch.bfloat16).to(f32) if c in rnd else t  # noqa: E731
+
+    class _L(LoraLinear32):
+        def __call__(self, x, record=None):
+            return bf(super().__call__(bf(x, "lin_in"), record), "lin_out")
+    L = lambda m: (_L if rnd else LoraLinear32)(m, theta_k)  # noqa: E731
     a = tr.config
     B, C, H, W = hidden_states.shape
     x = hidden_states.to(f32).permute(0, 2, 3, 1).reshape(B, H * W, C)
-    x = F.linear(x, _w(tr.patch_w), _w(tr.patch_b))
+    x = bf(F.linear(x, _w(tr.patch_w), _w(tr.patch_b)), "x")
     te = tr.time_embed
-    t = L(te.timestep_embedder.linear_2)(F.silu(L(te.timestep_embedder.linear_1)(timestep_embedding(timestep), record)),
-                                          record)
-    g = L(te.guidance_embedder.linear_2)(F.silu(L(te.guidance_embedder.linear_1)(timestep_embedding(guidance), record)),
-                                          record)
-    cond = t + g
-    timestep6 = L(te.linear)(F.silu(cond), record)
+    te_ = lambda t: bf(t, "temb")  # noqa: E731
+    t = te_(L(te.timestep_embedder.linear_2)(te_(F.silu(L(te.timestep_embedder.linear_1)(
+        te_(timestep_embedding(timestep)), record))), record))
+    g = te_(L(te.guidance_embedder.linear_2)(te_(F.silu(L(te.guidance_embedder.linear_1)(
+        te_(timestep_embedding(guidance)), record))), record))
+    cond = te_(t + g)
+    timestep6 = L(te.linear)(te_(F.silu(cond)), record)
     cp = tr.caption_projection
     enc = L(cp.linear_2)(F.gelu(L(cp.linear_1)(enc_states.to(f32), record), approximate="tanh"), record)
-    enc = rownorm(enc, tr.caption_norm.eps, w=_w(tr.caption_norm.weight))
+    enc = bf(rownorm(enc, tr.caption_norm.eps, w=_w(tr.caption_norm.weight)), "norm")
     mask_bias = ((1.0 - enc_mask.to(f32)) * -10000.0).view(B, 1, 1, -1)
     N = H * W
     for blk in tr.transformer_blocks:
-        mods = _w(blk.scale_shift_table)[None] + timestep6.view(B, 6, -1)
-        n = rownorm(x, blk.eps, layer=True, mscale=mods[:, 1:2], mshift=mods[:, 0:1])
+        mods = bf(_w(blk.scale_shift_table)[None] + timestep6.view(B, 6, -1), "mods")
+        n = bf(rownorm(x, blk.eps, layer=True, mscale=mods[:, 1:2], mshift=mods[:, 0:1]), "norm")
         at = blk.attn1
-        q = rownorm(L(at.to_q)(n, record), at.norm_q.eps, w=_w(at.norm_q.weight), act="relu")
-        k = rownorm(L(at.to_k)(n, record), at.norm_k.eps, w=_w(at.norm_k.weight), act="relu")
+        q = bf(rownorm(L(at.to_q)(n, record), at.norm_q.eps, w=_w(at.norm_q.weight), act="relu"), "norm")
+        k = bf(rownorm(L(at.to_k)(n, record), at.norm_k.eps, w=_w(at.norm_k.weight), act="relu"), "norm")
         v = L(at.to_v)(n, record)
         sh = (B, N, at.heads, at.head_dim)
-        o = linear_attention(q.view(sh), k.view(sh), v.view(sh), relu_qk=False)
-        x = x + mods[:, 2:3] * L(at.to_out[0])(o, record)
+        o = bf(linear_attention(q.view(sh), k.view(sh), v.view(sh), relu_qk=False), "attn")
+        x = bf(x + mods[:, 2:3] * L(at.to_out[0])(o, record), "x")
         ca = blk.attn2
         Lc = enc.shape[1]
-        q = rownorm(L(ca.to_q)(x, record), ca.norm_q.eps, w=_w(ca.norm_q.weight)).view(B, N, ca.heads, ca.head_dim)
-        k = rownorm(L(ca.to_k)(enc, record), ca.norm_k.eps, w=_w(ca.norm_k.weight)).view(B, Lc, ca.heads, ca.head_dim)
+        q = bf(rownorm(L(ca.to_q)(x, record), ca.norm_q.eps, w=_w(ca.norm_q.weight)), "norm").view(B, N, ca.heads,
+                                                                                                    ca.head_dim)
+        k = bf(rownorm(L(ca.to_k)(enc, record), ca.norm_k.eps, w=_w(ca.norm_k.weight)), "norm").view(B, Lc, ca.heads,
+                                                                                                      ca.head_dim)
         v = L(ca.to_v)(enc, record).view(B, Lc, ca.heads, ca.head_dim)
         s = torch.einsum("bnhd,blhd->bhnl", q, k) * ca.head_dim ** -0.5 + mask_bias
-        o = torch.einsum("bhnl,blhd->bnhd", torch.softmax(s, -1), v).reshape(B, N, -1)
-        x = x + L(ca.to_out[0])(o, record)
-        n = rownorm(x, blk.eps, layer=True, mscale=mods[:, 4:5], mshift=mods[:, 3:4])
+        o = bf(torch.einsum("bhnl,blhd->bnhd", torch.softmax(s, -1), v).reshape(B, N, -1), "attn")
+        x = bf(x + L(ca.to_out[0])(o, record), "x")
+        n = bf(rownorm(x, blk.eps, layer=True, mscale=mods[:, 4:5], mshift=mods[:, 3:4]), "norm")
         ff = blk.ff
-        h = F.linear(n, _w(ff.w_inv), _w(ff.b_inv)).view(B, H, W, -1)
-        gl = dwconv_nhwc(h, _w(ff.w_dw), _w(ff.b_dw), 3, pre_silu=True, glu=True)
-        x = x + mods[:, 5:6] * F.linear(gl.reshape(B, N, -1), _w(ff.w_point))
-    mods = _w(tr.scale_shift_table)[None] + cond[:, None]
-    x = rownorm(x, a.norm_eps, layer=True, mscale=mods[:, 1:2], mshift=mods[:, 0:1])
-    x = L(tr.proj_out)(x, record)
+        h = bf(F.linear(n, _w(ff.w_inv), _w(ff.b_inv)), "lin_out").view(B, H, W, -1)
+        gl = bf(dwconv_nhwc(h, _w(ff.w_dw), _w(ff.b_dw), 3, pre_silu=True, glu=True), "attn")
+        x = bf(x + mods[:, 5:6] * bf(F.linear(gl.reshape(B, N, -1), _w(ff.w_point)), "lin_out"), "x")
+    mods = bf(_w(tr.scale_shift_table)[None] + cond[:, None], "mods")
+    x = bf(rownorm(x, a.norm_eps, layer=True, mscale=mods[:, 1:2], mshift=mods[:, 0:1]), "norm")
+    x = bf(L(tr.proj_out)(x, record), "out")
     return x.view(B, H, W, a.out_channels).permute(0, 3, 1, 2)
 
 
@@ -181,45 +194,57 @@ def _upshortcut(x, cout):
     return y.permute(0, 2, 3, 1)
 
 
-def dcae_fp32(vae, z):
+def dcae_fp32(vae, z, rnd=()):
+    """rnd (drift attribution): "dx" rounds the residual stream after every block ("dx_vit" / "dx_res" /
+    "dx_up": only after the EfficientViT blocks + conv_in / the ResBlocks / the up-blocks), "dact" every
+    other activation the build stores in bf16 (conv / GEMM outputs, attention outputs, the input)."""
     from hyperscalees_t2i_amd.dcae import EfficientViTBlock, ResBlock, UpBlock
-    zt = z.to(f32).permute(0, 2, 3, 1)
-    x = conv3x3(zt, _w(vae.conv_in.weight), _w(vae.conv_in.bias)) + zt.repeat_interleave(vae.in_repeats, dim=-1)
+    _bf = lambda t, c: t.to(torch.bfloat16).to(f32) if c in rnd else t  # noqa: E731
+    kind = {"vit": "dx_vit", "res": "dx_res", "up": "dx_up"}
+
+    def bf(t, c, k=None):
+        if c == "dx" and k is not None and kind[k] in rnd:
+            return t.to(torch.bfloat16).to(f32)
+        return _bf(t, c)
+    zt = bf(z.to(f32).permute(0, 2, 3, 1), "dact")
+    x = bf(conv3x3(zt, _w(vae.conv_in.weight), _w(vae.conv_in.bias)) + zt.repeat_interleave(vae.in_repeats, dim=-1), "dx",
+           "vit")
     for st in vae.stages:
         for blk in st:
             if isinstance(blk, UpBlock):
                 cout = blk.conv.weight.shape[0]
                 up = F.interpolate(x.permute(0, 3, 1, 2), scale_factor=2, mode="nearest").permute(0, 2, 3, 1)
-                x = conv3x3(up, _w(blk.conv.weight), _w(blk.conv.bias)) + _upshortcut(x, cout)
+                x = bf(conv3x3(up, _w(blk.conv.weight), _w(blk.conv.bias)) + _upshortcut(x, cout), "dx", "up")
             elif isinstance(blk, ResBlock):
-                h = F.silu(conv3x3(x, _w(blk.conv1.weight), _w(blk.conv1.bias)))
+                h = bf(F.silu(conv3x3(x, _w(blk.conv1.weight), _w(blk.conv1.bias))), "dact")
                 h = conv3x3(h, _w(blk.conv2.weight), None)
-                x = rownorm(h, blk.norm.eps, w=_w(blk.norm.weight), b=_w(blk.norm.bias), res=x)
+                x = bf(rownorm(h, blk.norm.eps, w=_w(blk.norm.weight), b=_w(blk.norm.bias), res=x), "dx", "res")
             elif isinstance(blk, EfficientViTBlock):
-                x = _msla(blk.attn, x)
+                x = bf(_msla(blk.attn, x, bf), "dx", "vit")
                 c = blk.conv_out
-                h = F.linear(x, _w(c.w_inv), _w(c.b_inv))
-                g = dwconv_nhwc(h, _w(c.w_dw), _w(c.b_dw), 3, pre_silu=True, glu=True)
-                x = rownorm(F.linear(g, _w(c.w_point)), c.norm.eps, w=_w(c.norm.weight), b=_w(c.norm.bias), res=x)
+                h = bf(F.linear(x, _w(c.w_inv), _w(c.b_inv)), "dact")
+                g = bf(dwconv_nhwc(h, _w(c.w_dw), _w(c.b_dw), 3, pre_silu=True, glu=True), "dact")
+                x = bf(rownorm(bf(F.linear(g, _w(c.w_point)), "dact"), c.norm.eps, w=_w(c.norm.weight),
+                               b=_w(c.norm.bias), res=x), "dx", "vit")
             else:
                 raise TypeError(type(blk))
-    x = rownorm(x, vae.norm_out.eps, w=_w(vae.norm_out.weight), b=_w(vae.norm_out.bias), act="relu")
+    x = bf(rownorm(x, vae.norm_out.eps, w=_w(vae.norm_out.weight), b=_w(vae.norm_out.bias), act="relu"), "dact")
     return conv3x3(x, _w(vae.conv_out.weight), _w(vae.conv_out.bias)).permute(0, 3, 1, 2)
 
 
-def _msla(at, x):
+def _msla(at, x, bf=lambda t, c: t):
     B, H, W, C = x.shape
     hd, heads = at.hd, at.heads
-    qkv = F.linear(x, _w(at.w_qkv))                                        # [B,H,W,3*inner], head h: [q|k|v]
+    qkv = bf(F.linear(x, _w(at.w_qkv)), "dact")                           # [B,H,W,3*inner], head h: [q|k|v]
     outs = []
     t = qkv.reshape(B, H * W, heads, 3, hd)
-    outs.append(linear_attention(t[:, :, :, 0], t[:, :, :, 1], t[:, :, :, 2], relu_qk=True))
+    outs.append(bf(linear_attention(t[:, :, :, 0], t[:, :, :, 1], t[:, :, :, 2], relu_qk=True), "dact"))
     for ks, wdw, wpw in zip(at.scales, at.ms_dw, at.ms_pw):
         d = dwconv_nhwc(qkv, _w(wdw), None, ks, pre_silu=False, glu=False)
         g = d.reshape(B * H * W, 3 * heads, hd)
-        pg = torch.einsum("ngi,goi->ngo", g, _w(wpw)).reshape(B, H * W, heads, 3, hd)
-        outs.append(linear_attention(pg[:, :, :, 0], pg[:, :, :, 1], pg[:, :, :, 2], relu_qk=True))
-    y = F.linear(torch.cat(outs, -1).view(B, H, W, -1), _w(at.w_out))
+        pg = bf(torch.einsum("ngi,goi->ngo", g, _w(wpw)), "dact").reshape(B, H * W, heads, 3, hd)
+        outs.append(bf(linear_attention(pg[:, :, :, 0], pg[:, :, :, 1], pg[:, :, :, 2], relu_qk=True), "dact"))
+    y = bf(F.linear(torch.cat(outs, -1).view(B, H, W, -1), _w(at.w_out)), "dact")
     n = at.norm_out
     return rownorm(y, n.eps, w=_w(n.weight), b=_w(n.bias), res=x)
 
@@ -230,8 +255,9 @@ def _msla(at, x):
 
 
 def generate_fp32(es_model, theta_k, prompt_embeds, prompt_mask, latents, guidance_scale: float,
-                  record: Optional[list] = None):
-    """models/SanaSprint.py:96-160 with the build's weights in fp32: (eps_pred, image)."""
+                  record: Optional[list] = None, rnd=(), drnd=()):
+    """models/SanaSprint.py:96-160 with the build's weights in fp32: (eps_pred, image); rnd: see
+    transformer_fp32."""
     b = latents.shape[0]
     sd = es_model.sigma_data
     lmi = latents / sd
@@ -241,11 +267,11 @@ def generate_fp32(es_model, theta_k, prompt_embeds, prompt_mask, latents, guidan
     guidance = torch.full((b,), guidance_scale, device=latents.device, dtype=es_model.DTYPE)
     guidance = guidance * es_model.transformer_config.guidance_embeds_scale
     eps = transformer_fp32(es_model.transformer, theta_k, lmi.to(f32), scm, prompt_embeds.to(f32), prompt_mask,
-                           guidance.to(f32), record)
-    return eps, decode_fp32(es_model, eps, latents)
+                           guidance.to(f32), record, rnd)
+    return eps, decode_fp32(es_model, eps, latents, drnd)
 
 
-def decode_fp32(es_model, eps, latents):
+def decode_fp32(es_model, eps, latents, drnd=()):
     """models/SanaSprint.py:133-160 after the transformer: nan_to_num, SCM combine (the reference's fp16
     casts), x0, fp32 DC-AE decode.  Also used on the build's bf16 transformer output to split the image
     drift into its transformer and DC-AE parts."""
@@ -258,7 +284,7 @@ def decode_fp32(es_model, eps, latents):
     pred = ((1 - 2 * se) * lmi + (1 - 2 * se + 2 * se ** 2) * eps.to(lmi.dtype)) / torch.sqrt(se ** 2 + (1 - se) ** 2)
     pred = pred.float() * sd
     x0 = (0.267 * latents - 0.964 * pred) / sd
-    return dcae_fp32(es_model.vae, x0.to(f32) / es_model.vae.scaling_factor)
+    return dcae_fp32(es_model.vae, x0.to(f32) / es_model.vae.scaling_factor, drnd)
 
 
 class Rewards32:

@@ -901,6 +901,71 @@ def test_gemm_320_tile_bitexact_vs_256(dev, M, N, Kd, r, rpm):
         assert torch.equal(o8, o10), epi
 
 
+@pytest.mark.parametrize("rows,C,rpg", [(3000, 2240, 1000), (777, 128, 100), (64, 96, 64)])
+def test_rownorm_fp32_stream_vs_torch(dev, rows, C, rpg):
+    """eggroll_rownorm_ex: fp32 residual-stream input and fp32 AdaLN modulation vs the
+    torch fp32 formula, output rounded once to bf16; the bf16-input / bf16-modulation form is the
+    unchanged eggroll_rownorm (bit-identical to it)."""
+    g = torch.Generator(device=dev).manual_seed(rows + C)
+    x = torch.randn((rows, C), generator=g, device=dev) * 3 + 0.5
+    G = -(-rows // rpg)
+    mods = torch.randn((G, 6, C), generator=g, device=dev) * 0.3
+    y = K.rownorm(x, 1e-6, layer=True, mscale=mods[:, 1], mshift=mods[:, 0], rows_per_group=rpg)
+    gi = torch.arange(rows, device=dev) // rpg
+    ref = torch.nn.functional.layer_norm(x, (C,), eps=1e-6) * (1 + mods[gi, 1]) + mods[gi, 0]
+    assert y.dtype == torch.bfloat16
+    assert (y.float() - ref).abs().max() <= 2 ** -8 * ref.abs().max() + 1e-5
+    # bf16 x + bf16 modulation through the new entry point == the old kernel path, bit for bit
+    xb, mb = x.to(torch.bfloat16), mods.to(torch.bfloat16)
+    a = K.rownorm(xb, 1e-6, layer=True, mscale=mb[:, 1], mshift=mb[:, 0], rows_per_group=rpg)
+    out = torch.empty_like(xb)
+    from hyperscalees_t2i_amd import _lib
+    _lib.call("eggroll_rownorm", xb.data_ptr(), rows, C, 1e-6, 1, None, None, mb[:, 1].data_ptr(), mb[:, 0].data_ptr(),
+              6 * C, rpg, 0, None, out.data_ptr(), K._stream(dev))
+    assert torch.equal(a, out)
+
+
+def test_gated_residual_f32(dev):
+    """x = fma(gate, y, x) on the fp32 stream (gate fp32 / bf16 / none), bf16 shadow = bf16(x)."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    rows, C, rpg = 4096, 2240, 1024
+    x = torch.randn((rows, C), generator=g, device=dev)
+    y = torch.randn((rows, C), generator=g, device=dev).to(torch.bfloat16)
+    gate = torch.randn((rows // rpg, 6 * C), generator=g, device=dev)[:, 2 * C:3 * C]
+    gi = torch.arange(rows, device=dev) // rpg
+    for gt in (gate, gate.to(torch.bfloat16), None):
+        x1, sh = x.clone(), torch.empty((rows, C), dtype=torch.bfloat16, device=dev)
+        K.gated_residual_f32_(x1, y, gt, rpg, shadow=sh)
+        gg = 1.0 if gt is None else gt.double()[gi]
+        ref = (x.double() + gg * y.double())
+        assert (x1.double() - ref).abs().max() <= 2 ** -23 * ref.abs().max(), gt is None
+        assert torch.equal(sh, x1.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("epi,r,M,N,Kd,rpm", [("gated32", 2, 4 * 4096, 2240, 2240, 4096), ("res32", 2, 4 * 4096, 2240, 2240, 4096),
+                                             ("gated32", 1, 3 * 1000 + 200, 384, 256, 1000), ("res32", 0, 777, 200, 128, 777)])
+def test_lora_epilogue_fp32_stream_bitexact(dev, epi, r, M, N, Kd, rpm):
+    """EPI_RES32 / EPI_GATED32 (the fp32 residual stream fused into kernel 8's store phase) == the same
+    GEMM followed by eggroll_gated_residual_f32, bit for bit, stream and bf16 shadow; ragged shapes."""
+    g = torch.Generator(device=dev).manual_seed(M + N + 1)
+    x = torch.randn((M, Kd), generator=g, device=dev).to(torch.bfloat16)
+    W = (torch.randn((N, Kd), generator=g, device=dev) / Kd ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=dev).to(torch.bfloat16)
+    tp = torch.randn((-(-M // rpm), Kd * r + N * r + 8), generator=g, device=dev) * 0.05 if r else None
+    offA, offB = 0, Kd * r
+    y = K.lora_gemm(x, W, bias, K.lora_project(x, tp, offA, r, rpm) if r else None, tp, offB, r, 2.0, rpm, kernel=8) \
+        if r else K.lora_linear_pop(x, W, bias, None, 0, 0, 0, 0.0, M, kernel=8)
+    res = torch.randn((M, N), generator=g, device=dev)
+    rpg = 512
+    gate = torch.randn((-(-M // rpg), 3 * N), generator=g, device=dev)[:, N:2 * N]
+    ref, ref_sh = res.clone(), torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    K.gated_residual_f32_(ref, y, gate if epi == "gated32" else None, rpg, shadow=ref_sh)
+    got, sh = res.clone(), torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, epi, res=got, gate=gate if epi == "gated32" else None,
+                          rows_per_group=rpg, out=sh)
+    assert torch.equal(got, ref) and torch.equal(sh, ref_sh)
+
+
 @pytest.mark.parametrize("B,N,H,L,U", [(4, 64, 2, 37, 2), (3, 100, 3, 300, 3), (6, 17, 1, 320, 2), (16, 1024, 20, 300, 4)])
 def test_cross_attention_vs_sdpa(dev, B, N, H, L, U):
     """eggroll_cross_attention (MFMA, caption rows through enc_index, additive mask) vs fp32 SDPA on the

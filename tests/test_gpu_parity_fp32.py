@@ -49,7 +49,8 @@ BOUNDS = {
 KEYS = ("lora_rel", "eps_rel", "image_rel", "reward_abs", "S_abs")
 # test_rank_fidelity_over_seeds (sigma 1e-2, 12 epochs' seeds x 8 members, 336 member pairs): bounds at
 # ~1.5x the measured S drift; pooled Kendall tau >= 0.95 (VERDICT r2 bar)
-RANK_BOUNDS = {"S_abs": 0.028, "pooled_tau": 0.95}   # measured (round 3, 12 seeds): S_abs 0.0194, pooled tau 0.952
+RANK_BOUNDS = {"S_abs": 0.028, "pooled_tau": 0.95,   # measured (round 3, 12 seeds): S_abs 0.0194, pooled tau 0.952
+               "best_worst_misses": 1}
 
 
 def kendall_tau(a, b):
@@ -169,7 +170,10 @@ def test_member_eval_bf16_vs_fp32_with_reference_noise(stack, dev, golden, case,
     sc32, _, _ = O.ref_promptnorm(S32.cpu().numpy())
     spread = float(S32.std(0).mean())
     order, order32 = np.argsort(sc, kind="stable"), np.argsort(sc32, kind="stable")
+    gaps = np.diff(np.sort(sc32))
     report = {"case": case, "sigma": sigma, **{k: round(v, 6) for k, v in worst.items()},
+              "scores32": np.round(sc32, 5).tolist(), "scores": np.round(sc, 5).tolist(),
+              "min_score_gap32": round(float(gaps.min()), 5),
               "S_member_spread": round(spread, 6), "rank_exact": bool(np.array_equal(order, order32)),
               "kendall_tau": round(float(kendall_tau(sc, sc32)), 4),
               "best_same": bool(order[-1] == order32[-1]), "worst_same": bool(order[0] == order32[0])}
@@ -194,7 +198,10 @@ def test_rank_fidelity_over_seeds(stack, dev, golden):
     """Fitness-order agreement with the fp32 restatement at the BASELINE sigma (1e-2), product path
     (fused epilogues, shared projections), over several epochs' seeds (latents + prompt draw differ):
     one 8-member tau is a coarse statistic (one swapped pair = 0.93), so the bar is on the pooled
-    discordant-pair fraction and on best / worst member agreement.  Reference noise injected (g10)."""
+    discordant-pair fraction and on best / worst member agreement.  Reference noise injected (g10).
+    The per-stage breakdown is pooled over the same 12 seeds: S recomputed with only one stage at the
+    build's precision (transformer -> fp32 DC-AE -> fp32 towers; transformer + DC-AE image -> fp32
+    towers; fp32 image -> build towers), so the discordant pairs are attributed to a stage."""
     be, rewards, rewards32 = stack
     g = golden("g10_member_eval_injection.npz")
     params, shapes = be.collect_lora_params()
@@ -204,37 +211,65 @@ def test_rank_fidelity_over_seeds(stack, dev, golden):
     fac = torch.from_numpy(noiser.layout.pack_factors(g["s0/factors"])).to(dev)
     eps_ref = torch.from_numpy(g["s0/eps"]).to(dev)
     tp = noiser.perturb(theta, fac, pop, 0, pop)
-    taus, disc, pairs, best, worst, s_abs, spread = [], 0, 0, 0, 0, 0.0, []
+    stages = ("all", "transformer", "transformer+dcae", "towers")
+    st = {k: {"disc": 0, "best": 0, "worst": 0, "S_abs": 0.0} for k in stages}
+    taus, pairs, spread = [], 0, []
     seeds = tuple(range(5, 17))   # 12 epochs' seeds, 336 member pairs (one pair = 0.006 of pooled tau)
     for seed in seeds:
         info = be.step_sampling_info(seed)
         flat, m = info["flat_ids"], info["m"]
         B = len(flat)
         pe, am = be._gather(flat)
-        imgs = be.generate_population(flat, seed, 4.5, tp)
+        tr_out = []
+        hook = be.es_model.transformer.register_forward_hook(lambda _m, _i, o: tr_out.append(o))
+        try:
+            imgs = be.generate_population(flat, seed, 4.5, tp)
+        finally:
+            hook.remove()
         j_of = torch.tensor([info["pid_to_j"][p] for p in flat], device=dev)
-        rew = rewards.score(imgs, j_of.repeat(pop), rewards.prompt_features(info["unique_texts"]))
-        S, _ = aggregate_member_rewards(rew, flat, info["pid_to_j"], pop, m)
+        feats = rewards.prompt_features(info["unique_texts"])
+        rew = rewards.score(imgs, j_of.repeat(pop), feats)
+        Sx = {"all": aggregate_member_rewards(rew, flat, info["pid_to_j"], pop, m)[0]}
         lat = be.es_model._latents(B, seed, 4, 4)
         feats32 = rewards32.prompt_features(info["unique_texts"])
-        S32 = torch.stack([aggregate_member_rewards(
-            rewards32.score(R.generate_fp32(be.es_model, theta + sigma * eps_ref[k], pe, am, lat, 4.5)[1], j_of,
-                            feats32), flat, info["pid_to_j"], 1, m)[0][0] for k in range(pop)])
-        sc = K.fitness(S, True)["scores"].cpu().numpy()
+        agg = lambda rw: aggregate_member_rewards(rw, flat, info["pid_to_j"], 1, m)[0][0]  # noqa: E731
+        rows = {k: [] for k in ("S32", "transformer", "transformer+dcae", "towers")}
+        for k in range(pop):
+            img32 = R.generate_fp32(be.es_model, theta + sigma * eps_ref[k], pe, am, lat, 4.5)[1]
+            rows["S32"].append(agg(rewards32.score(img32, j_of, feats32)))
+            rows["transformer"].append(agg(rewards32.score(R.decode_fp32(be.es_model, tr_out[0][k * B:(k + 1) * B], lat),
+                                                           j_of, feats32)))
+            rows["transformer+dcae"].append(agg(rewards32.score(imgs[k * B:(k + 1) * B].float(), j_of, feats32)))
+            rows["towers"].append(agg(rewards.score(img32.to(torch.bfloat16), j_of, feats)))
+        S32 = torch.stack(rows["S32"])
+        for k in ("transformer", "transformer+dcae", "towers"):
+            Sx[k] = torch.stack(rows[k])
         sc32, _, _ = O.ref_promptnorm(S32.cpu().numpy())
-        t = kendall_tau(sc, sc32)
-        taus.append(round(float(t), 4))
-        disc += round((1 - t) / 2 * (pop * (pop - 1) // 2))
+        o32 = np.argsort(sc32, kind="stable")
+        for name in stages:
+            sc = (K.fitness(Sx[name], True)["scores"].cpu().numpy() if name == "all"
+                  else O.ref_promptnorm(Sx[name].cpu().numpy())[0])
+            t = kendall_tau(sc, sc32)
+            if name == "all":
+                taus.append(round(float(t), 4))
+            o = np.argsort(sc, kind="stable")
+            d = st[name]
+            d["disc"] += round((1 - t) / 2 * (pop * (pop - 1) // 2))
+            d["best"] += int(o[-1] == o32[-1])
+            d["worst"] += int(o[0] == o32[0])
+            d["S_abs"] = max(d["S_abs"], float((Sx[name] - S32).abs().max()))
         pairs += pop * (pop - 1) // 2
-        o, o32 = np.argsort(sc, kind="stable"), np.argsort(sc32, kind="stable")
-        best += int(o[-1] == o32[-1])
-        worst += int(o[0] == o32[0])
-        s_abs = max(s_abs, float((S - S32).abs().max()))
         spread.append(float(S32.std(0).mean()))
-    report = {"sigma": sigma, "seeds": list(seeds), "kendall_tau": taus, "pooled_tau": round(1 - 2 * disc / pairs, 4),
-              "discordant_pairs": disc, "pairs": pairs, "best_same": best, "worst_same": worst,
-              "S_abs_max": round(s_abs, 6), "S_member_spread_mean": round(float(np.mean(spread)), 6)}
+    for d in st.values():
+        d["pooled_tau"] = round(1 - 2 * d["disc"] / pairs, 4)
+        d["S_abs"] = round(d["S_abs"], 6)
+    a = st["all"]
+    report = {"sigma": sigma, "seeds": list(seeds), "kendall_tau": taus, "pooled_tau": a["pooled_tau"],
+              "discordant_pairs": a["disc"], "pairs": pairs, "best_same": a["best"], "worst_same": a["worst"],
+              "S_abs_max": a["S_abs"], "S_member_spread_mean": round(float(np.mean(spread)), 6),
+              "stages": {k: st[k] for k in stages if k != "all"}}
     print("[fp32-parity] rank fidelity over seeds", json.dumps(report))
-    assert s_abs <= RANK_BOUNDS["S_abs"], report
+    assert a["S_abs"] <= RANK_BOUNDS["S_abs"], report
     assert report["pooled_tau"] >= RANK_BOUNDS["pooled_tau"], report
-    assert best >= len(seeds) - 1 and worst >= len(seeds) - 1, report
+    assert a["best"] >= len(seeds) - RANK_BOUNDS["best_worst_misses"], report
+    assert a["worst"] >= len(seeds) - RANK_BOUNDS["best_worst_misses"], report
