@@ -45,7 +45,9 @@ SIGNATURES = {
     "eggroll_dwconv_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i32, i32, i32, vp, vp]),
     "eggroll_rownorm": (C.c_int, [vp, i64, i64, f32, i32, vp, vp, vp, vp, i64, i64, i32, vp, vp, vp]),
     "eggroll_gated_residual": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, vp]),
-    "eggroll_rownorm_ex": (C.c_int, [vp, i32, i64, i64, f32, i32, vp, vp, vp, vp, i64, i32, i64, i32, vp, vp, vp]),
+    "eggroll_rownorm_ex": (C.c_int, [vp, i32, i64, i64, f32, i32, vp, vp, vp, vp, i64, i32, i64, i32, vp, i32, vp, i32,
+                                     vp, vp]),
+    "eggroll_subpixel_shortcut_f32": (C.c_int, [vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, vp]),
     "eggroll_gated_residual_f32": (C.c_int, [vp, vp, vp, i32, i64, i64, i64, i64, vp, vp]),
     "eggroll_resid_layernorm": (C.c_int, [vp, i64, vp, i64, i64, i64, f32, vp, vp, vp, vp]),
     "eggroll_dwconv_pw_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i32, vp, vp]),

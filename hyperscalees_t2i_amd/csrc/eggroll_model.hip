@@ -259,16 +259,18 @@ __device__ __forceinline__ void load8f(const void* p, int f32, int64_t off, floa
 }
 
 // XF: x is fp32 (the fp32 residual stream of the Sana blocks); mf32: the modulation
-// vectors mscale / mshift are fp32 (the fp32 AdaLN modulation).  Output bf16 (a GEMM operand).
-template <int SEG, int NCH, bool XF>
+// vectors mscale / mshift are fp32 (the fp32 AdaLN modulation); rf32: res is fp32.  OF: the output
+// is fp32 (the DC-AE fp32 residual stream: out = res + norm(x) in place of res) and `shadow` (optional)
+// receives its bf16 copy; else the output is bf16 (a GEMM operand).
+template <int SEG, int NCH, bool XF, bool OF>
 __global__ __launch_bounds__(256) void k_rownorm(const void* __restrict__ x, int64_t rows, int C, float eps,
                                                  int layer, const unsigned short* __restrict__ w,
                                                  const unsigned short* __restrict__ b,
                                                  const void* __restrict__ mscale,
                                                  const void* __restrict__ mshift, int64_t mstride, int mf32,
                                                  int64_t rows_per_group, int act,
-                                                 const unsigned short* __restrict__ res,
-                                                 unsigned short* __restrict__ out) {
+                                                 const void* __restrict__ res, int rf32,
+                                                 void* __restrict__ out, unsigned short* __restrict__ shadow) {
     const int lane = threadIdx.x & 63;
     const int seg_lane = lane % SEG;
     const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / SEG;
@@ -341,14 +343,21 @@ __global__ __launch_bounds__(256) void k_rownorm(const void* __restrict__ x, int
             for (int i = 0; i < 8; ++i) y[i] = silu(y[i]);
         }
         if (res) {
-            load8f(res, 0, row * C + c0, q);
+            load8f(res, rf32, row * C + c0, q);
 #pragma unroll
             for (int i = 0; i < 8; ++i) y[i] += q[i];
         }
-        u16x8m o;
+        if constexpr (OF) {
+            float* o32 = reinterpret_cast<float*>(out) + row * C + c0;
+            *reinterpret_cast<float4*>(o32) = float4{y[0], y[1], y[2], y[3]};
+            *reinterpret_cast<float4*>(o32 + 4) = float4{y[4], y[5], y[6], y[7]};
+        }
+        if (!OF || shadow) {
+            u16x8m o;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = f2b(y[i]);
-        *reinterpret_cast<u16x8m*>(out + row * C + c0) = o;
+            for (int i = 0; i < 8; ++i) o[i] = f2b(y[i]);
+            *reinterpret_cast<u16x8m*>((OF ? shadow : reinterpret_cast<unsigned short*>(out)) + row * C + c0) = o;
+        }
     }
 }
 
@@ -551,12 +560,15 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut(const unsigned short*
 // 32/REP-channel window of x[b, h, w] starting at 4 c0 / REP, loaded as 16-byte vectors and indexed
 // with compile-time positions (the per-output kernel above gathers them as 8 scalar 2-byte loads
 // per output chunk).  REP = 4 Cout / Cin in {1, 2, 4}.
-template <int REP>
+// F32: the DC-AE fp32 residual stream — x (the shortcut source) and out are fp32, and `shadow`
+// (optional) receives bf16(out); the same arithmetic on the fp32 shortcut values.
+template <int REP, bool F32 = false>
 __global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short* __restrict__ y4,
-                                                            const unsigned short* __restrict__ x,
+                                                            const void* __restrict__ x,
                                                             const unsigned short* __restrict__ bias,
-                                                            unsigned short* __restrict__ out, int H, int W, int Cin,
-                                                            int Cout, int lowpix_total) {
+                                                            void* __restrict__ out, int H, int W, int Cin,
+                                                            int Cout, int lowpix_total,
+                                                            unsigned short* __restrict__ shadow = nullptr) {
     constexpr int XW = 32 / REP;  // source window (channels)
     const int groups = Cout >> 3;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -567,11 +579,11 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short
     const int bb = lp / HW;
     const int r = lp - bb * HW;
     const int h = r / W, w = r - h * W;
-    const unsigned short* src = x + (int64_t)lp * Cin + 4 * c0 / REP;
-    unsigned short xs[XW];
+    float xs[XW];
 #pragma unroll
     for (int v = 0; v < XW / 8; ++v) {
-        const u16x8m q = *reinterpret_cast<const u16x8m*>(src + 8 * v);
+        float q[8];
+        load8f(x, F32, (int64_t)lp * Cin + 4 * c0 / REP + 8 * v, q);
 #pragma unroll
         for (int e = 0; e < 8; ++e) xs[8 * v + e] = q[e];
     }
@@ -594,10 +606,21 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = k >> 1, j = k & 1;
-        u16x8m o;
+        const int64_t opix = ((int64_t)(bb * 2 * H + 2 * h + i) * (2 * W) + 2 * w + j) * Cout + c0;
+        float f[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = f2b(b2f(yv[k][q]) + bv[q] + b2f(xs[(4 * q + k) / REP]));
-        *reinterpret_cast<u16x8m*>(out + ((int64_t)(bb * 2 * H + 2 * h + i) * (2 * W) + 2 * w + j) * Cout + c0) = o;
+        for (int q = 0; q < 8; ++q) f[q] = b2f(yv[k][q]) + bv[q] + xs[(4 * q + k) / REP];
+        if constexpr (F32) {
+            float* o32 = reinterpret_cast<float*>(out) + opix;
+            *reinterpret_cast<float4*>(o32) = float4{f[0], f[1], f[2], f[3]};
+            *reinterpret_cast<float4*>(o32 + 4) = float4{f[4], f[5], f[6], f[7]};
+        }
+        if (!F32 || shadow) {
+            u16x8m o;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[q] = f2b(f[q]);
+            *reinterpret_cast<u16x8m*>((F32 ? shadow : reinterpret_cast<unsigned short*>(out)) + opix) = o;
+        }
     }
 }
 
@@ -1245,36 +1268,40 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
 template <int SEG, int NCH>
 static void launch_rownorm(const void* x, int xf32, int64_t rows, int C, float eps, int layer, const void* w,
                            const void* b, const void* ms, const void* mh, int64_t mstride, int mf32, int64_t rpg,
-                           int act, const void* res, void* out, hipStream_t st) {
+                           int act, const void* res, int rf32, void* out, int of32, void* shadow, hipStream_t st) {
     const int64_t threads = rows * SEG;
     const dim3 grid((unsigned)((threads + 255) / 256));
-    if (xf32)
-        hipLaunchKernelGGL((k_rownorm<SEG, NCH, true>), grid, dim3(256), 0, st, x, rows, C, eps, layer,
-                           (const unsigned short*)w, (const unsigned short*)b, ms, mh, mstride, mf32, rpg, act,
-                           (const unsigned short*)res, (unsigned short*)out);
-    else
-        hipLaunchKernelGGL((k_rownorm<SEG, NCH, false>), grid, dim3(256), 0, st, x, rows, C, eps, layer,
-                           (const unsigned short*)w, (const unsigned short*)b, ms, mh, mstride, mf32, rpg, act,
-                           (const unsigned short*)res, (unsigned short*)out);
+#define EGG_RNK(XF_, OF_)                                                                                          \
+    hipLaunchKernelGGL((k_rownorm<SEG, NCH, XF_, OF_>), grid, dim3(256), 0, st, x, rows, C, eps, layer,          \
+                       (const unsigned short*)w, (const unsigned short*)b, ms, mh, mstride, mf32, rpg, act, res, rf32, \
+                       out, (unsigned short*)shadow)
+    if (xf32) EGG_RNK(true, false);
+    else if (of32) EGG_RNK(false, true);
+    else EGG_RNK(false, false);
+#undef EGG_RNK
 }
 
 extern "C" int eggroll_rownorm_ex(const void* x, int32_t x_f32, int64_t rows, int64_t C, float eps, int32_t layer,
                                   const void* w, const void* b, const void* mscale, const void* mshift,
                                   int64_t mstride, int32_t mod_f32, int64_t rows_per_group, int32_t act,
-                                  const void* res, void* out, void* stream) {
+                                  const void* res, int32_t res_f32, void* out, int32_t out_f32, void* shadow,
+                                  void* stream) {
     EGG_CHECK_ARG(rows >= 0 && C > 0 && C % 8 == 0 && C <= 8 * 64 * 8, "rownorm: need C %% 8 == 0, C <= 4096");
     EGG_CHECK_ARG(act >= 0 && act <= 2 && rows_per_group > 0, "rownorm: bad act / rows_per_group");
     EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 && (!res || ((uintptr_t)res & 15) == 0) &&
-                      (!mscale || ((uintptr_t)mscale & 15) == 0) && (!mshift || ((uintptr_t)mshift & 15) == 0),
+                      (!mscale || ((uintptr_t)mscale & 15) == 0) && (!mshift || ((uintptr_t)mshift & 15) == 0) &&
+                      ((uintptr_t)shadow & 15) == 0,
                   "rownorm: pointers must be 16-byte aligned");
     EGG_CHECK_ARG(mstride % 8 == 0, "rownorm: modulation stride must be a multiple of 8");
-    EGG_CHECK_ARG((x_f32 == 0 || x_f32 == 1) && (mod_f32 == 0 || mod_f32 == 1), "rownorm: x_f32 / mod_f32 are 0 or 1");
+    EGG_CHECK_ARG((x_f32 == 0 || x_f32 == 1) && (mod_f32 == 0 || mod_f32 == 1) && (res_f32 == 0 || res_f32 == 1) &&
+                      (out_f32 == 0 || out_f32 == 1) && !(x_f32 && out_f32) && (out_f32 || !shadow),
+                  "rownorm: dtype flags are 0 / 1; fp32 x with fp32 out, or a shadow without fp32 out, unsupported");
     if (rows == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(x && out, "rownorm: NULL pointer");
     hipStream_t st = as_stream(stream);
     const int nch = (int)(C / 8);
 #define EGG_RN(S_, N_) launch_rownorm<S_, N_>(x, x_f32, rows, (int)C, eps, layer, w, b, mscale, mshift, mstride, mod_f32, \
-                                              rows_per_group, act, res, out, st)
+                                              rows_per_group, act, res, res_f32, out, out_f32, shadow, st)
     if (nch <= 16) EGG_RN(16, 1);
     else if (nch <= 32) EGG_RN(32, 1);
     else if (nch <= 64) EGG_RN(64, 1);
@@ -1293,7 +1320,7 @@ extern "C" int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps
                                const void* b, const void* mscale, const void* mshift, int64_t mstride,
                                int64_t rows_per_group, int32_t act, const void* res, void* out, void* stream) {
     return eggroll_rownorm_ex(x, 0, rows, C, eps, layer, w, b, mscale, mshift, mstride, 0, rows_per_group, act, res,
-                              out, stream);
+                              0, out, 0, nullptr, stream);
 }
 
 extern "C" int eggroll_resid_layernorm(float* h, int64_t ldh, const void* y, int64_t ldy, int64_t rows, int64_t C,
@@ -1485,6 +1512,34 @@ extern "C" int eggroll_subpixel_shortcut(const void* y4, const void* x, const vo
                        (const unsigned short*)y4, (const unsigned short*)x, (const unsigned short*)bias,
                        (unsigned short*)out, (int)H, (int)W, (int)Cin, (int)Cout, (int)rep, (int)pix);
     EGG_CHECK_LAUNCH("subpixel_shortcut");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_subpixel_shortcut_f32(const void* y4, const float* x, const void* bias, float* out,
+                                             void* shadow, int64_t B, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                             void* stream) {
+    const int64_t rep = Cin > 0 ? 4 * Cout / Cin : 0;
+    EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && (4 * Cout) % Cin == 0 && Cout % 8 == 0 &&
+                      (rep == 1 || rep == 2 || rep == 4) && Cin % 8 == 0,
+                  "subpixel_shortcut_f32: bad sizes (4 Cout / Cin in {1, 2, 4})");
+    EGG_CHECK_ARG(B * 4 * H * W * Cout < (1ll << 31) && B * (H + 1) * (W + 1) * 4 * Cout < (1ll << 31),
+                  "subpixel_shortcut_f32: tensor too large");
+    if (B == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(y4 && x && out, "subpixel_shortcut_f32: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)bias & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                      ((uintptr_t)shadow & 15) == 0,
+                  "subpixel_shortcut_f32: pointers must be 16-byte aligned");
+    const int64_t lowpix = B * H * W;
+    const dim3 grid((unsigned)((lowpix * (Cout / 8) + 255) / 256));
+#define EGG_SP4F(RP)                                                                                                  \
+    hipLaunchKernelGGL((k_subpixel_shortcut4<RP, true>), grid, dim3(256), 0, as_stream(stream),                   \
+                       (const unsigned short*)y4, (const void*)x, (const unsigned short*)bias, (void*)out, (int)H,  \
+                       (int)W, (int)Cin, (int)Cout, (int)lowpix, (unsigned short*)shadow)
+    if (rep == 1) EGG_SP4F(1);
+    else if (rep == 2) EGG_SP4F(2);
+    else EGG_SP4F(4);
+#undef EGG_SP4F
+    EGG_CHECK_LAUNCH("subpixel_shortcut_f32");
     return EGGROLL_OK;
 }
 

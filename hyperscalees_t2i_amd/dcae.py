@@ -46,8 +46,11 @@ class RMSNormC(nn.Module):
         self.weight = _p(c)
         self.bias = _p(c)
 
-    def forward(self, x, res=None, act=None):  # NHWC; fused norm * w + b [act] [+ res]
-        return K.rownorm(x.contiguous(), self.eps, layer=False, w=self.weight, b=self.bias, act=act, res=res)
+    def forward(self, x, res=None, act=None, shadow=None):  # NHWC; fused norm * w + b [act] [+ res]
+        """An fp32 res is the fp32 residual stream: updated in place (res = norm(x) * w + b + res), shadow
+        receiving its bf16 copy."""
+        return K.rownorm(x.contiguous(), self.eps, layer=False, w=self.weight, b=self.bias, act=act, res=res,
+                         shadow=shadow)
 
 
 class Conv3x3(nn.Module):
@@ -106,6 +109,22 @@ class ResBlock(nn.Module):
         h = K.bias_act_(h, c1.bias, "silu")                       # bias + SiLU in one pass
         return self.norm(self.conv2(h), res=x)
 
+    def forward_f32(self, x32, x16):
+        """The block on the fp32 residual stream (x32 updated in place, x16 its bf16 shadow = the convs'
+        input): conv1 + SiLU and conv2 on libeggroll's MFMA kernels (conv2 without the fused norm tail),
+        then RMSNorm + the fp32 residual add in one row pass."""
+        if self.px and x16.shape[2] % self.px == 0:
+            if self.packed is None:
+                self.refresh_packed_weights()
+            w1, b1, w2 = self.packed
+            h = K.conv3x3_nhwc(K.conv3x3_nhwc(x16, w1, b1, self.px, "silu"), w2, None, self.px)
+        else:
+            c1 = self.conv1
+            h = nhwc(F.conv2d(nchw(x16), c1.weight, None, padding=1)).contiguous()
+            h = self.conv2(K.bias_act_(h, c1.bias, "silu"))
+        self.norm(h, res=x32, shadow=x16)
+        return x32, x16
+
     def forward_reference(self, x):
         return self.norm(self.conv2(F.silu(self.conv1(x))), res=x)
 
@@ -121,7 +140,9 @@ class GLUMBConvC(nn.Module):
         self.w_point = _p(c, h)
         self.norm = RMSNormC(c)
 
-    def forward(self, x):  # NHWC
+    def forward(self, x, res32=None, shadow=None):  # NHWC
+        """res32 (optional): the fp32 residual stream, updated in place instead of returning x + block(x)
+        (shadow = its bf16 copy)."""
         B, H, W, C = x.shape
         if C <= 512:
             # 1x1 conv + SiLU on the 8-phase GEMM (SiLU in its epilogue; same values as the unfused
@@ -136,7 +157,7 @@ class GLUMBConvC(nn.Module):
         else:
             h = F.linear(x, self.w_inv, self.b_inv)
             g = K.dwconv_nhwc(h, self.w_dw, self.b_dw, 3, pre_silu=True, glu=True)
-        return self.norm(F.linear(g, self.w_point), res=x)
+        return self.norm(F.linear(g, self.w_point), res=x if res32 is None else res32, shadow=shadow)
 
 
 class MultiscaleLinearAttention(nn.Module):
@@ -189,7 +210,7 @@ class MultiscaleLinearAttention(nn.Module):
             self._planar_key = key
         return self._planar_w
 
-    def forward(self, x):  # NHWC
+    def forward(self, x, res32=None, shadow=None):  # NHWC; res32 / shadow: as GLUMBConvC.forward
         B, H, W, C = x.shape
         planar = H * W >= self.PLANAR_MIN_TOKENS
         w_qkv, ms_dw, ms_pw = self._planar_weights() if planar else (self.w_qkv, self.ms_dw, self.ms_pw)
@@ -204,7 +225,7 @@ class MultiscaleLinearAttention(nn.Module):
             pg = K.dwconv_pw_nhwc(qkv, wdw, wpw, ks).view(B * H * W, 3 * inner)
             self._attend(pg.view(B, H, W, 3 * inner), o[:, (i + 1) * inner:(i + 2) * inner], planar)
         y = F.linear(o.view(B, H, W, -1), self.w_out)
-        return self.norm_out(y, res=x)
+        return self.norm_out(y, res=x if res32 is None else res32, shadow=shadow)
 
 
 class EfficientViTBlock(nn.Module):
@@ -215,6 +236,11 @@ class EfficientViTBlock(nn.Module):
 
     def forward(self, x):
         return self.conv_out(self.attn(x))
+
+    def forward_f32(self, x32, x16):
+        self.attn(x16, res32=x32, shadow=x16)
+        self.conv_out(x16, res32=x32, shadow=x16)
+        return x32, x16
 
 
 def subpixel_phase_weights(w3: torch.Tensor) -> torch.Tensor:
@@ -264,6 +290,19 @@ class UpBlock(nn.Module):
             y4 = nhwc(F.conv2d(nchw(x), self.w4, None, padding=1)).contiguous()
         return K.subpixel_shortcut(y4, x, bias=self.conv.bias)
 
+    def forward_f32(self, x32, x16):
+        """On the fp32 residual stream: the phase conv reads the bf16 shadow, the interleave + bias +
+        shortcut reads the fp32 stream and writes the new fp32 stream and its shadow in one pass."""
+        if self.w4 is None:
+            self.refresh_phase_weights()
+        if self.w4p is not None:
+            y4 = K.conv_nhwc(x16, self.w4p, None, 2)
+        else:
+            y4 = nhwc(F.conv2d(nchw(x16), self.w4, None, padding=1)).contiguous()
+        B, H, W, _ = x32.shape
+        s16 = torch.empty((B, 2 * H, 2 * W, y4.shape[-1] // 4), dtype=torch.bfloat16, device=x32.device)
+        return K.subpixel_shortcut_f32(y4, x32, bias=self.conv.bias, shadow=s16), s16
+
     def forward_reference(self, x):  # the literal architecture (for tests)
         up = F.interpolate(nchw(x), scale_factor=2, mode="nearest")
         y = self.conv(nhwc(up).contiguous())
@@ -277,6 +316,7 @@ class DCAEDecoder(nn.Module):
         self.scaling_factor = scaling_factor
         self.latent_channels = latent_channels
         self.widths, self.layers, self.vit_from = tuple(widths), tuple(layers), vit_from
+        self.fp32_stream = True   # the fp32 residual stream; False: the round-3 bf16 stream (A/B)
         self.conv_in = Conv3x3(latent_channels, widths[-1])
         self.in_repeats = widths[-1] // latent_channels
         stages = []
@@ -314,6 +354,8 @@ class DCAEDecoder(nn.Module):
                 m.refresh_packed_weights()
 
     def forward(self, z):  # z [B, 32, h, w] -> image [B, 3, 32h, 32w] (channels-last) in ~[-1, 1]
+        if self.fp32_stream:
+            return self.forward_f32(z)
         zt = nhwc(z.to(torch.bfloat16)).contiguous()
         x = self.conv_in(zt) + zt.repeat_interleave(self.in_repeats, dim=-1)
         for st in self.stages:
@@ -323,3 +365,20 @@ class DCAEDecoder(nn.Module):
             return nchw(K.dcae_head(x, no.eps, no.weight, no.bias, self.conv_out.weight, self.conv_out.bias))
         x = self.norm_out(x, act="relu")
         return nchw(self.conv_out(x))
+
+    def forward_f32(self, z):
+        """The decoder on an fp32 residual stream: every block updates the fp32 stream x32
+        in place (fused into the row norm / up-block interleave passes) and refreshes its bf16 shadow x16,
+        which is what every conv / GEMM reads; the conv_in shortcut adds the fp32 latent.  The bf16
+        stream rounded the decoder's residual after every block — the largest source of member-
+        differential drift left after the transformer's fp32 stream."""
+        zt = nhwc(z.to(torch.bfloat16)).contiguous()
+        x32 = self.conv_in(zt).float() + nhwc(z.float()).repeat_interleave(self.in_repeats, dim=-1)
+        x16 = x32.to(torch.bfloat16)
+        for st in self.stages:
+            for blk in st:
+                x32, x16 = blk.forward_f32(x32, x16)
+        if x16.shape[-1] == 128 and self.conv_out.weight.shape[0] == 3:
+            no = self.norm_out
+            return nchw(K.dcae_head(x16, no.eps, no.weight, no.bias, self.conv_out.weight, self.conv_out.bias))
+        return nchw(self.conv_out(self.norm_out(x16, act="relu")))

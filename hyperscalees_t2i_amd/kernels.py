@@ -551,21 +551,32 @@ ACT = {None: 0, "none": 0, "relu": 1, "silu": 2}
 def rownorm(x: torch.Tensor, eps: float, layer: bool = False, w: Optional[torch.Tensor] = None,
             b: Optional[torch.Tensor] = None, mscale: Optional[torch.Tensor] = None,
             mshift: Optional[torch.Tensor] = None, rows_per_group: int = 1, act=None,
-            res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+            res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+            shadow: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused (RMS|Layer)Norm over the last dim [+w][*(1+mscale[g])][+mshift[g]][+b][act][+res].
     mscale / mshift: [groups, C] views (rows `mstride` apart), g = row // rows_per_group.
-    x may be fp32 (the fp32 residual stream) and mscale / mshift fp32 (the fp32 modulation); the
-    output is bf16 (eggroll_rownorm_ex)."""
+    x may be fp32 (the Sana fp32 residual stream) and mscale / mshift fp32 (the fp32 modulation); the
+    output is bf16 — unless res is fp32 (the DC-AE fp32 residual stream): then the output is fp32
+    (default: written into res in place) and `shadow` (optional bf16) receives its bf16 copy
+    (eggroll_rownorm_ex)."""
     if x.dtype not in (torch.bfloat16, torch.float32):
         raise _lib.EggrollError("rownorm(x): expected bf16 or fp32")
     _dev(x, "rownorm(x)", x.dtype)
     C = x.shape[-1]
     rows = x.numel() // C
+    of32 = res is not None and res.dtype == torch.float32
     if out is None:
-        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-    for t, nm in ((w, "w"), (b, "b"), (res, "res")):
+        out = res if of32 else torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    _dev(out, "rownorm(out)", torch.float32 if of32 else torch.bfloat16)
+    if shadow is not None:
+        if not of32:
+            raise ValueError("rownorm: shadow needs an fp32 res / output")
+        _dev(shadow, "rownorm(shadow)", torch.bfloat16)
+    for t, nm in ((w, "w"), (b, "b")):
         if t is not None:
             _dev(t, f"rownorm({nm})", torch.bfloat16)
+    if res is not None:
+        _dev(res, "rownorm(res)", res.dtype)
     ps, st1 = _row_ptr(mscale, "rownorm(mscale)", C, allow_f32=True)
     ph, st2 = _row_ptr(mshift, "rownorm(mshift)", C, allow_f32=True)
     if ps is not None and ph is not None and (st1 != st2 or mscale.dtype != mshift.dtype):
@@ -574,9 +585,10 @@ def rownorm(x: torch.Tensor, eps: float, layer: bool = False, w: Optional[torch.
     xf32 = int(x.dtype == torch.float32)
     e0 = OpTimer.begin()
     _lib.call("eggroll_rownorm_ex", x.data_ptr(), xf32, rows, C, float(eps), int(bool(layer)), _p(w), _p(b), ps, ph,
-              st1 or st2 or C, mf32, int(rows_per_group), ACT[act], _p(res), out.data_ptr(), _stream(x.device))
-    OpTimer.end(e0, f"rownorm(C={C})", (2.0 + 2 * xf32) * rows * C + 2.0 * rows * C * (2 if res is not None else 1),
-                f"rows{rows}")
+              st1 or st2 or C, mf32, int(rows_per_group), ACT[act], _p(res), int(of32), out.data_ptr(), int(of32),
+              _p(shadow), _stream(x.device))
+    OpTimer.end(e0, f"rownorm(C={C})", (2.0 + 2 * xf32) * rows * C + rows * C * (
+        (8.0 + (2 if shadow is not None else 0)) if of32 else (4.0 if res is not None else 2.0)), f"rows{rows}")
     return out
 
 
@@ -678,6 +690,31 @@ def subpixel_shortcut(y4: torch.Tensor, x: torch.Tensor, out: Optional[torch.Ten
     _lib.call("eggroll_subpixel_shortcut", y4.data_ptr(), x.data_ptr(), _p(bias), out.data_ptr(), B, H, W, Cin,
               Cout, _stream(x.device))
     OpTimer.end(e0, "subpixel_shortcut", 2.0 * (y4.numel() + x.numel() + out.numel()), f"{tuple(x.shape)}->{Cout}")
+    return out
+
+
+def subpixel_shortcut_f32(y4: torch.Tensor, x32: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                          shadow: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """subpixel_shortcut on the DC-AE fp32 residual stream: x32 [B,H,W,Cin] fp32 (shortcut source) ->
+    out [B,2H,2W,Cout] fp32; shadow (optional [B,2H,2W,Cout] bf16) receives bf16(out)."""
+    _dev(y4, "subpixel_f32(y4)", torch.bfloat16)
+    _dev(x32, "subpixel_f32(x)", torch.float32)
+    B, H, W, Cin = x32.shape
+    if y4.shape[:3] != (B, H + 1, W + 1) or y4.shape[3] % 4:
+        raise ValueError(f"subpixel_f32: y4 {tuple(y4.shape)} vs x {tuple(x32.shape)}")
+    Cout = y4.shape[3] // 4
+    if bias is not None:
+        _dev(bias, "subpixel_f32(bias)", torch.bfloat16)
+    out = torch.empty((B, 2 * H, 2 * W, Cout), dtype=torch.float32, device=x32.device)
+    if shadow is not None:
+        _dev(shadow, "subpixel_f32(shadow)", torch.bfloat16)
+        if shadow.shape != out.shape:
+            raise ValueError("subpixel_f32: shadow shape")
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_subpixel_shortcut_f32", y4.data_ptr(), x32.data_ptr(), _p(bias), out.data_ptr(), _p(shadow), B,
+              H, W, Cin, Cout, _stream(x32.device))
+    OpTimer.end(e0, "subpixel_shortcut_f32", 2.0 * y4.numel() + 4.0 * x32.numel() + (6.0 if shadow is not None else 4.0)
+                * out.numel(), f"{tuple(x32.shape)}->{Cout}")
     return out
 
 

@@ -257,12 +257,15 @@ int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps, int32_t l
 /* x[r, :] += gate[r / rows_per_group, :] * y[r, :]  (bf16, in place; gate rows gstride apart). */
 int eggroll_gated_residual(void* x, const void* y, const void* gate, int64_t gstride, int64_t rows,
                            int64_t C, int64_t rows_per_group, void* stream);
-/* The same row normalisation with an fp32 input x (x_f32 = 1: the fp32 residual stream of the Sana
- * blocks) and / or fp32 modulation vectors (mod_f32 = 1: the fp32 AdaLN modulation); output bf16.   */
+/* The same row normalisation with dtype options: x_f32 = 1: fp32 input x (the fp32 residual stream of
+ * the Sana blocks); mod_f32 = 1: fp32 modulation vectors (the fp32 AdaLN modulation); res_f32 = 1: fp32
+ * res; out_f32 = 1: fp32 output (the DC-AE fp32 residual stream, out = norm(x)·w + b + res, may alias
+ * res) with `shadow` (optional) receiving bf16(out); else out is bf16 and shadow must be NULL.
+ * x_f32 with out_f32 is not supported.                                                             */
 int eggroll_rownorm_ex(const void* x, int32_t x_f32, int64_t rows, int64_t C, float eps, int32_t layer,
                        const void* w, const void* b, const void* mscale, const void* mshift, int64_t mstride,
-                       int32_t mod_f32, int64_t rows_per_group, int32_t act, const void* res, void* out,
-                       void* stream);
+                       int32_t mod_f32, int64_t rows_per_group, int32_t act, const void* res, int32_t res_f32,
+                       void* out, int32_t out_f32, void* shadow, void* stream);
 /* fp32 residual stream update: x = fma(gate[g], y, x) (gate bf16 or fp32 per gate_f32; NULL: x += y),
  * x fp32 [rows, C] in place, y bf16; shadow (optional) receives bf16(x).  The unfused form of the
  * EPI_RES32 / EPI_GATED32 GEMM epilogues (eggroll_lora_linear_pop_epi epi 4 / 5), bit-identical.   */
@@ -289,6 +292,10 @@ int eggroll_upshortcut_add(void* y, const void* x, int64_t B, int64_t H, int64_t
  * the phase conv runs without one).                                                            */
 int eggroll_subpixel_shortcut(const void* y4, const void* x, const void* bias, void* out, int64_t B,
                               int64_t H, int64_t W, int64_t Cin, int64_t Cout, void* stream);
+/* The same on the DC-AE fp32 residual stream: x (shortcut source) and out fp32, shadow (optional)
+ * bf16(out); 4 Cout / Cin in {1, 2, 4}, Cin % 8 == 0.                                              */
+int eggroll_subpixel_shortcut_f32(const void* y4, const float* x, const void* bias, float* out, void* shadow,
+                                  int64_t B, int64_t H, int64_t W, int64_t Cin, int64_t Cout, void* stream);
 
 /* DC-AE decoder head (norm_out + ReLU + conv_out of the reference AutoencoderDC decoder), NHWC:
  *   a[p, c] = bf16(relu(x[p, c] / sqrt(mean_c x[p, :]^2 + eps) * norm_w[c] + norm_b[c]))

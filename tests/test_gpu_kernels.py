@@ -441,6 +441,52 @@ def test_subpixel_shortcut_bit_exact(dev, cin, cout, with_bias):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("cin,cout", [(64, 32), (64, 64), (128, 64)])
+def test_subpixel_shortcut_f32(dev, cin, cout):
+    """The DC-AE fp32-stream up-block interleave: fp32 shortcut source and output, bf16 shadow = bf16(out);
+    the same arithmetic as the bf16 kernel on the fp32 values (exact vs the torch restatement)."""
+    g = torch.Generator().manual_seed(cin * cout)
+    B, H, W = 2, 5, 7
+    x = torch.randn(B, H, W, cin, generator=g).to(dev)
+    y4 = torch.randn(B, H + 1, W + 1, 4 * cout, generator=g).to(torch.bfloat16).to(dev)
+    bias = torch.randn(cout, generator=g).to(torch.bfloat16).to(dev)
+    sh = torch.empty(B, 2 * H, 2 * W, cout, dtype=torch.bfloat16, device=dev)
+    got = K.subpixel_shortcut_f32(y4, x, bias=bias, shadow=sh)
+    rep = 4 * cout // cin
+    ref = torch.empty(B, 2 * H, 2 * W, cout, device=dev)
+    c = torch.arange(cout, device=dev)
+    for i in range(2):
+        for j in range(2):
+            k = 2 * i + j
+            ref[:, i::2, j::2, :] = (y4[:, i:i + H, j:j + W, k * cout:(k + 1) * cout].float() + bias.float()) \
+                + x[:, :, :, (4 * c + k) // rep]
+    assert torch.equal(got, ref) and torch.equal(sh, ref.to(torch.bfloat16))
+
+
+def test_rownorm_fp32_residual_stream(dev):
+    """eggroll_rownorm_ex with an fp32 res and fp32 output (the DC-AE fp32 stream, in place) and a bf16
+    shadow: out = rms(x) * w + b + res exactly as the bf16-output kernel computes it before rounding."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    rows, C = 5000, 256
+    x = (torch.randn((rows, C), generator=g, device=dev) * 2).to(torch.bfloat16)
+    w = (torch.rand(C, generator=g, device=dev) + 0.5).to(torch.bfloat16)
+    b = (torch.randn(C, generator=g, device=dev) * 0.1).to(torch.bfloat16)
+    r32 = torch.randn((rows, C), generator=g, device=dev)
+    sh = torch.empty((rows, C), dtype=torch.bfloat16, device=dev)
+    st = r32.clone()
+    out = K.rownorm(x, 1e-5, w=w, b=b, res=st, shadow=sh)
+    assert out.data_ptr() == st.data_ptr() and out.dtype == torch.float32
+    xf = x.float()
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float() + b.float() + r32
+    assert (out - ref).abs().max() <= 1e-5 * ref.abs().max()
+    assert torch.equal(sh, out.to(torch.bfloat16))
+    # bf16 res -> bf16 output: the unchanged kernel path equals bf16 of the fp32 form with bf16 res
+    o16 = K.rownorm(x, 1e-5, w=w, b=b, res=r32.to(torch.bfloat16))
+    st2 = r32.to(torch.bfloat16).float()
+    o32 = K.rownorm(x, 1e-5, w=w, b=b, res=st2)
+    assert torch.equal(o16, o32.to(torch.bfloat16))
+
+
 @pytest.mark.parametrize("B,H,W", [(2, 37, 21), (1, 64, 64)])
 def test_dcae_head_matches_unfused(dev, B, H, W):
     """k_dcae_head (RMSNorm*w+b -> ReLU -> 3x3 conv 128->3 +bias, MFMA) vs the unfused rownorm kernel +
