@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
                                                      const unsigned short* __restrict__ bias, // [Cin] or null
                                                      int H, int W, int Cin, int xtiles, int bands, int cslices,
                                                      unsigned short* __restrict__ out,
-                                                     const unsigned short* __restrict__ pw = nullptr, int ord = 0) {
+                                                     const unsigned short* __restrict__ pw = nullptr, int ord = 0,
+                                                     int ldo = 0) {
     static_assert(!PW || (!GLU && DW_CS == 32 && DW_TH * DW_TW == 256), "PW: one 32-channel group per block");
     constexpr int PLANES = GLU ? 2 : 1;
     constexpr int HALO = KS / 2;
@@ -65,6 +66,9 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
     char* const pwt = lds + IN_BYTES;
     auto swz = [](uint32_t L) { return L ^ ((L >> 3) & 32u); };
     const int Cout = GLU ? Cin / 2 : Cin;
+    // output row stride: ldo > Cout pads each pixel's row (the last channel slice's blocks zero the
+    // <= 32 pad channels), so a following GEMM sees K = ldo, a multiple of its 64-wide k-step
+    const int64_t ldo_ = ldo > 0 ? ldo : Cout;
     const int tid = threadIdx.x;
     // Block order on each XCD (xcd_remap: an XCD walks a contiguous range of ids, ~96 blocks in flight).
     // ord 0: channel slice fastest — adjacent slices share 128-B lines, but a band's vertical neighbour
@@ -202,7 +206,10 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
                     u16x4m o;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) o[i] = f2b(GLU ? res[oy][i] * silu(acc[i]) : acc[i]);
-                    *reinterpret_cast<u16x4m*>(out + (((int64_t)b * H + y) * W + x) * Cout + cq) = o;
+                    unsigned short* orow = out + (((int64_t)b * H + y) * W + x) * ldo_;
+                    *reinterpret_cast<u16x4m*>(orow + cq) = o;
+                    if (ldo_ > Cout && cs == cslices - 1 && Cout + q * 4 < ldo_)
+                        *reinterpret_cast<u16x4m*>(orow + Cout + q * 4) = u16x4m{0, 0, 0, 0};
                 }
             }
         }
@@ -1097,6 +1104,9 @@ __global__ __launch_bounds__(256) void k_clip_resize_v(const unsigned char* __re
 //   o = O / rowsum, written as 4 consecutive dims of one query per lane (8-B stores) in the q layout.
 // Keys past L are excluded (-inf); the additive bias is the reference's attention mask.
 // ------------------------------------------------------------------------------------
+#ifndef EGG_XA_PREFETCH
+#define EGG_XA_PREFETCH 1
+#endif
 constexpr int XA_LMAX = 320;          // keys per (caption, head) staged in LDS
 constexpr int XA_KF = XA_LMAX / 16;   // key fragments
 
@@ -1151,20 +1161,33 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     __syncthreads();
     const int nkf = (L + 15) / 16, nkb = (L + 31) / 32;  // key fragments / 32-key PV steps in use
     const int nqb = (N + 16 * QF - 1) / (16 * QF);
-    for (int qb = w; qb < nqb; qb += NWAVE) {
-        // B = Q^T fragments for the 4 k-steps (dims 32ks + 8g .. +7; dims >= 112 are zero)
-        la_bf16x8 bq[QF][KSN];
+    // B = Q^T fragments for the 4 k-steps (dims 32ks + 8g .. +7; dims >= 112 are zero).  EGG_XA_PREFETCH:
+    // the next block's q fragments are loaded right after this block's S^T MFMAs are issued, so their
+    // global-load latency runs under the softmax and PV instead of opening the next block.
+    auto load_q = [&](int qb_, la_bf16x8 (&dst)[QF][KSN]) {
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
-            const int qrow = qb * 16 * QF + 16 * x + r16;
+            const int qrow = qb_ * 16 * QF + 16 * x + r16;
 #pragma unroll
             for (int ks = 0; ks < KSN; ++ks) {
                 const int d0 = 32 * ks + 8 * g;
                 u16x8m t = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
                 if (d0 < HD && qrow < N)
                     t = *reinterpret_cast<const u16x8m*>(q + ((int64_t)b * N + qrow) * ldq + (int64_t)h * HD + d0);
-                bq[x][ks] = __builtin_bit_cast(la_bf16x8, t);
+                dst[x][ks] = __builtin_bit_cast(la_bf16x8, t);
             }
+        }
+    };
+    la_bf16x8 bq[QF][KSN], bqn[QF][KSN];
+    if (EGG_XA_PREFETCH && w < nqb) load_q(w, bqn);
+    for (int qb = w; qb < nqb; qb += NWAVE) {
+        if (EGG_XA_PREFETCH) {
+#pragma unroll
+            for (int x = 0; x < QF; ++x)
+#pragma unroll
+                for (int ks = 0; ks < KSN; ++ks) bq[x][ks] = bqn[x][ks];
+        } else {
+            load_q(qb, bq);
         }
         // S^T[key][query] for every key fragment
         la_f32x4 sf[QF][XA_KF];
@@ -1197,6 +1220,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
                 }
             }
         }
+        if (EGG_XA_PREFETCH && qb + NWAVE < nqb) load_q(qb + NWAVE, bqn);
         float sum[QF];
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
@@ -1395,15 +1419,24 @@ extern "C" int eggroll_dwconv_nhwc(const void* in, const void* w_t, const void* 
 extern "C" int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
                                        int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
                                        int32_t kernel, void* stream) {
+    return eggroll_dwconv_nhwc_ex(in, w_t, bias, B, H, W, C, ks, pre_silu, glu, out, glu ? C / 2 : C, kernel, stream);
+}
+
+extern "C" int eggroll_dwconv_nhwc_ex(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
+                                      int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
+                                      int64_t ldo, int32_t kernel, void* stream) {
     EGG_CHECK_ARG(kernel >= 0 && kernel <= 2, "dwconv: kernel must be 0 (auto), 1 (channel-fastest) or 2 (column "
                   "sweep) (got %d)", kernel);
     EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0 && C > 0, "dwconv: bad sizes");
     const int64_t cout = glu ? C / 2 : C;
     EGG_CHECK_ARG((!glu || C % 2 == 0) && cout % DW_CS == 0, "dwconv: output channels must be a multiple of %d", DW_CS);
+    EGG_CHECK_ARG(ldo >= cout && ldo - cout <= DW_CS && ldo % 8 == 0,
+                  "dwconv: output row stride %lld must be in [%lld, %lld] and a multiple of 8", (long long)ldo,
+                  (long long)cout, (long long)(cout + DW_CS));
     EGG_CHECK_ARG(ks == 3 || ks == 5, "dwconv: ks=%d unsupported (3, 5)", ks);
     EGG_CHECK_ARG(((uintptr_t)in & 15) == 0 && ((uintptr_t)w_t & 15) == 0 && ((uintptr_t)out & 15) == 0,
                   "dwconv: pointers must be 16-byte aligned");
-    EGG_CHECK_ARG(H * W * C < (1ll << 31), "dwconv: image too large");
+    EGG_CHECK_ARG(H * W * C < (1ll << 31) && H * W * ldo < (1ll << 31), "dwconv: image too large");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(in && w_t && out, "dwconv: NULL pointer");
     const int64_t bands = (H + DW_TH - 1) / DW_TH, xtiles = (W + DW_TW - 1) / DW_TW, cslices = cout / DW_CS;
@@ -1417,7 +1450,7 @@ extern "C" int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const vo
     auto* o = (unsigned short*)out;
 #define EGG_DW(KS_, PS_, GL_)                                                                                 \
     hipLaunchKernelGGL((k_dwconv_nhwc<KS_, PS_, GL_>), grid, dim3(256), 0, st, i, w, bb, (int)H, (int)W, (int)C,  \
-                       (int)xtiles, (int)bands, (int)cslices, o, nullptr, dw_order(kernel))
+                       (int)xtiles, (int)bands, (int)cslices, o, nullptr, dw_order(kernel), (int)ldo)
     if (ks == 3 && pre_silu && glu) EGG_DW(3, true, true);
     else if (ks == 3 && !pre_silu && glu) EGG_DW(3, false, true);
     else if (ks == 3 && pre_silu && !glu) EGG_DW(3, true, false);

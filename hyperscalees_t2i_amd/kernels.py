@@ -493,9 +493,11 @@ class OpTimer:
 
 
 def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], ks: int, pre_silu: bool,
-                glu: bool, out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
+                glu: bool, out: Optional[torch.Tensor] = None, kernel: int = 0, ldo: int = 0) -> torch.Tensor:
     """x [B,H,W,C] bf16 contiguous; w_t [ks*ks, C] bf16; returns [B,H,W,C or C/2].
-    kernel: block order, 0 auto, 1 channel-fastest, 2 column sweep (eggroll_dwconv_nhwc_sel)."""
+    kernel: block order, 0 auto, 1 channel-fastest, 2 column sweep (eggroll_dwconv_nhwc_sel).
+    ldo > 0: output channel stride (eggroll_dwconv_nhwc_ex): returns [B,H,W,ldo] whose channels past
+    C (C/2) are zeros."""
     _dev(x, "dwconv(x)", torch.bfloat16)
     _dev(w_t, "dwconv(w_t)", torch.bfloat16)
     B, H, W, C = x.shape
@@ -504,11 +506,14 @@ def dwconv_nhwc(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor]
     if bias is not None:
         _dev(bias, "dwconv(bias)", torch.bfloat16)
     co = C // 2 if glu else C
+    ldo = ldo or co
     if out is None:
-        out = torch.empty((B, H, W, co), dtype=torch.bfloat16, device=x.device)
+        out = torch.empty((B, H, W, ldo), dtype=torch.bfloat16, device=x.device)
+    elif out.shape != (B, H, W, ldo) or not out.is_contiguous():
+        raise ValueError(f"dwconv(out) {tuple(out.shape)} != ({B}, {H}, {W}, {ldo}) contiguous")
     e0 = OpTimer.begin()
-    _lib.call("eggroll_dwconv_nhwc_sel", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu),
-              int(glu), out.data_ptr(), int(kernel), _stream(x.device))
+    _lib.call("eggroll_dwconv_nhwc_ex", x.data_ptr(), w_t.data_ptr(), _p(bias), B, H, W, C, ks, int(pre_silu),
+              int(glu), out.data_ptr(), ldo, int(kernel), _stream(x.device))
     OpTimer.end(e0, f"dwconv_nhwc<{ks},{int(pre_silu)},{int(glu)}>", 2.0 * B * H * W * (C + co), f"{B}x{H}x{W}x{C}")
     return out
 

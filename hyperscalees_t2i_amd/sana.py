@@ -219,17 +219,36 @@ class GLUMBConv(nn.Module):
         self.b_dw = nn.Parameter(torch.zeros(2 * hidden, dtype=torch.bfloat16), requires_grad=False)
         self.w_point = nn.Parameter(torch.empty(dim, hidden, dtype=torch.bfloat16), requires_grad=False)
 
-    def forward(self, x, H: int, W: int):  # x [B, N, D]
+    def _point_weight(self, kp: int) -> torch.Tensor:
+        """w_point zero-padded to kp input channels (cached; rebuilt when w_point changes)."""
+        key = (self.w_point._version, self.w_point.data_ptr(), kp)
+        if getattr(self, "_wp_key", None) != key:
+            self._wp = F.pad(self.w_point.detach(), (0, kp - self.hidden)).contiguous()
+            self._wp_key = key
+        return self._wp
+
+    def forward(self, x, H: int, W: int, res=None, gate=None):  # x [B, N, D]
+        """res / gate (optional): the block's gated residual x += gate_mlp * ff(x) fused into the
+        point conv's GEMM epilogue ("gated32" on the fp32 stream, "gated" on bf16); returns res."""
         B, N, D = x.shape
         # 1x1 conv + SiLU on the 8-phase GEMM (SiLU of the bf16-rounded output in its epilogue), then
         # dw3x3 -> GLU fused; the same values as F.linear -> dwconv(pre_silu=True)
+        kp = -(-self.hidden // 64) * 64     # 5600 -> 5632: the GEMM's k-step is 64
         if lora.FUSE_EPILOGUES:
             h = K.lora_linear_pop_epi(x.reshape(B * N, D), self.w_inv, self.b_inv, None, 0, 0, 0, 0.0, B * N, "silu")
-            g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=False, glu=True)
+            g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=False, glu=True, ldo=kp)
         else:
             h = K.lora_linear_pop(x.reshape(B * N, D), self.w_inv, self.b_inv, None, 0, 0, 0, 0.0, B * N)
-            g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=True, glu=True)
-        return F.linear(g.view(B, N, -1), self.w_point)
+            g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=True, glu=True, ldo=kp)
+        # 1x1 point conv on the 8-phase GEMM: the GLU output's zero pad channels meet the weight's zero
+        # pad columns (exact), so hipBLASLt's K = 5600 GEMM and its separate residual pass are gone
+        g, wp = g.view(B * N, kp), self._point_weight(kp)
+        if res is None:
+            return K.lora_linear_pop(g, wp, None, None, 0, 0, 0, 0.0, B * N).view(B, N, D)
+        epi = "gated32" if res.dtype == torch.float32 else "gated"
+        K.lora_linear_pop_epi(g, wp, None, None, 0, 0, 0, 0.0, B * N, epi, res=res.view(B * N, D), gate=gate,
+                              rows_per_group=N)
+        return res
 
 
 class SanaBlock(nn.Module):
@@ -258,7 +277,10 @@ class SanaBlock(nn.Module):
             K.gated_residual_f32_(x32, self.attn1(n), mods[:, 2], rows_per_group=N, shadow=x16)
             K.gated_residual_f32_(x32, self.attn2(x16, enc, mask_bias, enc_index), None, rows_per_group=N)
         n = K.rownorm(x32, self.eps, layer=True, mscale=mods[:, 4], mshift=mods[:, 3], rows_per_group=N)
-        K.gated_residual_f32_(x32, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
+        if lora.FUSE_EPILOGUES:
+            self.ff(n, H, W, res=x32, gate=mods[:, 5])             # x32 += gate_mlp * ff(n)
+        else:
+            K.gated_residual_f32_(x32, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
         return x32
 
     def forward(self, x, enc, mask_bias, timestep, H, W, enc_index=None):
@@ -273,7 +295,10 @@ class SanaBlock(nn.Module):
             K.gated_residual_(x, self.attn1(n), mods[:, 2], rows_per_group=N)
             x = x + self.attn2(x, enc, mask_bias, enc_index)
         n = K.rownorm(x, self.eps, layer=True, mscale=mods[:, 4], mshift=mods[:, 3], rows_per_group=N)
-        K.gated_residual_(x, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
+        if lora.FUSE_EPILOGUES:
+            self.ff(n, H, W, res=x, gate=mods[:, 5])               # x += gate_mlp * ff(n)
+        else:
+            K.gated_residual_(x, self.ff(n, H, W), mods[:, 5], rows_per_group=N)
         return x
 
 

@@ -245,6 +245,13 @@ int eggroll_dwconv_nhwc_sel(const void* in, const void* w_t, const void* bias, i
                             int32_t kernel, void* stream);
 int eggroll_dwconv_pw_nhwc_sel(const void* in, const void* w_t, const void* pw, int64_t B, int64_t H,
                                int64_t W, int64_t C, int32_t ks, void* out, int32_t kernel, void* stream);
+/* eggroll_dwconv_nhwc_sel with an output row stride ldo (elements, cout <= ldo <= cout + 32,
+ * ldo % 8 == 0; cout = glu ? C/2 : C): channels [cout, ldo) of every output pixel are written as
+ * zeros.  The Sana FFN's GLU output (5600 channels) is written at ldo 5632 so the point-wise conv
+ * runs on the LoRA GEMM (K % 64 == 0) against a zero-padded weight.                             */
+int eggroll_dwconv_nhwc_ex(const void* in, const void* w_t, const void* bias, int64_t B, int64_t H,
+                           int64_t W, int64_t C, int32_t ks, int32_t pre_silu, int32_t glu, void* out,
+                           int64_t ldo, int32_t kernel, void* stream);
 
 /* Model-side fused row normalisation of x [rows, C] bf16 (C % 8 == 0, C <= 4096):
  *   y = (x - mean·layer) * rsqrt(var + eps) [* w] [* (1 + mscale[g])] [+ mshift[g]] [+ b];

@@ -9,6 +9,7 @@ import math
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from hyperscalees_t2i_amd import kernels as K
 from hyperscalees_t2i_amd.es import EggRollNoiser, paper_prompt_normalized_scores, standardize_fitness
@@ -346,6 +347,54 @@ def test_dwconv_rejects_unsupported_channels(dev):
     w = torch.zeros(9, 48, dtype=torch.bfloat16, device=dev)
     with pytest.raises(_lib.EggrollError, match="multiple of 32"):
         K.dwconv_nhwc(x, w, None, 3, False, False)
+    x = torch.zeros(1, 4, 4, 64, dtype=torch.bfloat16, device=dev)
+    w = torch.zeros(9, 64, dtype=torch.bfloat16, device=dev)
+    with pytest.raises(_lib.EggrollError, match="row stride"):
+        K.dwconv_nhwc(x, w, None, 3, False, True, ldo=72)    # cout 32: at most 32 pad channels
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 32, 32, 192), (1, 9, 11, 11200)])
+def test_dwconv_padded_output_stride(dev, B, H, W, C):
+    """eggroll_dwconv_nhwc_ex: the GLU output written at row stride cout + 32 equals the packed output
+    in its first cout channels and is zero in the pad (the buffer starts as NaN, so every pad value
+    was written)."""
+    g = torch.Generator().manual_seed(C + 1)
+    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(dev)
+    w = (torch.randn(9, C, generator=g) / 3).to(torch.bfloat16).to(dev)
+    b = torch.randn(C, generator=g).to(torch.bfloat16).to(dev)
+    co = C // 2
+    ref = K.dwconv_nhwc(x, w, b, 3, True, True)
+    out = torch.full((B, H, W, co + 32), float("nan"), dtype=torch.bfloat16, device=dev)
+    got = K.dwconv_nhwc(x, w, b, 3, True, True, out=out, ldo=co + 32)
+    assert torch.equal(got[..., :co], ref)
+    assert torch.equal(got[..., co:], torch.zeros_like(got[..., co:]))
+
+
+def test_sana_ffn_point_conv_on_lora_gemm(dev):
+    """The Sana FFN (GLUMBConv, hidden 5600 -> K padded to 5632) on the 8-phase GEMM vs the torch
+    composition it replaces (F.linear at K = 5600 on hipBLASLt), and its fused gated-residual
+    epilogue ("gated32" into the fp32 stream) vs the unfused gated_residual_f32_."""
+    from hyperscalees_t2i_amd.sana import GLUMBConv
+    B, H, W, D, hid = 2, 16, 16, 2240, 5600
+    ff = GLUMBConv(D, hid).to(dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    with torch.no_grad():
+        for p, s in ((ff.w_inv, D ** -0.5), (ff.w_dw, 1 / 3), (ff.w_point, 0.5 * hid ** -0.5)):
+            p.copy_(torch.randn(p.shape, generator=g, device=dev) * s)
+        ff.b_inv.copy_(torch.randn(ff.b_inv.shape, generator=g, device=dev) * 0.1)
+    x = torch.randn(B, H * W, D, generator=g, device=dev).bfloat16()
+    y = ff(x, H, W)
+    h = F.silu(F.linear(x, ff.w_inv, ff.b_inv))
+    gl = K.dwconv_nhwc(h.view(B, H, W, -1).contiguous(), ff.w_dw, ff.b_dw, 3, pre_silu=False, glu=True)
+    ref = F.linear(gl.view(B, H * W, -1).float(), ff.w_point.float())
+    err = (y.float() - ref).abs()
+    assert (err <= 2 ** -7 * ref.abs() + 1e-2).all(), float(err.max())
+    gate = torch.randn(B, D, generator=g, device=dev)
+    res = torch.randn(B * H * W, D, generator=g, device=dev)
+    want = res.clone()
+    K.gated_residual_f32_(want, y.view(-1, D), gate, rows_per_group=H * W)
+    got = ff(x, H, W, res=res.clone(), gate=gate)
+    assert torch.equal(got, want)
 
 
 # ---------------------------------------------------------------------------------- fused row ops (model)
