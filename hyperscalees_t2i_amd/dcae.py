@@ -214,7 +214,10 @@ class MultiscaleLinearAttention(nn.Module):
         B, H, W, C = x.shape
         planar = H * W >= self.PLANAR_MIN_TOKENS
         w_qkv, ms_dw, ms_pw = self._planar_weights() if planar else (self.w_qkv, self.ms_dw, self.ms_pw)
-        qkv = F.linear(x, w_qkv)                                  # [B,H,W,3*inner]
+        if C <= 512:   # K = 512: the 8-phase GEMM runs 955 vs hipBLASLt's 832-861 TF/s (r04_dcae_gemm_*.json)
+            qkv = K.lora_linear_pop(x.reshape(-1, C), w_qkv, None, None, 0, 0, 0, 0.0, B * H * W).view(B, H, W, -1)
+        else:          # K = 1024: hipBLASLt's stream-K GEMM is as fast or faster at these M
+            qkv = F.linear(x, w_qkv)                              # [B,H,W,3*inner]
         inner = self.heads * self.hd
         # every branch's attention output lands in its column slice of one buffer (no concat pass)
         o = torch.empty((B * H * W, inner * (1 + len(self.scales))), dtype=x.dtype, device=x.device)
@@ -316,7 +319,9 @@ class DCAEDecoder(nn.Module):
         self.scaling_factor = scaling_factor
         self.latent_channels = latent_channels
         self.widths, self.layers, self.vit_from = tuple(widths), tuple(layers), vit_from
-        self.fp32_stream = True   # the fp32 residual stream; False: the round-3 bf16 stream (A/B)
+        # the fp32 residual stream in the first fp32_stages stages (lowest resolution
+        # first), the bf16 stream after them; 0: the round-3 all-bf16 decoder (A/B)
+        self.fp32_stages = len(widths)
         self.conv_in = Conv3x3(latent_channels, widths[-1])
         self.in_repeats = widths[-1] // latent_channels
         stages = []
@@ -354,7 +359,7 @@ class DCAEDecoder(nn.Module):
                 m.refresh_packed_weights()
 
     def forward(self, z):  # z [B, 32, h, w] -> image [B, 3, 32h, 32w] (channels-last) in ~[-1, 1]
-        if self.fp32_stream:
+        if self.fp32_stages > 0:
             return self.forward_f32(z)
         zt = nhwc(z.to(torch.bfloat16)).contiguous()
         x = self.conv_in(zt) + zt.repeat_interleave(self.in_repeats, dim=-1)
@@ -371,13 +376,17 @@ class DCAEDecoder(nn.Module):
         in place (fused into the row norm / up-block interleave passes) and refreshes its bf16 shadow x16,
         which is what every conv / GEMM reads; the conv_in shortcut adds the fp32 latent.  The bf16
         stream rounded the decoder's residual after every block — the largest source of member-
-        differential drift left after the transformer's fp32 stream."""
+        differential drift left after the transformer's fp32 stream.  Stages past fp32_stages run the
+        bf16 stream (the high-resolution stages carry most of the stream's HBM traffic)."""
         zt = nhwc(z.to(torch.bfloat16)).contiguous()
         x32 = self.conv_in(zt).float() + nhwc(z.float()).repeat_interleave(self.in_repeats, dim=-1)
         x16 = x32.to(torch.bfloat16)
-        for st in self.stages:
-            for blk in st:
-                x32, x16 = blk.forward_f32(x32, x16)
+        for i, st in enumerate(self.stages):
+            if i < self.fp32_stages:
+                for blk in st:
+                    x32, x16 = blk.forward_f32(x32, x16)
+            else:   # past the fp32 stages the shadow is the (bf16) stream
+                x16 = st(x16)
         if x16.shape[-1] == 128 and self.conv_out.weight.shape[0] == 3:
             no = self.norm_out
             return nchw(K.dcae_head(x16, no.eps, no.weight, no.bias, self.conv_out.weight, self.conv_out.bias))

@@ -37,7 +37,9 @@ TINY = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_
 # Stated tolerances (bf16 storage / MFMA inputs vs fp32; measured values in DESIGN.md §3).
 # s0 = the BASELINE noise scale sigma = 1e-2; s1 = sigma 0.5, where the perturbed network amplifies
 # the bf16 rounding with depth (measured: 0.3 % at the first linears -> 21 % at block 0's attn2 out)
-# while the member spread of S (1.5) still dwarfs |dS| — so ranks must agree exactly there.
+# while the member spread of S (1.5) still dwarfs |dS| — so ranks must agree there up to near-ties:
+# a pair may only swap if its fp32 scores are closer than twice the largest score error (S1_SCORE_ERR
+# bounds that error; measured round 4: 0.0032, one pair 0.0024 apart swapped).
 BOUNDS = {
     "s0": {"lora_rel": 9e-3,     # every LoRA'd / frozen linear output, ||y - y32|| / ||y32|| (measured 0.59 %)
            "eps_rel": 8.5e-3,    # transformer output (0.56 %)
@@ -46,6 +48,7 @@ BOUNDS = {
            "S_abs": 0.017},      # S[k, j] (0.011; member spread of S 0.051)
     "s1": {"lora_rel": 0.32, "eps_rel": 0.078, "image_rel": 0.095, "reward_abs": 0.11, "S_abs": 0.106},
 }
+S1_SCORE_ERR = 0.006
 KEYS = ("lora_rel", "eps_rel", "image_rel", "reward_abs", "S_abs")
 # test_rank_fidelity_over_seeds (sigma 1e-2, 12 epochs' seeds x 8 members, 336 member pairs): bounds at
 # ~1.5x the measured S drift; pooled Kendall tau >= 0.95 (VERDICT r2 bar)
@@ -177,6 +180,11 @@ def test_member_eval_bf16_vs_fp32_with_reference_noise(stack, dev, golden, case,
               "S_member_spread": round(spread, 6), "rank_exact": bool(np.array_equal(order, order32)),
               "kendall_tau": round(float(kendall_tau(sc, sc32)), 4),
               "best_same": bool(order[-1] == order32[-1]), "worst_same": bool(order[0] == order32[0])}
+    score_err = float(np.abs(sc - sc32).max())
+    disc = [(i, j) for i in range(pop) for j in range(i + 1, pop)
+            if np.sign(sc[i] - sc[j]) * np.sign(sc32[i] - sc32[j]) < 0]
+    report["score_err"] = round(score_err, 5)
+    report["discordant_gaps32"] = [round(float(abs(sc32[i] - sc32[j])), 5) for i, j in disc]
     stages = {}
     for name, Sx in (("transformer", S_tr), ("transformer+dcae", S_img), ("towers", S_tow),
                      ("towers_bf16_residual", S_tow16), ("all", S)):
@@ -188,8 +196,9 @@ def test_member_eval_bf16_vs_fp32_with_reference_noise(stack, dev, golden, case,
                                                  for i, v in per_lin.items()})
     for k, b in BOUNDS[case].items():
         assert worst[k] <= b, (k, worst[k], b, report)
-    if case == "s1":   # member signal >> bf16 noise: the fitness order must be the reference's
-        assert report["rank_exact"] and report["kendall_tau"] == 1.0, report
+    if case == "s1":   # member signal >> bf16 noise: the reference's order up to near-ties
+        assert score_err <= S1_SCORE_ERR and report["best_same"] and report["worst_same"], report
+        assert all(gap <= 2 * score_err for gap in report["discordant_gaps32"]), report
     else:              # one seed's 8 members: a single swapped close pair reads 0.93 (pooled over seeds:
         assert report["kendall_tau"] >= 0.85, report   # test_rank_fidelity_over_seeds)
 
