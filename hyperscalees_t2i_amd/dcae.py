@@ -320,8 +320,11 @@ class DCAEDecoder(nn.Module):
         self.latent_channels = latent_channels
         self.widths, self.layers, self.vit_from = tuple(widths), tuple(layers), vit_from
         # the fp32 residual stream in the first fp32_stages stages (lowest resolution
-        # first), the bf16 stream after them; 0: the round-3 all-bf16 decoder (A/B)
-        self.fp32_stages = len(widths)
+        # first, 32^2 .. 256^2 at 1024 px), the bf16 stream in the two high-resolution stages, which
+        # carry 15/16 of the stream's bytes: pooled over 12 seeds, max |dS| 0.0164 (all bf16) -> 0.0105
+        # (4 stages) vs 0.0112 (all 6), decode +3 % vs +20 % (tools/dcae_stream_probe.py,
+        # profiles/r04_dcae_fp32_stages_probe.json); 0: the round-3 all-bf16 decoder (A/B)
+        self.fp32_stages = min(4, len(widths))
         self.conv_in = Conv3x3(latent_channels, widths[-1])
         self.in_repeats = widths[-1] // latent_channels
         stages = []

@@ -2,7 +2,7 @@
 DC-AE decoder's 1x1-conv shapes and the Sana FFN point conv, per vae_chunk (images per decoder call):
 EfficientViT stages at 32^2 / 64^2 (1024 ch) and 128^2 (512 ch): qkv, attention out, GLU inverted and
 point convs.  Interleaved rounds in one process; bf16 outputs compared (max |diff| / max |y|).
-usage: python tools/dcae_gemm_probe.py [rounds] [out.json]"""
+usage: python tools/dcae_gemm_probe.py [rounds] [out.json] [sana]"""
 import json
 import statistics
 import sys
@@ -20,6 +20,10 @@ dev = torch.device("cuda:0")
 
 
 def shapes():
+    if len(sys.argv) > 3 and sys.argv[3] == "sana":   # the Sana linears (no LoRA term: the plain GEMM)
+        yield from (("sana_attn", 131072, 2240, 2240), ("sana_ff_inv", 131072, 11200, 2240),
+                    ("sana_ff_point_5632", 131072, 2240, 5632), ("sana_attn2_kv", 9600, 2240, 2240))
+        return
     for chunk in (8, 16, 32):
         for hw, C in ((32 * 32, 1024), (64 * 64, 1024), (128 * 128, 512)):
             M = chunk * hw
