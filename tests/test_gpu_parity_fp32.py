@@ -36,24 +36,25 @@ TINY = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_
 
 # Stated tolerances (bf16 storage / MFMA inputs vs fp32; measured values in DESIGN.md §3).
 # s0 = the BASELINE noise scale sigma = 1e-2; s1 = sigma 0.5, where the perturbed network amplifies
-# the bf16 rounding with depth (measured: 0.3 % at the first linears -> 21 % at block 0's attn2 out)
+# the bf16 rounding with depth (measured round 4: 0.3 % at the first linears -> 8.6 % at block 1's attn1 out)
 # while the member spread of S (1.5) still dwarfs |dS| — so ranks must agree there up to near-ties:
 # a pair may only swap if its fp32 scores are closer than twice the largest score error (S1_SCORE_ERR
-# bounds that error; measured round 4: 0.0032, one pair 0.0024 apart swapped).
-BOUNDS = {
-    "s0": {"lora_rel": 9e-3,     # every LoRA'd / frozen linear output, ||y - y32|| / ||y32|| (measured 0.59 %)
-           "eps_rel": 8.5e-3,    # transformer output (0.56 %)
-           "image_rel": 1.8e-2,  # decoded image (1.17 %)
-           "reward_abs": 0.033,  # per-image combined reward, PickScore scale exp(logit_scale) = 14.3 (0.022)
-           "S_abs": 0.017},      # S[k, j] (0.011; member spread of S 0.051)
-    "s1": {"lora_rel": 0.32, "eps_rel": 0.078, "image_rel": 0.095, "reward_abs": 0.11, "S_abs": 0.106},
+# bounds that error; measured round 4: 0.0036, one pair 0.0024 apart swapped).
+BOUNDS = {   # ~1.5x the round-4 measurement (fp32 residual streams in the Sana blocks and DC-AE stages 0-3)
+    "s0": {"lora_rel": 6.5e-3,   # every LoRA'd / frozen linear output, ||y - y32|| / ||y32|| (measured 0.43 %)
+           "eps_rel": 3e-3,      # transformer output (0.19 %; round 3: 0.56 %)
+           "image_rel": 1.25e-2, # decoded image (0.83 %)
+           "reward_abs": 0.02,   # per-image combined reward, PickScore scale exp(logit_scale) = 14.3 (0.013)
+           "S_abs": 0.0125},     # S[k, j] (0.0081; member spread of S 0.051)
+    "s1": {"lora_rel": 0.13, "eps_rel": 0.029, "image_rel": 0.03, "reward_abs": 0.04, "S_abs": 0.022},
 }
 S1_SCORE_ERR = 0.006
 KEYS = ("lora_rel", "eps_rel", "image_rel", "reward_abs", "S_abs")
-# test_rank_fidelity_over_seeds (sigma 1e-2, 12 epochs' seeds x 8 members, 336 member pairs): bounds at
-# ~1.5x the measured S drift; pooled Kendall tau >= 0.95 (VERDICT r2 bar)
-RANK_BOUNDS = {"S_abs": 0.028, "pooled_tau": 0.95,   # measured (round 3, 12 seeds): S_abs 0.0194, pooled tau 0.952
-               "best_worst_misses": 1}
+# test_rank_fidelity_over_seeds (sigma 1e-2, 12 epochs' seeds x 8 members, 336 member pairs): max |dS| at
+# ~1.5x the measurement; pooled Kendall tau >= 0.95 (VERDICT r2 bar) = up to 8 discordant pairs, 3 more
+# than measured; best / worst member may differ in at most 2 of the 12 epochs (measured: 0 / 1)
+RANK_BOUNDS = {"S_abs": 0.016, "pooled_tau": 0.95,   # measured (round 4, 12 seeds): S_abs 0.0105, pooled tau 0.970
+               "best_worst_misses": 2}
 
 
 def kendall_tau(a, b):
