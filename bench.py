@@ -68,11 +68,14 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--small", action="store_true", help="tiny architecture (smoke only; not a valid metric)")
     p.add_argument("--aux-out", type=str, default="", help="write per-phase / per-kernel details here")
-    p.add_argument("--workload", choices=("sana", "var_d16"), default="sana",
-                   help="var_d16: BASELINE configs[0] (VAR-d16, LoRA r 4, 4 classes x 4 batches) on the GPU path")
+    p.add_argument("--workload", choices=("sana", "var_d16", "zimage"), default="sana",
+                   help="var_d16: BASELINE configs[0] (VAR-d16, LoRA r 4, 4 classes x 4 batches) on the GPU path; "
+                        "zimage: configs[3] (Z-Image-Turbo, egg rank 4, one GPU's 16 of pop 128, 384 px, 7 steps)")
     a = p.parse_args()
     if a.workload == "var_d16" and a.pop_per_gpu == 8 and "--pop-per-gpu" not in sys.argv:
         a.pop_per_gpu = 4           # configs[0]: pop_size 4
+    if a.workload == "zimage" and a.pop_per_gpu == 8 and "--pop-per-gpu" not in sys.argv:
+        a.pop_per_gpu = 16          # configs[3]: pop_size 128 across 8 GPUs
     return a
 
 
@@ -135,9 +138,38 @@ def build_var(args, world, rank, device):
     return backend, engine, noiser, theta, pop
 
 
+def build_zimage(args, world, rank, device):
+    """BASELINE configs[3]: Z-Image-Turbo LoRA ES, LoRA r 2 / alpha 8 on to_q,to_k,to_v,linear,w1,w2,w3,
+    egg rank 4, pop_per_gpu (16 = one GPU's share of pop 128) antithetic, 4 prompts x 4 batches per member
+    at 384 px, 7 flow-matching steps, guidance 0 (unifed_es.py:408-492 defaults)."""
+    from hyperscalees_t2i_amd.backend import ZImageBackend, ZImageConfig
+    from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params
+    from hyperscalees_t2i_amd.es_step import DistInfo, ESConfig, ESEngine
+    from hyperscalees_t2i_amd.rewards import RewardModels
+    from hyperscalees_t2i_amd.zimage import ZImageArch
+
+    cfg = ZImageConfig(synthetic_weights=True)
+    if args.small:
+        cfg.arch = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256)
+        cfg.vae_widths, cfg.width_px, cfg.height_px, cfg.num_inference_steps = (32, 32, 64, 64), 64, 64, 2
+    backend = ZImageBackend(device=str(device), cfg=cfg)
+    backend.init_and_attach_lora()
+    params, shapes = backend.collect_lora_params()
+    theta = flatten_params(params).to(device=device, dtype=torch.float32)
+    noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=4, use_antithetic=True)
+    rewards = RewardModels.build(device, tiny=args.small, synthetic=True)
+    pop = args.pop_per_gpu * world
+    es_cfg = ESConfig(pop_size=pop, sigma=1e-2, lr_scale=1e-1, egg_rank=4, use_antithetic=True, promptnorm=True,
+                      theta_max_norm=40.0, max_step_norm=0.0)
+    engine = ESEngine(backend, rewards, noiser, es_cfg, device, DistInfo(rank, world, None))
+    return backend, engine, noiser, theta, pop
+
+
 def build(args, world, rank, device):
     if args.workload == "var_d16":
         return build_var(args, world, rank, device)
+    if args.workload == "zimage":
+        return build_zimage(args, world, rank, device)
     from hyperscalees_t2i_amd.backend import SanaBackend, SanaConfig
     from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params
     from hyperscalees_t2i_amd.es_step import DistInfo, ESConfig, ESEngine
@@ -282,7 +314,27 @@ def main():
         from oracle import cpu_baseline
         cpu = cpu_baseline.run()
         log(f"cpu baseline: {cpu['value']:.4g} member-evals/s on {cpu['cores']} threads ({cpu.pop('wall_s'):.1f}s)")
-    if rank == 0 and args.workload == "var_d16":
+    if rank == 0 and args.workload == "zimage":
+        c = backend.cfg
+        line = {
+            "metric": "ES member-evals/sec Z-Image-Turbo 384px egg_rank=4 (BASELINE configs[3], pop 128 over 8 GPUs)",
+            "value": value, "unit": "member-evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init Z-Image-Turbo 6B / FLUX VAE / CLIP weights, synthetic Qwen3 prompt embeds)",
+            "config": {"workload": "tiny-arch smoke (INVALID as metric)" if args.small else "zimage_turbo_384px_es_epoch",
+                       "pop_per_gpu": args.pop_per_gpu, "pop_total": pop,
+                       "images_per_member": c.prompts_per_gen * c.batches_per_gen, "resolution_px": c.width_px,
+                       "steps": c.num_inference_steps, "guidance": c.guidance_scale, "egg_rank": 4, "lora_r": c.lora_r,
+                       "lora_alpha": c.lora_alpha, "theta_D": noiser.num_params,
+                       "parallelism": f"member-shard x{world} (S all-gather)"},
+            "roofline": roofline, "cpu_baseline": None, "phases_ms": phases, "aux_kernels": aux,
+            "model_kernels": model_kernels,
+        }
+        print(json.dumps(line), flush=True)
+        if args.aux_out:
+            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
+    elif rank == 0 and args.workload == "var_d16":
         c = backend.cfg
         line = {
             "metric": "ES member-evals/sec VAR-d16 class-conditional 256px pop=4 (BASELINE configs[0] on the GPU path)",

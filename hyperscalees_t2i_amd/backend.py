@@ -368,3 +368,157 @@ class VarBackend(ESBackend):
         label = torch.as_tensor([int(c) for c in flat_ids], device=self.device, dtype=torch.long)
         return self.es_model.generate_population(label, theta_pop, seed, guidance_scale, self.cfg.top_k,
                                                  self.cfg.top_p)
+
+
+# ---------------------------------------------------------------------------------------
+# Z-Image-Turbo backend (es_backend.py:457-678) — BASELINE configs[3]
+# ---------------------------------------------------------------------------------------
+
+
+@dataclass
+class ZImageConfig:
+    """es_backend.py:457-495 (+ build knobs).  Reference CLI defaults: unifed_es.py:408-492."""
+
+    model_name: str = "Tongyi-MAI/Z-Image-Turbo"
+    prompts_txt_path: str = "untitled.txt"
+    encoded_prompt_path: str = ""
+    auto_encode_if_missing: bool = False
+    width_px: int = 384
+    height_px: int = 384
+    num_inference_steps: int = 7
+    guidance_scale: float = 0.0
+    micro_batch: int = 1
+    prompts_per_gen: int = 4
+    batches_per_gen: int = 4
+    max_log_batches: int = 1
+    compile_transformer: bool = False
+    attention_backend: str = "flash"
+    use_gguf: bool = False
+    lora_r: int = 2
+    lora_alpha: int = 8
+    lora_dropout: float = 0.0
+    lora_target_modules: List[str] = field(default_factory=lambda: ["to_q", "to_k", "to_v", "linear", "w1", "w2", "w3"])
+    use_vae_decoder_lora: bool = False
+    dtype: str = "bfloat16"
+    # build-specific
+    arch: Any = None                         # None: the Z-Image-Turbo config (zimage.ZIMAGE_TURBO)
+    vae_widths: Tuple[int, ...] = (128, 256, 512, 512)
+    vae_chunk: int = 16
+    synthetic_prompts: int = 4               # used when encoded_prompt_path is empty
+    synthetic_prompt_lens: Tuple[int, int] = (16, 100)
+    lora_b_std: float = 0.02
+    lora_seed: int = 1234
+    weight_seed: int = 0
+    synthetic_weights: bool = False          # no Z-Image checkpoint loader: True is required (explicit opt-in)
+
+
+def synthetic_zimage_prompt_data(P: int = 4, lens: Tuple[int, int] = (16, 100), dim: int = 2560,
+                                 seed: int = 0) -> Dict[str, Any]:
+    """Same dict format as ZImageTurboES.encode_prompts (models/zImageTurbo.py:246-296): prompts and
+    prompt_embeds = a list of per-prompt [T_i, dim] bf16 tensors (T_i ~ U[lens])."""
+    g = torch.Generator().manual_seed(seed)
+    T = torch.randint(lens[0], lens[1] + 1, (P,), generator=g).tolist()
+    emb = [torch.randn(t, dim, generator=g).to(torch.bfloat16) for t in T]
+    return {"prompts": [f"synthetic prompt {i}: a detailed photo of object {i}" for i in range(P)], "prompt_embeds": emb}
+
+
+class ZImageBackend(ESBackend):
+    """es_backend.py:498-678."""
+
+    def __init__(self, device: str, cfg: ZImageConfig):
+        self.name = "zimage"
+        self.device = device
+        self.cfg = cfg
+        self.es_model = None
+        self.prompt_data = None
+        self.base_prompt_embeds = None
+        self.prompts_list = None
+        self.image_pil_mode = 0
+
+    def _load_or_encode_prompts(self):
+        """es_backend.py:515-562 (no text encoder offline: an encoded file or the synthetic set)."""
+        if self.cfg.encoded_prompt_path:
+            enc = Path(self.cfg.encoded_prompt_path)
+            if not enc.is_file():
+                raise FileNotFoundError(f"encoded_prompt_path not found and auto_encode unsupported: {enc}")
+            self.prompt_data = torch.load(enc, map_location="cpu", weights_only=True)
+        else:
+            a = self.cfg.arch
+            self.prompt_data = synthetic_zimage_prompt_data(self.cfg.synthetic_prompts, self.cfg.synthetic_prompt_lens,
+                                                            a.cap_feat_dim if a is not None else 2560)
+        self.base_prompt_embeds = self.prompt_data["prompt_embeds"]
+        self.prompts_list = self.prompt_data.get("prompts", None)
+        self._dev_prompts = [self._get_prompt_embed(p) for p in range(self._total_prompts())]
+
+    def init_and_attach_lora(self):
+        from .zimage import ZIMAGE_TURBO
+        from .zimage_pipeline import ZImageTurboES
+        c = self.cfg
+        if c.use_vae_decoder_lora:
+            raise NotImplementedError("VAE-decoder LoRA (es_backend.py:586-595) is not built")
+        self._load_or_encode_prompts()
+        self.es_model = ZImageTurboES(c.model_name, device=self.device, num_inference_steps=c.num_inference_steps,
+                                      arch=c.arch or ZIMAGE_TURBO, vae_widths=c.vae_widths, vae_chunk=c.vae_chunk,
+                                      weight_seed=c.weight_seed, synthetic_weights=c.synthetic_weights)
+        n = attach_lora(self.es_model.transformer, c.lora_r, c.lora_alpha, c.lora_target_modules)
+        if n == 0:
+            raise RuntimeError("no LoRA target module matched")
+        g = torch.Generator(device=self.device).manual_seed(c.lora_seed)
+        for m in lora_modules(self.es_model.transformer):
+            m.reset_lora(g, b_std=c.lora_b_std)
+        self.es_model.transformer.eval()
+
+    def collect_lora_params(self):
+        return get_trainable_params_and_shapes(self.es_model.transformer)
+
+    def save_lora(self, save_dir: Path) -> None:
+        """es_backend.py:611-619: the transformer adapter under save_dir/transformer."""
+        c = self.cfg
+        _save_adapter(self.es_model.transformer, Path(save_dir) / "transformer",
+                      {"peft_type": "LORA", "r": c.lora_r, "lora_alpha": c.lora_alpha, "lora_dropout": c.lora_dropout,
+                       "target_modules": list(c.lora_target_modules), "base_model_name_or_path": c.model_name,
+                       "bias": "none", "task_type": None})
+
+    def load_lora(self, save_dir: Path) -> None:
+        _load_adapter(self.es_model.transformer, Path(save_dir) / "transformer")
+
+    def _total_prompts(self) -> int:
+        pe = self.base_prompt_embeds
+        return len(pe) if isinstance(pe, list) else int(pe.shape[0])
+
+    def _get_prompt_embed(self, pid: int) -> torch.Tensor:
+        return self.base_prompt_embeds[pid].to(self.device)
+
+    def step_sampling_info(self, seed: int) -> Dict[str, Any]:
+        """es_backend.py:629-656."""
+        unique_ids = sample_indices_unique(seed=seed, total=self._total_prompts(), k=self.cfg.prompts_per_gen)
+        flat_ids = repeat_batches(unique_ids, repeats=self.cfg.batches_per_gen)
+        m = len(unique_ids)
+        name = (lambda pid: self.prompts_list[pid] if self.prompts_list is not None else f"prompt_{pid}")
+        log_batches = int(max(0, min(self.cfg.max_log_batches, self.cfg.batches_per_gen)))
+        return dict(unique_ids=unique_ids, flat_ids=flat_ids, unique_texts=[name(p) for p in unique_ids],
+                    flat_texts=[name(p) for p in flat_ids], pid_to_j={pid: j for j, pid in enumerate(unique_ids)},
+                    m=m, total_imgs_per_indiv=len(flat_ids), total_imgs_for_logging=log_batches * m,
+                    log_batches=log_batches)
+
+    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                      flat_seeds: Optional[List[int]] = None) -> List[Any]:
+        """es_backend.py:658-669: one member (the transformer's own LoRA params), PIL images."""
+        if flat_seeds is not None:
+            raise NotImplementedError("Z-Image latents are seeded per image from `seed` (per-prompt generators)")
+        c = self.cfg
+        images, _ = self.es_model.generate_one_batch([self._dev_prompts[p] for p in flat_ids], seed=seed,
+                                                     guidance_scale=guidance_scale, width_px=c.width_px,
+                                                     height_px=c.height_px, num_inference_steps=c.num_inference_steps,
+                                                     micro_batch=c.micro_batch)
+        return images
+
+    def generate_population(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                            theta_pop: torch.Tensor) -> torch.Tensor:
+        """The distinct prompts run the caption path once per member; image j keeps the latent of the
+        reference's j-th per-prompt generator (seed + j)."""
+        uniq = list(dict.fromkeys(int(f) for f in flat_ids))
+        idx = torch.tensor([uniq.index(int(f)) for f in flat_ids], device=self.device)
+        c = self.cfg
+        return self.es_model.generate_population([self._dev_prompts[p] for p in uniq], idx, theta_pop, seed,
+                                                 guidance_scale, c.width_px, c.height_px, c.num_inference_steps)

@@ -12,8 +12,8 @@ lists drive them at each config's real sizes.
   zimage_turbo_lora_shapes Z-Image-Turbo (es_backend.py:457-678, unifed_es.py:482-485: r 2, targets
                            to_q,to_k,to_v,linear,w1,w2,w3) from the published ZImageTransformer2DModel
                            config (dim 3840, 30 layers + 2 noise-refiner + 2 context-refiner blocks,
-                           FFN 10240, final_layer.linear -> 2*2*16).  UNPINNED: diffusers is absent, so
-                           the module tree cannot be walked here.
+                           FFN 10240, final_layer.linear -> 2*2*16); the restated host is zimage.py.
+                           UNPINNED: diffusers is absent, so its module tree cannot be walked here.
   infinity_lora_shapes     Infinity (es_backend.py:680-1023, unifed_es.py:469-472: r 2, targets fc1)
                            from models/Infinity.py:164-181 (depth / embed_dim / mlp_ratio per variant)
                            and the Infinity repo's FFN naming (fc1: C -> 4C).  UNPINNED: the Infinity
@@ -47,13 +47,13 @@ def var_d16_lora_shapes(r: int = 4, depth: int = 16, vocab: int = 4096) -> List[
 
 def zimage_turbo_lora_shapes(r: int = 2, dim: int = 3840, layers: int = 30, refiner_layers: int = 2,
                              ffn: int = 10240, out_ch: int = 64) -> List[Shape]:
-    """Per transformer block (noise refiner, context refiner, main stack): attention.to_q/k/v
-    (dim -> dim) and feed_forward.w1 (dim -> ffn), w2 (ffn -> dim), w3 (dim -> ffn); then
-    final_layer.linear (dim -> patch^2 * C_out).  Block order: noise_refiner, context_refiner, layers."""
-    pairs = []
+    """all_final_layer.*.linear (dim -> patch^2 * C_out) first — diffusers registers the final layer with
+    the x embedder, before the blocks — then per transformer block (noise refiner, context refiner, main
+    stack): attention.to_q/k/v (dim -> dim) and feed_forward.w1 (dim -> ffn), w2 (ffn -> dim), w3
+    (dim -> ffn).  Equal to zimage.zimage_lora_shapes() (the restated module tree, tests/test_zimage.py)."""
+    pairs = [(dim, out_ch)]
     for _ in range(2 * refiner_layers + layers):
         pairs += [(dim, dim)] * 3 + [(dim, ffn), (ffn, dim), (dim, ffn)]
-    pairs.append((dim, out_ch))
     return _lora(pairs, r)
 
 

@@ -1,0 +1,107 @@
+"""Z-Image-Turbo host (BASELINE configs[3]) on the GPU, tiny architecture: the population forward vs
+one member at a time, the bf16 build vs the fp32 restatement of the same architecture with member
+factors from theta_k (oracle/zimage_fp32.py), and a full ES epoch at egg rank 4 vs the oracle's
+epoch tail.  The architecture restates diffusers' (absent here): parity with diffusers UNPINNED."""
+import numpy as np
+import pytest
+import torch
+
+from hyperscalees_t2i_amd.backend import ZImageBackend, ZImageConfig
+from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params, unflatten_to_params
+from hyperscalees_t2i_amd.es_step import ESConfig, ESEngine
+from hyperscalees_t2i_amd.rewards import RewardModels
+from hyperscalees_t2i_amd.zimage import ZImageArch
+from oracle import eggroll_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TINY = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256)
+PX = 64     # 8 x 8 latent, 16 image tokens
+
+
+@pytest.fixture(scope="module")
+def setup(dev):
+    cfg = ZImageConfig(synthetic_weights=True, arch=TINY, vae_widths=(32, 32, 64, 64), width_px=PX, height_px=PX,
+                       num_inference_steps=3, batches_per_gen=2, synthetic_prompt_lens=(20, 70))
+    be = ZImageBackend(str(dev), cfg)
+    be.init_and_attach_lora()
+    params, shapes = be.collect_lora_params()
+    return be, params, shapes
+
+
+def test_lora_layout(setup):
+    be, params, shapes = setup
+    assert len(shapes) == 2 * (4 * 6 + 1)
+    assert tuple(shapes[0]) == (2, 256) and tuple(shapes[1]) == (64, 2)
+
+
+def test_population_forward_matches_single_member(setup, dev):
+    be, params, shapes = setup
+    theta0 = flatten_params(params).to(dev)
+    noiser = EggRollNoiser(shapes, sigma=0.05, lr_scale=0.1, rank=4, use_antithetic=True)
+    pop = 3
+    tp = noiser.perturb(theta0, noiser.sample_factors(pop, dev, seed=5), pop, 0, pop)
+    flat = be.step_sampling_info(1)["flat_ids"]
+    imgs = be.generate_population(flat, 1, 0.0, tp).float()
+    B = len(flat)
+    assert imgs.shape == (pop * B, 3, PX, PX) and torch.isfinite(imgs).all()
+    for k in range(pop):
+        unflatten_to_params(tp[k], params, shapes)
+        one, _ = be.es_model.generate_one_batch([be._dev_prompts[p] for p in flat], seed=1, width_px=PX,
+                                                height_px=PX, num_inference_steps=3, output_type="pt")
+        a, b = imgs[k * B:(k + 1) * B], one.float()
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel < 3e-2, (k, rel)
+    unflatten_to_params(theta0, params, shapes)
+    assert (imgs[:B] - imgs[B:2 * B]).abs().max().item() > 0      # members really differ
+
+
+def test_bf16_build_vs_fp32_restatement(setup, dev):
+    """Member k's velocity at every step and its decoded images vs the fp32 restatement (same weights,
+    same factors, same latents); sigma 5e-2 so the members' LoRA terms are well above bf16 noise.
+    Bounds: ~2x the first measurement on MI355X (printed)."""
+    from oracle import zimage_fp32 as Z
+    be, params, shapes = setup
+    theta0 = flatten_params(params).to(dev)
+    noiser = EggRollNoiser(shapes, sigma=5e-2, lr_scale=0.1, rank=4, use_antithetic=True)
+    pop = 2
+    tp = noiser.perturb(theta0, noiser.sample_factors(pop, dev, seed=9), pop, 0, pop)
+    info = be.step_sampling_info(2)
+    flat = info["flat_ids"]
+    uniq = list(dict.fromkeys(flat))
+    idx = torch.tensor([uniq.index(f) for f in flat], device=dev)
+    embeds = [be._dev_prompts[p] for p in uniq]
+    m = be.es_model
+    vel = []
+    hook = m.transformer.register_forward_hook(lambda _m, _i, o: vel.append(o))
+    try:
+        imgs = m.generate_population(embeds, idx, tp, 2, 0.0, PX, PX, 3).float()
+    finally:
+        hook.remove()
+    B = len(flat)
+    worst = {"vel_rel": 0.0, "img_rel": 0.0}
+    for k in range(pop):
+        v32, img32 = Z.generate_fp32(m, tp[k], embeds, idx, 2, PX, PX, 3)
+        for s in range(3):
+            v = vel[s][k * B:(k + 1) * B]
+            worst["vel_rel"] = max(worst["vel_rel"], ((v - v32[s]).norm() / v32[s].norm()).item())
+        a = imgs[k * B:(k + 1) * B]
+        worst["img_rel"] = max(worst["img_rel"], ((a - img32).norm() / img32.norm()).item())
+    print("[zimage-fp32]", worst)
+    assert worst["vel_rel"] < 0.05 and worst["img_rel"] < 0.08, worst
+
+
+def test_engine_step_rank4_matches_oracle(setup, dev):
+    be, params, shapes = setup
+    rewards = RewardModels.build(dev, tiny=True, synthetic=True)
+    theta = flatten_params(params).to(dev)
+    pop = 4
+    noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=4, use_antithetic=True)
+    eng = ESEngine(be, rewards, noiser, ESConfig(pop_size=pop, egg_rank=4, promptnorm=True, theta_max_norm=40.0), dev)
+    new, st = eng.step(theta, seed=3, guidance_scale=0.0)
+    eps = noiser.eps_from_factors(noiser.sample_factors(pop, dev, seed=3), pop).cpu().numpy()
+    ref, info = O.ref_es_tail(st["_S"].numpy(), eps, theta.cpu().numpy(), promptnorm=True, lr_scale=1e-1,
+                              sigma=1e-2, max_step_norm=0.0, theta_max_norm=40.0)
+    np.testing.assert_allclose(new.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
+    assert np.array_equal(st["_fitness"]["order"].numpy(), info["order"])
+    assert np.isfinite(st["summary/mean_reward"])
