@@ -35,6 +35,10 @@ from . import kernels as K
 FUSE_EPILOGUES = True
 
 
+# bytes of one GEMM operand the kernels can address (32-bit buffer offsets); larger X runs in row chunks
+GEMM_OPERAND_LIMIT = 1 << 31
+
+
 @dataclass
 class PopulationContext:
     theta_pop: Optional[torch.Tensor] = None  # [n_members, ld] fp32 (perturbed theta per member)
@@ -153,6 +157,8 @@ class LoRALinear(nn.Module):
         x2 = x2.contiguous()
         M = x2.shape[0]
         ctx = self.ctx
+        if M * self.in_features * 2 >= GEMM_OPERAND_LIMIT:   # the GEMMs address X with 32-bit buffer offsets
+            return self._forward_chunked(x2, shp, epi, res, gate, rows_per_group, T, shadow)
         if epi == "silu":   # silu of the bf16-rounded output, in the GEMM epilogue where it applies
             if (FUSE_EPILOGUES and ctx is not None and ctx.theta_pop is not None and self.r <= 2 and not GemmTimer.active
                     and M % ctx.n_members == 0 and (self.r == 0 or M // ctx.n_members >= 256)
@@ -220,6 +226,47 @@ class LoRALinear(nn.Module):
             y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
         return y.view(*shp[:-1], self.out_features)
 
+
+    def _forward_chunked(self, x2, shp, epi, res, gate, rows_per_group, T, shadow):
+        """forward() over row chunks whose X stays under 2 GiB: whole members per chunk on the population
+        path (theta_pop rows sliced alongside), any 256-row multiple otherwise."""
+        M, ctx = x2.shape[0], self.ctx
+        limit = max(256, (GEMM_OPERAND_LIMIT // (2 * self.in_features) - 1) // 256 * 256)
+        pop = self.r and ctx is not None and ctx.theta_pop is not None
+        if pop:
+            n = ctx.n_members
+            if M % n:
+                raise RuntimeError(f"{M} rows do not split over {n} members")
+            rpm = M // n
+            if rpm > limit:
+                raise RuntimeError(f"one member's {rpm} x {self.in_features} rows exceed the GEMM's 2 GiB operand")
+            per = limit // rpm
+            bounds = [(k0 * rpm, min(k0 + per, n) * rpm, k0, min(k0 + per, n)) for k0 in range(0, n, per)]
+        else:
+            bounds = [(r0, min(r0 + limit, M), 0, 0) for r0 in range(0, M, limit)]
+        outs = []
+        try:
+            for r0, r1, k0, k1 in bounds:
+                if pop:
+                    sub = PopulationContext()
+                    sub.theta_pop, sub.n_members, sub.T_ws, sub.multi_ws = ctx.theta_pop[k0:k1], k1 - k0, ctx.T_ws, ctx.multi_ws
+                    self.ctx = sub
+                g = None
+                if gate is not None:
+                    if r0 % rows_per_group:
+                        raise RuntimeError("row chunk does not start on a gate group boundary")
+                    g = gate[r0 // rows_per_group:]
+                rr = res.view(M, self.out_features)[r0:r1] if res is not None else None
+                sh = shadow.view(M, self.out_features)[r0:r1] if shadow is not None else None
+                outs.append(self.forward(x2[r0:r1], epi=epi, res=rr, gate=g, rows_per_group=rows_per_group,
+                                         T=T[r0:r1] if T is not None else None, shadow=sh))
+                if pop:
+                    ctx.T_ws, ctx.multi_ws = sub.T_ws, sub.multi_ws
+        finally:
+            self.ctx = ctx
+        if res is not None and epi not in (None, "silu"):
+            return res
+        return torch.cat(outs).view(*shp[:-1], self.out_features)
 
     def _weight32(self) -> torch.Tensor:
         key = (self.weight._version, self.weight.data_ptr())

@@ -59,7 +59,7 @@ def test_population_forward_matches_single_member(setup, dev):
 def test_bf16_build_vs_fp32_restatement(setup, dev):
     """Member k's velocity at every step and its decoded images vs the fp32 restatement (same weights,
     same factors, same latents); sigma 5e-2 so the members' LoRA terms are well above bf16 noise.
-    Bounds: ~2x the first measurement on MI355X (printed)."""
+    Bounds: ~2x the measurement on MI355X (printed; r04u: velocity 0.68 %, image 1.05 %)."""
     from oracle import zimage_fp32 as Z
     be, params, shapes = setup
     theta0 = flatten_params(params).to(dev)
@@ -88,7 +88,7 @@ def test_bf16_build_vs_fp32_restatement(setup, dev):
         a = imgs[k * B:(k + 1) * B]
         worst["img_rel"] = max(worst["img_rel"], ((a - img32).norm() / img32.norm()).item())
     print("[zimage-fp32]", worst)
-    assert worst["vel_rel"] < 0.05 and worst["img_rel"] < 0.08, worst
+    assert worst["vel_rel"] < 0.015 and worst["img_rel"] < 0.02, worst   # measured 0.0068 / 0.0105
 
 
 def test_engine_step_rank4_matches_oracle(setup, dev):
@@ -105,3 +105,30 @@ def test_engine_step_rank4_matches_oracle(setup, dev):
     np.testing.assert_allclose(new.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
     assert np.array_equal(st["_fitness"]["order"].numpy(), info["order"])
     assert np.isfinite(st["summary/mean_reward"])
+
+
+def test_lora_linear_row_chunks_match_one_launch(dev, monkeypatch):
+    """X beyond the GEMMs' 2 GiB operand runs in whole-member row chunks (LoRALinear._forward_chunked):
+    with the limit lowered, the chunked population forward equals the one-launch forward, for the plain,
+    SiLU-epilogue and gated-residual forms."""
+    from hyperscalees_t2i_amd import lora
+    m = lora.LoRALinear(256, 320, bias=True, r=2, alpha=8.0).to(dev)
+    g = torch.Generator(device=dev).manual_seed(4)
+    with torch.no_grad():
+        m.weight.copy_(torch.randn(m.weight.shape, generator=g, device=dev) * 0.06)
+        m.bias.copy_(torch.randn(320, generator=g, device=dev) * 0.1)
+    lora.bind_theta_layout(m)
+    n, rpm = 4, 512
+    ctx = lora.PopulationContext()
+    ctx.theta_pop = torch.randn(n, 2 * 256 + 320 * 2, generator=g, device=dev) * 0.1
+    ctx.n_members = n
+    lora.set_population(m, ctx)
+    x = torch.randn(n * rpm, 256, generator=g, device=dev).bfloat16()
+    gate = torch.randn(n * rpm // 256, 320, generator=g, device=dev).bfloat16()
+    res0 = torch.randn(n * rpm, 320, generator=g, device=dev).bfloat16()
+    want = [m(x), m(x, epi="silu"), m(x, epi="gated", res=res0.clone(), gate=gate, rows_per_group=256)]
+    monkeypatch.setattr(lora, "GEMM_OPERAND_LIMIT", 2 * 256 * (2 * rpm))     # one member per chunk
+    got = [m(x), m(x, epi="silu"), m(x, epi="gated", res=res0.clone(), gate=gate, rows_per_group=256)]
+    lora.set_population(m, None)
+    for a, b in zip(got, want):
+        assert torch.allclose(a.float(), b.float(), rtol=1e-2, atol=1e-2), (a.float() - b.float()).abs().max()
