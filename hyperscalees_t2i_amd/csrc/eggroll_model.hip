@@ -1340,6 +1340,71 @@ extern "C" int eggroll_rownorm_ex(const void* x, int32_t x_f32, int64_t rows, in
     return EGGROLL_OK;
 }
 
+// ------------------------------------------------------------------------------------
+// Per-head RMS norm + rotary position embedding, in place (the Z-Image q / k, head dim 128):
+//   y = x * rsqrt(mean_head(x^2) + eps) * w;   (y[2p], y[2p+1]) <- (y0 c - y1 s, y0 s + y1 c)
+// with c, s = cos / sin[row % tab_rows][p] (fp32 tables, one row per token position of one member; the
+// member copies of a population batch repeat them).  16 lanes per (token, head), 8 consecutive values =
+// 4 rotation pairs per lane, fp32 throughout and one bf16 rounding.  Replaces the norm pass and torch's
+// fp32 rotation (~10 full passes over q and k per attention).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_qk_norm_rope(unsigned short* __restrict__ x, int64_t ldx, int heads,
+                                                      float eps, const unsigned short* __restrict__ w,
+                                                      const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                      int64_t tab_rows, int64_t segs) {
+    const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int l = threadIdx.x & 15;
+    const bool live = seg < segs;
+    const int64_t row = live ? seg / heads : 0;
+    const int h = live ? (int)(seg - row * heads) : 0;
+    unsigned short* p = x + row * ldx + h * 128 + l * 8;
+    u16x8m v = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+    if (live) v = *reinterpret_cast<const u16x8m*>(p);
+    float f[8], ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        f[i] = b2f(v[i]);
+        ss += f[i] * f[i];
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);   // within the 16-lane segment
+    const float r = rsqrtf(ss / 128.f + eps);
+    if (!live) return;
+    const u16x8m wv = *reinterpret_cast<const u16x8m*>(w + l * 8);
+    const int64_t tr = row % tab_rows;
+    const float4 c4 = *reinterpret_cast<const float4*>(cosb + tr * 64 + l * 4);
+    const float4 s4 = *reinterpret_cast<const float4*>(sinb + tr * 64 + l * 4);
+    const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+    u16x8m o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float y0 = f[2 * j] * r * b2f(wv[2 * j]), y1 = f[2 * j + 1] * r * b2f(wv[2 * j + 1]);
+        o[2 * j] = f2b(y0 * cs[j] - y1 * sn[j]);
+        o[2 * j + 1] = f2b(y0 * sn[j] + y1 * cs[j]);
+    }
+    *reinterpret_cast<u16x8m*>(p) = o;
+}
+
+extern "C" int eggroll_qk_norm_rope(void* x, int64_t ldx, int64_t rows, int32_t heads, int32_t head_dim, float eps,
+                                    const void* w, const float* cos_tab, const float* sin_tab, int64_t tab_rows,
+                                    void* stream) {
+    EGG_CHECK_ARG(head_dim == 128, "qk_norm_rope: head_dim must be 128 (got %d)", head_dim);
+    EGG_CHECK_ARG(rows >= 0 && heads > 0 && ldx >= (int64_t)heads * 128 && ldx % 8 == 0 && tab_rows > 0,
+                  "qk_norm_rope: bad sizes / strides");
+    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)cos_tab & 15) == 0 &&
+                      ((uintptr_t)sin_tab & 15) == 0,
+                  "qk_norm_rope: pointers must be 16-byte aligned");
+    if (rows == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(x && w && cos_tab && sin_tab, "qk_norm_rope: NULL pointer");
+    const int64_t segs = rows * heads;
+    EGG_CHECK_ARG(segs < (1ll << 31) / 16, "qk_norm_rope: too many rows");
+    hipLaunchKernelGGL(k_qk_norm_rope, dim3((unsigned)((segs * 16 + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       (unsigned short*)x, ldx, (int)heads, eps, (const unsigned short*)w, cos_tab, sin_tab, tab_rows,
+                       segs);
+    EGG_CHECK_LAUNCH("qk_norm_rope");
+    return EGGROLL_OK;
+}
+
 extern "C" int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps, int32_t layer, const void* w,
                                const void* b, const void* mscale, const void* mshift, int64_t mstride,
                                int64_t rows_per_group, int32_t act, const void* res, void* out, void* stream) {

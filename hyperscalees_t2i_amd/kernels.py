@@ -597,6 +597,24 @@ def rownorm(x: torch.Tensor, eps: float, layer: bool = False, w: Optional[torch.
     return out
 
 
+def qk_norm_rope_(x: torch.Tensor, w: torch.Tensor, eps: float, cos: torch.Tensor, sin: torch.Tensor,
+                  heads: int) -> torch.Tensor:
+    """In place on x [rows, >= heads*128] bf16 (row stride x.stride(0)): per-head RMS norm * w [128], then
+    the rotation of adjacent pairs by cos / sin [tab_rows, 64] fp32 (table row = row % tab_rows) —
+    eggroll_qk_norm_rope (the Z-Image q / k path)."""
+    _dev(x, "qk_norm_rope(x)", torch.bfloat16, contiguous=False)
+    _dev(w, "qk_norm_rope(w)", torch.bfloat16)
+    _dev(cos, "qk_norm_rope(cos)", torch.float32)
+    _dev(sin, "qk_norm_rope(sin)", torch.float32)
+    if x.dim() != 2 or x.stride(1) != 1 or cos.shape != sin.shape or cos.shape[-1] != 64 or w.numel() != 128:
+        raise ValueError(f"qk_norm_rope: x {tuple(x.shape)}, w {tuple(w.shape)}, tables {tuple(cos.shape)}")
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_qk_norm_rope", x.data_ptr(), x.stride(0), x.shape[0], int(heads), 128, float(eps), w.data_ptr(),
+              cos.data_ptr(), sin.data_ptr(), cos.numel() // 64, _stream(x.device))
+    OpTimer.end(e0, "qk_norm_rope", 4.0 * x.shape[0] * heads * 128, f"rows{x.shape[0]}")
+    return x
+
+
 def gated_residual_(x: torch.Tensor, y: torch.Tensor, gate: torch.Tensor, rows_per_group: int) -> torch.Tensor:
     """x += gate[g] * y in place (g = row // rows_per_group); gate a [groups, C] view."""
     _dev(x, "gated_residual(x)", torch.bfloat16)

@@ -14,9 +14,9 @@ diffusers numerics and the exact module tree are UNPINNED (no diffusers, no chec
 shapes, FLOPs, token counts and the LoRA target set follow the published config, which is what the
 throughput of configs[3] depends on.
 
-Every linear runs on libeggroll's population GEMM (LoRA'd or plain); q/k norms and every RMSNorm /
-modulation / gated residual on `eggroll_rownorm`; attention on SDPA; the FFN's silu(w1 x) on the
-GEMM's SiLU epilogue.
+Every linear runs on libeggroll's population GEMM (LoRA'd or plain); the q/k norm + RoPE on
+`eggroll_qk_norm_rope` (one in-place pass per tensor); every RMSNorm / modulation / gated residual on
+`eggroll_rownorm`; attention on SDPA; the FFN's silu(w1 x) on the GEMM's SiLU epilogue.
 """
 from __future__ import annotations
 
@@ -104,16 +104,24 @@ class ZAttention(nn.Module):
         self.norm_q = RMSNorm(a.head_dim, a.norm_eps)
         self.norm_k = RMSNorm(a.head_dim, a.norm_eps)
         self.to_out = nn.ModuleList([LoRALinear(a.dim, a.dim, bias=False, lora=False)])
+        self.use_kernel = True   # eggroll_qk_norm_rope; False: rownorm + torch rotation (A/B, tests)
 
     def forward(self, x, cos, sin, n_rep: int, key_bias: Optional[torch.Tensor]):
         """x [B, S, dim]; key_bias [B, 1, 1, S] additive (batch padding) or None."""
         B, S, D = x.shape
         Tq, Tk, Tv = lora.shared_projection([self.to_q, self.to_k, self.to_v], x)   # X read once for 3 LoRAs
-        q = K.rownorm(self.to_q(x, T=Tq).view(-1, self.hd), self.norm_q.eps, w=self.norm_q.weight)
-        k = K.rownorm(self.to_k(x, T=Tk).view(-1, self.hd), self.norm_k.eps, w=self.norm_k.weight)
+        q, k = self.to_q(x, T=Tq), self.to_k(x, T=Tk)
+        if self.use_kernel and self.hd == 128:   # norm + RoPE in one in-place pass per tensor
+            c2, s2 = cos.reshape(-1, cos.shape[-1]), sin.reshape(-1, sin.shape[-1])
+            K.qk_norm_rope_(q.view(-1, D), self.norm_q.weight, self.norm_q.eps, c2, s2, self.heads)
+            K.qk_norm_rope_(k.view(-1, D), self.norm_k.weight, self.norm_k.eps, c2, s2, self.heads)
+            q, k = q.view(B, S, self.heads, self.hd), k.view(B, S, self.heads, self.hd)
+        else:
+            q = K.rownorm(q.view(-1, self.hd), self.norm_q.eps, w=self.norm_q.weight)
+            k = K.rownorm(k.view(-1, self.hd), self.norm_k.eps, w=self.norm_k.weight)
+            q = apply_rope(q.view(B, S, self.heads, self.hd), cos, sin, n_rep)
+            k = apply_rope(k.view(B, S, self.heads, self.hd), cos, sin, n_rep)
         v = self.to_v(x, T=Tv).view(B, S, self.heads, self.hd)
-        q = apply_rope(q.view(B, S, self.heads, self.hd), cos, sin, n_rep)
-        k = apply_rope(k.view(B, S, self.heads, self.hd), cos, sin, n_rep)
         o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
                                            attn_mask=key_bias, scale=self.hd ** -0.5)
         return self.to_out[0](o.transpose(1, 2).reshape(B, S, D))

@@ -264,6 +264,12 @@ int eggroll_rownorm(const void* x, int64_t rows, int64_t C, float eps, int32_t l
 /* x[r, :] += gate[r / rows_per_group, :] * y[r, :]  (bf16, in place; gate rows gstride apart). */
 int eggroll_gated_residual(void* x, const void* y, const void* gate, int64_t gstride, int64_t rows,
                            int64_t C, int64_t rows_per_group, void* stream);
+/* Per-head RMS norm + rotary embedding of x [rows, >= heads*128] bf16 (row stride ldx), in place:
+ * y = x * rsqrt(mean_head(x^2) + eps) * w[128], then every adjacent pair (2p, 2p+1) of a head rotated
+ * by cos / sin[row % tab_rows][p] (fp32 tables [tab_rows][64]); fp32 math, one bf16 rounding.  The
+ * Z-Image q / k path (diffusers ZImageTransformer2DModel: norm_q / norm_k then the 3-axis RoPE).    */
+int eggroll_qk_norm_rope(void* x, int64_t ldx, int64_t rows, int32_t heads, int32_t head_dim, float eps,
+                         const void* w, const float* cos_tab, const float* sin_tab, int64_t tab_rows, void* stream);
 /* The same row normalisation with dtype options: x_f32 = 1: fp32 input x (the fp32 residual stream of
  * the Sana blocks); mod_f32 = 1: fp32 modulation vectors (the fp32 AdaLN modulation); res_f32 = 1: fp32
  * res; out_f32 = 1: fp32 output (the DC-AE fp32 residual stream, out = norm(x)·w + b + res, may alias

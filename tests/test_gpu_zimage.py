@@ -132,3 +132,23 @@ def test_lora_linear_row_chunks_match_one_launch(dev, monkeypatch):
     lora.set_population(m, None)
     for a, b in zip(got, want):
         assert torch.allclose(a.float(), b.float(), rtol=1e-2, atol=1e-2), (a.float() - b.float()).abs().max()
+
+
+@pytest.mark.parametrize("rows,heads,tab", [(4 * 96, 2, 96), (777, 30, 777), (64, 3, 16)])
+def test_qk_norm_rope_vs_torch(dev, rows, heads, tab):
+    """eggroll_qk_norm_rope vs the fp32 torch form (RMS norm * w, then the complex rotation of adjacent
+    pairs with the table row = row % tab_rows): within one bf16 rounding of the output."""
+    from hyperscalees_t2i_amd import kernels as K
+    from oracle.zimage_fp32 import rope
+    g = torch.Generator(device=dev).manual_seed(rows)
+    x = (torch.randn(rows, heads * 128, generator=g, device=dev) * 3).bfloat16()
+    w = (1 + 0.1 * torch.randn(128, generator=g, device=dev)).bfloat16()
+    ang = torch.rand(tab, 64, generator=g, device=dev) * 6.3
+    cos, sin = torch.cos(ang).contiguous(), torch.sin(ang).contiguous()
+    xf = x.float().view(rows, heads, 128)
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    ti = torch.arange(rows, device=dev) % tab
+    ref = rope(y[None], cos[ti][None], sin[ti][None])[0].reshape(rows, -1)
+    got = K.qk_norm_rope_(x.clone(), w, 1e-5, cos, sin, heads).float()
+    err = (got - ref).abs()
+    assert (err <= 2 ** -8 * ref.abs() + 1e-6).all(), float(err.max())
