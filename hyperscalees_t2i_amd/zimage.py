@@ -268,45 +268,57 @@ class ZImageTransformer2DModel(nn.Module):
     def forward(self, lat: torch.Tensor, t: torch.Tensor, cap_feats: torch.Tensor, cap_lens: torch.Tensor,
                 enc_index: torch.Tensor, n_rep: int = 1) -> torch.Tensor:
         """lat [n_rep * b, C, H, W] (member-major); t [1] model time in [0, 1] (the step's, shared);
-        cap_feats [n_rep * U, Lc, cap_feat_dim] (member-major copies of the U distinct captions, padded
-        to Lc); cap_lens [U] valid (padded-to-32) caption lengths; enc_index [b] image -> caption row.
-        Returns the velocity [n_rep * b, C, H, W] (fp32)."""
+        cap_feats [n_rep * U, Lc, cap_feat_dim] (member-major copies of the U distinct captions, zero
+        beyond each); cap_lens [U] the captions' own token counts; enc_index [b] image -> caption.
+        Returns the velocity [n_rep * b, C, H, W] (fp32).
+
+        A caption of T tokens is padded to L = T rounded up to seq_multiple with cap_pad_token, and an
+        image attends to exactly its N image tokens + its caption's L tokens.  Images are processed in
+        groups of equal L (the context refiner per caption group, the main stack per image group), so
+        no attention needs a key-padding mask — with one, SDPA leaves the flash kernel for one at half
+        its speed.  The groups' images stay member-major, as the population GEMM needs."""
         a = self.config
         Bt, C, H, W = lat.shape
         b, U, Lc = Bt // n_rep, cap_lens.numel(), cap_feats.shape[1]
         hp, wp = H // a.patch, W // a.patch
-        N = hp * wp
+        N, D, dev = hp * wp, a.dim, lat.device
+        m = a.seq_multiple
+        real = [int(v) for v in cap_lens.tolist()]
+        padl = [-(-r // m) * m for r in real]
+        if max(padl) > Lc:
+            raise ValueError(f"cap_feats holds {Lc} tokens, a caption needs {max(padl)}")
+        ei = [int(v) for v in enc_index.tolist()]
         t_emb = self.t_embedder(t * a.t_scale)                                   # [1, 256] fp32
         x = self.all_x_embedder[f"{a.patch}-1"](self.patchify(lat.to(torch.bfloat16)).contiguous())   # [Bt, N, D]
         cap = self.cap_embedder[1](K.rownorm(cap_feats.to(torch.bfloat16).contiguous(), self.cap_embedder[0].eps,
                                              w=self.cap_embedder[0].weight))     # [n_rep * U, Lc, D]
-        # caption padding beyond a caption's own length: the pad token, masked out as a key
-        valid = torch.arange(Lc, device=lat.device)[None, :] < cap_lens[:, None]             # [U, Lc]
-        cap = torch.where(valid.repeat(n_rep, 1)[..., None], cap, self.cap_pad_token.view(1, 1, -1)).contiguous()
-        img_pos, cap_pos = self.positions(cap_lens, Lc, hp, wp)
+        # tokens past a caption's own length up to its padded length: cap_pad_token
+        valid = torch.arange(Lc, device=dev)[None, :] < cap_lens.to(dev)[:, None]            # [U, Lc]
+        cap = torch.where(valid.repeat(n_rep, 1)[..., None], cap, self.cap_pad_token.view(1, 1, -1))
+        img_pos, cap_pos = self.positions(torch.tensor(padl, device=dev), Lc, hp, wp)
         ci, si = rope_tables(a, img_pos[enc_index])                              # [b, N, 64]
-        cc, sc = rope_tables(a, cap_pos.expand(U, Lc, 3))                        # [U, Lc, 64]
-        ragged = bool((cap_lens < Lc).any())
-        cap_bias = None
-        if ragged:
-            cap_bias = torch.zeros(U, Lc, device=lat.device, dtype=torch.bfloat16).masked_fill(~valid, float("-inf"))
         for blk in self.noise_refiner:
             blk(x, ci, si, n_rep, None, t_emb)
-        kb = cap_bias.repeat(n_rep, 1)[:, None, None, :] if ragged else None
-        for blk in self.context_refiner:
-            blk(cap, cc, sc, n_rep, kb)
-        # the single stream: [image tokens | caption tokens] per image
-        rows = (torch.arange(n_rep, device=lat.device)[:, None] * U + enc_index[None, :]).reshape(-1)
-        u = torch.cat((x, cap.index_select(0, rows)), 1).contiguous()           # [Bt, N + Lc, D]
-        cu, su = torch.cat((ci, cc[enc_index]), 1), torch.cat((si, sc[enc_index]), 1)
-        ub = None
-        if ragged:
-            ub = torch.cat((torch.zeros(b, N, device=lat.device, dtype=torch.bfloat16), cap_bias[enc_index]), 1)
-            ub = ub.repeat(n_rep, 1)[:, None, None, :]
-        for blk in self.layers:
-            blk(u, cu, su, n_rep, ub, t_emb)
-        out = self.all_final_layer[f"{a.patch}-1"](u[:, :N], t_emb)              # [Bt, N, p*p*C]
-        return self.unpatchify(out.float(), H, W)
+        fl = self.all_final_layer[f"{a.patch}-1"]
+        out = torch.empty(n_rep, b, N, a.patch_dim, device=dev, dtype=torch.bfloat16)
+        x4, cap4 = x.view(n_rep, b, N, D), cap.view(n_rep, U, Lc, D)
+        for L in sorted(set(padl)):
+            ug = [u for u in range(U) if padl[u] == L]
+            ig = [j for j in range(b) if padl[ei[j]] == L]
+            if not ig:
+                continue
+            cc, sc = rope_tables(a, cap_pos[:L].expand(len(ug), L, 3))        # [Ug, L, 64]
+            cg = cap4[:, ug, :L].reshape(n_rep * len(ug), L, D).contiguous()
+            for blk in self.context_refiner:
+                blk(cg, cc, sc, n_rep, None)
+            loc = [ug.index(ei[j]) for j in ig]
+            u = torch.cat((x4[:, ig], cg.view(n_rep, len(ug), L, D)[:, loc]), 2).reshape(n_rep * len(ig), N + L, D)
+            cu, su = torch.cat((ci[ig], cc[loc]), 1), torch.cat((si[ig], sc[loc]), 1)
+            for blk in self.layers:
+                blk(u, cu, su, n_rep, None, t_emb)
+            og = fl(u.view(n_rep, len(ig), N + L, D)[:, :, :N].reshape(n_rep * len(ig), N, D), t_emb)
+            out[:, ig] = og.view(n_rep, len(ig), N, a.patch_dim)
+        return self.unpatchify(out.view(Bt, N, a.patch_dim).float(), H, W)
 
 
 def zimage_lora_shapes(a: ZImageArch = ZIMAGE_TURBO, r: int = 2, alpha: float = 8.0,

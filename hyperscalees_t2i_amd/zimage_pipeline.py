@@ -73,15 +73,16 @@ class ZImageTurboES:
         return torch.cat(out)
 
     def _captions(self, embeds: Sequence[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Distinct prompt embeddings -> [U, Lc, cap_dim] bf16 (zero beyond each caption) and the per-caption
-        lengths padded to a multiple of seq_multiple (the pad tokens are the model's cap_pad_token)."""
+        """Distinct prompt embeddings -> [U, Lc, cap_dim] bf16 (zero beyond each caption; Lc = the longest
+        caption rounded up to seq_multiple) and the captions' own token counts [U] (the model pads each
+        to a multiple of seq_multiple with its cap_pad_token)."""
         m = self.arch.seq_multiple
-        lens = [-(-int(e.shape[0]) // m) * m for e in embeds]
-        Lc = max(lens)
+        real = [int(e.shape[0]) for e in embeds]
+        Lc = max(-(-r // m) * m for r in real)
         cap = torch.zeros(len(embeds), Lc, self.arch.cap_feat_dim, device=self.device, dtype=torch.bfloat16)
         for u, e in enumerate(embeds):
             cap[u, :e.shape[0]] = e.to(self.device, torch.bfloat16)
-        return cap, torch.tensor(lens, device=self.device)
+        return cap, torch.tensor(real, device=self.device)
 
     @torch.no_grad()
     def _sample(self, lat: torch.Tensor, cap: torch.Tensor, cap_lens: torch.Tensor, prompt_index: torch.Tensor,

@@ -72,18 +72,20 @@ def transformer_fp32(tr, lat, t, cap_feats, cap_lens, enc_index, theta_k, record
     U, Lc = cap_lens.numel(), cap_feats.shape[1]
     hp, wp = H // a.patch, W // a.patch
     N = hp * wp
+    padl = (cap_lens + a.seq_multiple - 1) // a.seq_multiple * a.seq_multiple   # each caption's padded length
     te = tr.t_embedder
     t_emb = F.linear(F.silu(F.linear(timestep_embedding(t * a.t_scale), _w(te.mlp[0].weight), _w(te.mlp[0].bias))),
                      _w(te.mlp[2].weight), _w(te.mlp[2].bias))
     x = L(tr.all_x_embedder[f"{a.patch}-1"])(tr.patchify(lat.to(f32)))
     ce = tr.cap_embedder
     cap = L(ce[1])(rms(cap_feats.to(f32), _w(ce[0].weight), ce[0].eps))
-    valid = torch.arange(Lc, device=lat.device)[None, :] < cap_lens[:, None]
-    cap = torch.where(valid[..., None], cap, _w(tr.cap_pad_token).view(1, 1, -1))
-    img_pos, cap_pos = tr.positions(cap_lens, Lc, hp, wp)
+    tok = torch.arange(Lc, device=lat.device)[None, :]
+    cap = torch.where((tok < cap_lens[:, None])[..., None], cap, _w(tr.cap_pad_token).view(1, 1, -1))
+    img_pos, cap_pos = tr.positions(padl, Lc, hp, wp)
     ci, si = rope_tables(a, img_pos[enc_index])
     cc, sc = rope_tables(a, cap_pos.expand(U, Lc, 3))
-    cap_bias = torch.zeros(U, Lc, device=lat.device).masked_fill(~valid, float("-inf"))
+    # one batch with a key mask past each caption's padded length (the build groups images instead)
+    cap_bias = torch.zeros(U, Lc, device=lat.device).masked_fill(tok >= padl[:, None], float("-inf"))
     for blk in tr.noise_refiner:
         x = block(blk, x, ci, si, None, t_emb, theta_k, record)
     for blk in tr.context_refiner:
