@@ -65,6 +65,17 @@ class CLIPVisionTower:
                 w2=L.mlp.fc2.weight.detach(), b2=L.mlp.fc2.bias.detach()))
 
     @staticmethod
+    def _lin(x, w, b, ours: bool):
+        """x W^T + b: libeggroll's 8-phase GEMM (256x256 tile) where it measured faster than hipBLASLt —
+        CLIP-H/14's q/k/v and fc1 at 128 x 257 rows, 1252 vs 1196 and 1246 vs 1169 TF/s
+        (tools/dcae_gemm_probe.py ... clip, profiles/r05a_clip_gemm_hipblaslt_vs_8phase.json) — else F.linear."""
+        if ours and x.dtype == torch.bfloat16 and w.shape[1] % 64 == 0:
+            from . import kernels as K
+            x2 = x.reshape(-1, x.shape[-1]).contiguous()
+            return K.lora_linear_pop(x2, w, b, None, 0, 0, 0, 0.0, x2.shape[0], kernel=8).view(*x.shape[:-1], w.shape[0])
+        return F.linear(x, w, b)
+
+    @staticmethod
     def _ln(mod, x):
         return F.layer_norm(x, mod.normalized_shape, mod.weight, mod.bias, mod.eps)
 
@@ -97,11 +108,12 @@ class CLIPVisionTower:
         fused = self.fused_residual_ln and dt == torch.bfloat16 and C % 8 == 0
         ln_k = lambda mod, h_, add: K.resid_layernorm_(h_, add, mod.weight, mod.bias, mod.eps)  # noqa: E731
         y_next = ln_k(self.layers[0]["ln1"], h, None) if fused else None
+        big = fused and C >= 1024 and n * T >= 16384      # the CLIP-H/14 tower at the epoch's batch
         for i, L in enumerate(self.layers):
             y = y_next if fused else self._ln32(L["ln1"], h, dt)
             last_i = i == last
             if kernel:
-                qkv = F.linear(y, L["wqkv"], L["bqkv"]).view(n * T, 3 * C)
+                qkv = self._lin(y, L["wqkv"], L["bqkv"], big).view(n * T, 3 * C)
                 qv = qkv[::T] if last_i else qkv
                 o = K.cross_attention(qv, qkv[:, C:], qkv[:, 2 * C:], n, 1 if last_i else T, H, hd, T, L["scale"])
                 o = o.view(n, -1, C)
@@ -115,7 +127,7 @@ class CLIPVisionTower:
             if fused:        # h += out_proj(o); y = LN2(h)  (h: [n, T, C], or the [CLS] rows [n, 1, C] strided)
                 h2 = h.view(n * T, C) if not last_i else h[:, 0]
                 y = ln_k(L["ln2"], h2, F.linear(o.reshape(-1, C), L["wo"], L["bo"]))
-                m = F.linear(self.act(F.linear(y, L["w1"], L["b1"])), L["w2"], L["b2"])
+                m = F.linear(self.act(self._lin(y, L["w1"], L["b1"], big and not last_i)), L["w2"], L["b2"])
                 if not last_i:   # h += mlp(y); the next layer's LN1 in the same pass
                     y_next = ln_k(self.layers[i + 1]["ln1"], h2, m)
                 else:

@@ -2,7 +2,7 @@
 DC-AE decoder's 1x1-conv shapes and the Sana FFN point conv, per vae_chunk (images per decoder call):
 EfficientViT stages at 32^2 / 64^2 (1024 ch) and 128^2 (512 ch): qkv, attention out, GLU inverted and
 point convs.  Interleaved rounds in one process; bf16 outputs compared (max |diff| / max |y|).
-usage: python tools/dcae_gemm_probe.py [rounds] [out.json] [sana]"""
+usage: python tools/dcae_gemm_probe.py [rounds] [out.json] [sana|clip]"""
 import json
 import statistics
 import sys
@@ -20,6 +20,14 @@ dev = torch.device("cuda:0")
 
 
 def shapes():
+    if len(sys.argv) > 3 and sys.argv[3] == "clip":   # the reward towers' linears, 128 images per epoch
+        M = 128 * 257                                 # CLIP-H/14 vision: 257 tokens, width 1280, MLP 5120
+        yield from (("cliph_qkv", M, 3840, 1280), ("cliph_out", M, 1280, 1280), ("cliph_fc1", M, 5120, 1280),
+                    ("cliph_fc2", M, 1280, 5120))
+        M = 128 * 50                                  # CLIP-B/32 vision: 50 tokens, width 768, MLP 3072
+        yield from (("clipb_qkv", M, 2304, 768), ("clipb_out", M, 768, 768), ("clipb_fc1", M, 3072, 768),
+                    ("clipb_fc2", M, 768, 3072))
+        return
     if len(sys.argv) > 3 and sys.argv[3] == "sana":   # the Sana linears (no LoRA term: the plain GEMM)
         yield from (("sana_attn", 131072, 2240, 2240), ("sana_ff_inv", 131072, 11200, 2240),
                     ("sana_ff_point_5632", 131072, 2240, 5632), ("sana_attn2_kv", 9600, 2240, 2240))
