@@ -325,6 +325,7 @@ class DCAEDecoder(nn.Module):
         # (4 stages) vs 0.0112 (all 6), decode +3 % vs +20 % (tools/dcae_stream_probe.py,
         # profiles/r04_dcae_fp32_stages_probe.json); 0: the round-3 all-bf16 decoder (A/B)
         self.fp32_stages = min(4, len(widths))
+        self.hi_res_chunk = 8     # images per call of the two high-resolution stages (see _tail)
         self.conv_in = Conv3x3(latent_channels, widths[-1])
         self.in_repeats = widths[-1] // latent_channels
         stages = []
@@ -361,18 +362,39 @@ class DCAEDecoder(nn.Module):
             if isinstance(m, ResBlock):
                 m.refresh_packed_weights()
 
+    def _head(self, x):
+        if x.shape[-1] == 128 and self.conv_out.weight.shape[0] == 3:  # norm_out + ReLU + conv_out in one pass
+            no = self.norm_out
+            return nchw(K.dcae_head(x, no.eps, no.weight, no.bias, self.conv_out.weight, self.conv_out.bias))
+        return nchw(self.conv_out(self.norm_out(x, act="relu")))
+
+    def _tail(self, x16, first: int):
+        """Stages first.. (bf16 stream) + head; the two high-resolution stages in chunks of hi_res_chunk
+        images (their kernels index one tensor with 32 bits: 8 images of 1024^2 x 128 is the largest)."""
+        hi = len(self.stages) - 2
+        for st in self.stages[first:hi]:
+            x16 = st(x16)
+        B, c = x16.shape[0], self.hi_res_chunk
+        if B <= c:
+            for st in self.stages[max(first, hi):]:
+                x16 = st(x16)
+            return self._head(x16)
+        outs = []
+        for s0 in range(0, B, c):
+            xc = x16[s0:s0 + c]
+            for st in self.stages[max(first, hi):]:
+                xc = st(xc)
+            outs.append(self._head(xc))
+        return torch.cat(outs)
+
     def forward(self, z):  # z [B, 32, h, w] -> image [B, 3, 32h, 32w] (channels-last) in ~[-1, 1]
+        """The low-resolution stages run on the whole batch (a call may carry more images than one chunk:
+        their GEMMs / convs fill the chip better), the high-resolution stages chunk by hi_res_chunk."""
         if self.fp32_stages > 0:
             return self.forward_f32(z)
         zt = nhwc(z.to(torch.bfloat16)).contiguous()
         x = self.conv_in(zt) + zt.repeat_interleave(self.in_repeats, dim=-1)
-        for st in self.stages:
-            x = st(x)
-        if x.shape[-1] == 128 and self.conv_out.weight.shape[0] == 3:  # norm_out + ReLU + conv_out in one pass
-            no = self.norm_out
-            return nchw(K.dcae_head(x, no.eps, no.weight, no.bias, self.conv_out.weight, self.conv_out.bias))
-        x = self.norm_out(x, act="relu")
-        return nchw(self.conv_out(x))
+        return self._tail(x, 0)
 
     def forward_f32(self, z):
         """The decoder on an fp32 residual stream: every block updates the fp32 stream x32
@@ -384,13 +406,13 @@ class DCAEDecoder(nn.Module):
         zt = nhwc(z.to(torch.bfloat16)).contiguous()
         x32 = self.conv_in(zt).float() + nhwc(z.float()).repeat_interleave(self.in_repeats, dim=-1)
         x16 = x32.to(torch.bfloat16)
-        for i, st in enumerate(self.stages):
-            if i < self.fp32_stages:
+        n32 = min(self.fp32_stages, len(self.stages) - 2)
+        for st in self.stages[:n32]:
+            for blk in st:
+                x32, x16 = blk.forward_f32(x32, x16)
+        if self.fp32_stages > n32:   # fp32 stream into the high-resolution stages: unchunked (A/B only)
+            for st in self.stages[n32:self.fp32_stages]:
                 for blk in st:
                     x32, x16 = blk.forward_f32(x32, x16)
-            else:   # past the fp32 stages the shadow is the (bf16) stream
-                x16 = st(x16)
-        if x16.shape[-1] == 128 and self.conv_out.weight.shape[0] == 3:
-            no = self.norm_out
-            return nchw(K.dcae_head(x16, no.eps, no.weight, no.bias, self.conv_out.weight, self.conv_out.bias))
-        return nchw(self.conv_out(self.norm_out(x16, act="relu")))
+            n32 = self.fp32_stages
+        return self._tail(x16, n32)
