@@ -34,6 +34,9 @@ __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcp
 // previous kernel (8-channel threads, weights and every tap re-read from LDS, bf16->fp32 per use)
 // ran the Sana FFN shape at 1.4 TB/s, VALU-bound on conversions.
 // HBM traffic: input ~(TH+KS-1)/TH (halo rows, mostly L2 hits), output one write.
+#ifndef EGG_DW5_WIN
+#define EGG_DW5_WIN 0   // measured 11 % slower at 8x128x128x1536 (2 vs 3 waves per SIMD; profiles/r05e_dw5_register_window_ab.log)
+#endif
 constexpr int DW_CS = 32;  // channels per plane per block (64 B per pixel: adjacent blocks share lines)
 constexpr int DW_TW = 32;  // output columns per block
 constexpr int DW_TH = 8;   // output rows per block
@@ -148,21 +151,23 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) bs[i] = bias ? b2f(bias[pl * Cout + cq + i]) : 0.0f;
-        float win[3][3][4];  // KS == 3 only
-        if constexpr (KS == 3) {
+        // the KS x KS input window in registers, sliding down the band: one new input row (KS LDS reads)
+        // per output row instead of KS*KS.  KS = 5 with EGG_DW5_WIN = 0: every tap read from LDS (the
+        // round-3 form: fewer VGPRs, 3 waves per SIMD instead of 2; A/B knob)
+        constexpr bool WIN = KS == 3 || EGG_DW5_WIN;
+        float win[KS][KS][4];
+        if constexpr (WIN) {
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
+            for (int r = 0; r < KS - 1; ++r)
 #pragma unroll
-                for (int dx = 0; dx < 3; ++dx) rd(pl, r, xs + dx, win[r][dx]);
+                for (int dx = 0; dx < KS; ++dx) rd(pl, r, xs + dx, win[r][dx]);
         }
-        // KS = 5: one output row per iteration (not unrolled): the 25 taps' LDS reads of eight rows are not
-        // all hoisted into registers, which keeps the kernel at 3 waves per SIMD
         constexpr int ROW_UNROLL = KS == 3 ? DW_TH : 1;
 #pragma unroll ROW_UNROLL
         for (int oy = 0; oy < DW_TH; ++oy) {
-            if constexpr (KS == 3) {
+            if constexpr (WIN) {
 #pragma unroll
-                for (int dx = 0; dx < 3; ++dx) rd(pl, oy + 2, xs + dx, win[2][dx]);
+                for (int dx = 0; dx < KS; ++dx) rd(pl, oy + KS - 1, xs + dx, win[KS - 1][dx]);
             }
             float acc[4];
 #pragma unroll
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 #pragma unroll
                 for (int dx = 0; dx < KS; ++dx) {
                     float tap[4];
-                    if constexpr (KS == 3) {
+                    if constexpr (WIN) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) tap[i] = win[dy][dx][i];
                     } else {
@@ -181,14 +186,13 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 #pragma unroll
                     for (int i = 0; i < 4; ++i) acc[i] += tap[i] * w[dy * KS + dx][i];
                 }
-            if constexpr (KS == 3) {
+            if constexpr (WIN) {
 #pragma unroll
-                for (int dx = 0; dx < 3; ++dx)
+                for (int r = 0; r < KS - 1; ++r)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        win[0][dx][i] = win[1][dx][i];
-                        win[1][dx][i] = win[2][dx][i];
-                    }
+                    for (int dx = 0; dx < KS; ++dx)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) win[r][dx][i] = win[r + 1][dx][i];
             }
             if constexpr (PW) {
                 // conv tile -> LDS [pixel oy*32+x][32 ch], 64-B rows with slot ^= 2*((pixel >> 2) & 1): the
