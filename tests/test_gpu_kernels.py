@@ -1195,3 +1195,20 @@ def test_integration_example_runs(dev, pop, r, caps):
                               max_step_norm=max_step, theta_max_norm=max_theta)
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-7)
     assert np.array_equal(order.cpu().numpy(), info["order"])
+
+
+@pytest.mark.parametrize("fp32_stages", [0, 4])
+def test_dcae_high_res_chunking_is_exact(dev, fp32_stages):
+    """DCAEDecoder runs the low-resolution stages on the whole call and the two high-resolution stages in
+    chunks of hi_res_chunk images: the result equals decoding each chunk on its own, bitwise."""
+    from hyperscalees_t2i_amd.dcae import DCAEDecoder
+    vae = DCAEDecoder(32, widths=(16, 32, 32, 64, 64, 64), layers=(1, 1, 1, 1, 1, 1)).to(dev)
+    vae.init_weights(3)
+    vae.fp32_stages = fp32_stages
+    z = torch.randn(6, 32, 2, 2, generator=torch.Generator().manual_seed(5)).to(dev)
+    with torch.no_grad():
+        vae.hi_res_chunk = 2
+        got = vae(z)
+        vae.hi_res_chunk = 8
+        want = torch.cat([vae(z[s:s + 2]) for s in range(0, 6, 2)])
+    assert torch.equal(got, want)
