@@ -290,6 +290,10 @@ def main():
             "configs4_infinity_8b_pop32": aux_kernel_rooflines(ThetaLayout(infinity_lora_shapes(), 1), 32, 0, 4,
                                                                device)}
 
+    peaks = None
+    if rank == 0 and not args.small:   # achievable peaks on this box next to the vendor ones
+        from hyperscalees_t2i_amd.measure import achievable_peaks
+        peaks = achievable_peaks(device)
     value = pop * args.steps / elapsed
     variants = {k: v for k, v in gemm.items() if k != "all" and "tflops" in v}
     dom_name = max(variants, key=lambda k: variants[k]["total_ms"]) if variants else "all"
@@ -304,7 +308,9 @@ def main():
                 "flops_per_launch": dom["flops"] / max(dom["launches"], 1),
                 "window": {"epochs": n_roof, "ms_per_step": roof_ms_per_step,
                            "note": "HIP events on the launch stream; epochs right after the timed region"},
-                "all_variants": gemm.get("all")}
+                "all_variants": gemm.get("all"), "achievable_peaks": peaks,
+                "frac_of_achievable": (achieved / max(peaks["bf16_gemm_tflops_hipblaslt"],
+                                                      peaks["bf16_gemm_tflops_eggroll"]) if peaks else None)}
     for k, v in gemm.items():  # the projection pre-pass (HBM-bound) joins the aux kernel table
         if k.startswith("k_lora_project"):
             aux["lora_project"] = {"us": v["avg_us"], "bytes": v["bytes"] / v["launches"], "GBps": v["GBps"],

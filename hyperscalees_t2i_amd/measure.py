@@ -102,3 +102,27 @@ def aux_kernel_rooflines(layout: ThetaLayout, pop: int, member_lo: int, member_h
     out["sizes"] = {"pop": pop, "members": [member_lo, member_hi], "n_base": nb, "D": D,
                     "factor_len": F, "n_tiles": layout.n_tiles}
     return out
+
+
+def achievable_peaks(device) -> Dict[str, float]:
+    """the peaks measured on this box next to the vendor figures — the best of hipBLASLt's
+    and libeggroll's plain bf16 GEMM at a large square shape (16384 x 8192 x 8192) and a device-to-device
+    copy of 4 GiB (read + write bytes).  Outside the timed region; informational."""
+    g = torch.Generator(device=device).manual_seed(0)
+    M = N = 8192
+    Kd = 8192
+    x = torch.randn(2 * M, Kd, device=device, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, device=device, generator=g) * Kd ** -0.5).bfloat16()
+    fl = 2.0 * 2 * M * N * Kd
+    t_hip = _time(lambda: torch.nn.functional.linear(x, w), it=10)
+    out = torch.empty(2 * M, N, device=device, dtype=torch.bfloat16)
+    t_egg = _time(lambda: K.lora_linear_pop(x, w, None, None, 0, 0, 0, 0.0, 2 * M, out=out), it=10)
+    del x, w, out
+    a = torch.empty(1 << 31, dtype=torch.bfloat16, device=device)
+    b = torch.empty_like(a)
+    t_cp = _time(lambda: b.copy_(a), it=10)
+    del a, b
+    torch.cuda.empty_cache()
+    return {"bf16_gemm_tflops_hipblaslt": fl / t_hip / 1e12, "bf16_gemm_tflops_eggroll": fl / t_egg / 1e12,
+            "hbm_copy_GBps": 2.0 * 2 * (1 << 31) / t_cp / 1e9,
+            "note": "16384x8192x8192 bf16 GEMM (average of 10, HIP events); 4 GiB device copy, read + write bytes"}
