@@ -911,8 +911,52 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
         }
         const int row0 = m0 + rbase + (lane >> 3), col0 = n0 + cbase + (lane & 7) * 8;
         if constexpr (E32) {
+            // the fp32 residual rows (and gates) of 8 row-steps are all loaded before any is stored: one
+            // epi_store32 per row-step put every res load behind the previous row-step's stores (the
+            // compiler cannot prove they do not alias), i.e. 16 serial HBM round trips per wave
+            float* rb = const_cast<float*>(reinterpret_cast<const float*>(ea.res));
+            const float* gb = reinterpret_cast<const float*>(ea.gate);
 #pragma unroll
-            for (int it = 0; it < 16; ++it) epi_store32<EPI>(v[it], row0 + it * 8, col0, ea, Y, ldy);
+            for (int h = 0; h < 16; h += 8) {
+                float4 rv[8][2], gv[8][2];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int row = row0 + (h + i) * 8;
+                    const float* r = rb + (int64_t)row * ea.ldr + col0;
+                    rv[i][0] = *reinterpret_cast<const float4*>(r);
+                    rv[i][1] = *reinterpret_cast<const float4*>(r + 4);
+                    if constexpr (EPI == EPI_GATED32) {
+                        const float* g = gb + (int64_t)(row / ea.rpg) * ea.gstride + col0;
+                        gv[i][0] = *reinterpret_cast<const float4*>(g);
+                        gv[i][1] = *reinterpret_cast<const float4*>(g + 4);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int row = row0 + (h + i) * 8;
+                    const u16x8 yv = v[h + i];
+                    float x[8] = {rv[i][0].x, rv[i][0].y, rv[i][0].z, rv[i][0].w,
+                                  rv[i][1].x, rv[i][1].y, rv[i][1].z, rv[i][1].w};
+                    if constexpr (EPI == EPI_GATED32) {
+                        const float gg[8] = {gv[i][0].x, gv[i][0].y, gv[i][0].z, gv[i][0].w,
+                                             gv[i][1].x, gv[i][1].y, gv[i][1].z, gv[i][1].w};
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) x[u] = __builtin_fmaf(gg[u], bf16_to_f32(yv[u]), x[u]);
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) x[u] = x[u] + bf16_to_f32(yv[u]);
+                    }
+                    float* r = rb + (int64_t)row * ea.ldr + col0;
+                    *reinterpret_cast<float4*>(r) = float4{x[0], x[1], x[2], x[3]};
+                    *reinterpret_cast<float4*>(r + 4) = float4{x[4], x[5], x[6], x[7]};
+                    if (Y) {
+                        u16x8 o;
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) o[u] = f32_to_bf16(x[u]);
+                        *reinterpret_cast<u16x8*>(Y + (int64_t)row * ldy + col0) = o;
+                    }
+                }
+            }
             return;
         }
         if constexpr (EPI != EPI_NONE && !E32) {
