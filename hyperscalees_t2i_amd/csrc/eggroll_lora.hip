@@ -1528,10 +1528,73 @@ __device__ __forceinline__ void store_tile_wg(f32x4 (&acc)[8][5], char* smem, in
         }
     }
     __syncthreads();
+    constexpr bool E32 = EPI == EPI_RES32 || EPI == EPI_GATED32;
     const bool vec = (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0 &&
                      (EPI == EPI_NONE || EPI == EPI_SILU ||
                       ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
-                       (EPI != EPI_GATED || ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0))));
+                       ((EPI != EPI_GATED && EPI != EPI_GATED32) ||
+                        ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0))));
+    if constexpr (E32) {
+        // fp32 residual stream: per group of 5 chunks, every residual (and gate) load issued before any
+        // store (one load -> fma -> store per chunk serialises the loads behind the earlier stores)
+        float* rb = const_cast<float*>(reinterpret_cast<const float*>(ea.res));
+        const float* gb = reinterpret_cast<const float*>(ea.gate);
+#pragma unroll
+        for (int h = 0; h < 20; h += 5) {
+            u16x8 v[5];
+            float4 rv[5][2], gv[5][2];
+            int rows[5], cols[5];
+            bool ok[5];
+#pragma unroll
+            for (int it = 0; it < 5; ++it) {
+                const int idx = (h + it) * 64 + lane, rr = wave * 32 + idx / SL, ch = idx % SL;
+                v[it] = *reinterpret_cast<const u16x8*>(smem + rr * RB + (ch + rr) % SL * 16);
+                rows[it] = m0 + rr;
+                cols[it] = n0 + ch * 8;
+                ok[it] = rows[it] < M && cols[it] + 8 <= N && vec;
+                if (ok[it]) {
+                    const float* r = rb + (int64_t)rows[it] * ea.ldr + cols[it];
+                    rv[it][0] = *reinterpret_cast<const float4*>(r);
+                    rv[it][1] = *reinterpret_cast<const float4*>(r + 4);
+                    if constexpr (EPI == EPI_GATED32) {
+                        const float* g = gb + (int64_t)(rows[it] / ea.rpg) * ea.gstride + cols[it];
+                        gv[it][0] = *reinterpret_cast<const float4*>(g);
+                        gv[it][1] = *reinterpret_cast<const float4*>(g + 4);
+                    }
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < 5; ++it) {
+                const int row = rows[it], col = cols[it];
+                if (row >= M || col >= N) continue;
+                if (!ok[it]) {   // ragged tail / unaligned: the element form
+                    for (int u = 0; u < 8 && col + u < N; ++u) epi_store32_1<EPI>(v[it][u], row, col + u, ea, Y, ldy);
+                    continue;
+                }
+                float x[8] = {rv[it][0].x, rv[it][0].y, rv[it][0].z, rv[it][0].w,
+                              rv[it][1].x, rv[it][1].y, rv[it][1].z, rv[it][1].w};
+                if constexpr (EPI == EPI_GATED32) {
+                    const float gg[8] = {gv[it][0].x, gv[it][0].y, gv[it][0].z, gv[it][0].w,
+                                         gv[it][1].x, gv[it][1].y, gv[it][1].z, gv[it][1].w};
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = __builtin_fmaf(gg[u], bf16_to_f32(v[it][u]), x[u]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = x[u] + bf16_to_f32(v[it][u]);
+                }
+                float* r = rb + (int64_t)row * ea.ldr + col;
+                *reinterpret_cast<float4*>(r) = float4{x[0], x[1], x[2], x[3]};
+                *reinterpret_cast<float4*>(r + 4) = float4{x[4], x[5], x[6], x[7]};
+                if (Y) {
+                    u16x8 o;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) o[u] = f32_to_bf16(x[u]);
+                    *reinterpret_cast<u16x8*>(Y + (int64_t)row * ldy + col) = o;
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int h = 0; h < 20; h += 10) {
         u16x8 v[10];
@@ -2020,7 +2083,10 @@ static bool gemm8n_ok(int32_t r, int64_t rows_per_member) { return r == 0 || (r 
 // DESIGN §5).  131072 x 2240: 18 vs 14 x 1.22 rounds -> 10 (+3-6 % measured); 9600 x 2240: 2 vs 2 x 1.22
 // -> 8.  The residual / gated-residual epilogues stay on 8 (their loads slow kernel 10's store phase).
 static int gemm8_auto(int64_t M, int64_t N, int32_t r, int64_t rows_per_member, int32_t epi) {
-    if (!gemm8n_ok(r, rows_per_member) || (epi != EPI_NONE && epi != EPI_SILU)) return 8;
+    // the bf16 residual epilogues stay on 8 (their per-chunk loads slow kernel 10's store phase); the fp32
+    // ones load in batches and run equal (to_out) or 3 % faster (FFN point conv, K 5632) on 10
+    // (profiles/r05h_epi32_kernel8_vs_10_ab.log)
+    if (!gemm8n_ok(r, rows_per_member) || epi == EPI_RES || epi == EPI_GATED) return 8;
     const int64_t tm = (M + 255) / 256;
     const int64_t rounds8 = (tm * ((N + 255) / 256) + 255) / 256, rounds10 = (tm * ((N + 319) / 320) + 255) / 256;
     return 122 * rounds10 < 100 * rounds8 ? 10 : 8;
@@ -2048,7 +2114,9 @@ static int launch_gemm8n(const void* X, int64_t ldx, const void* W, int64_t ldw,
         case EPI_NONE: EGG_GEMM8N_R(EPI_NONE); break;
         case EPI_SILU: EGG_GEMM8N_R(EPI_SILU); break;
         case EPI_RES: EGG_GEMM8N_R(EPI_RES); break;
-        default: EGG_GEMM8N_R(EPI_GATED); break;
+        case EPI_GATED: EGG_GEMM8N_R(EPI_GATED); break;
+        case EPI_RES32: EGG_GEMM8N_R(EPI_RES32); break;
+        default: EGG_GEMM8N_R(EPI_GATED32); break;
     }
 #undef EGG_GEMM8N_R
 #undef EGG_GEMM8N
@@ -3230,7 +3298,6 @@ int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, i
         return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
                                            rows_per_member, M, N, K, Y, ldy, T_ws, kernel, stream);
     EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_GATED32, "lora_linear_pop_epi: epi=%d unknown", epi);
-    EGG_CHECK_ARG(kernel != 10 || epi <= EPI_GATED, "lora_linear_pop_epi: the fp32-stream epilogues run on kernel 8");
     EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
     EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
     EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "lora_linear_pop_epi: need K %% 64 == 0");

@@ -1037,11 +1037,13 @@ def test_gated_residual_f32(dev):
         assert torch.equal(sh, x1.to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("kernel", [8, 10])
 @pytest.mark.parametrize("epi,r,M,N,Kd,rpm", [("gated32", 2, 4 * 4096, 2240, 2240, 4096), ("res32", 2, 4 * 4096, 2240, 2240, 4096),
                                              ("gated32", 1, 3 * 1000 + 200, 384, 256, 1000), ("res32", 0, 777, 200, 128, 777)])
-def test_lora_epilogue_fp32_stream_bitexact(dev, epi, r, M, N, Kd, rpm):
-    """EPI_RES32 / EPI_GATED32 (the fp32 residual stream fused into kernel 8's store phase) == the same
-    GEMM followed by eggroll_gated_residual_f32, bit for bit, stream and bf16 shadow; ragged shapes."""
+def test_lora_epilogue_fp32_stream_bitexact(dev, epi, r, M, N, Kd, rpm, kernel):
+    """EPI_RES32 / EPI_GATED32 (the fp32 residual stream fused into the store phase of kernel 8 / 10) ==
+    the same GEMM followed by eggroll_gated_residual_f32, bit for bit, stream and bf16 shadow; ragged
+    shapes."""
     g = torch.Generator(device=dev).manual_seed(M + N + 1)
     x = torch.randn((M, Kd), generator=g, device=dev).to(torch.bfloat16)
     W = (torch.randn((N, Kd), generator=g, device=dev) / Kd ** 0.5).to(torch.bfloat16)
@@ -1057,7 +1059,7 @@ def test_lora_epilogue_fp32_stream_bitexact(dev, epi, r, M, N, Kd, rpm):
     K.gated_residual_f32_(ref, y, gate if epi == "gated32" else None, rpg, shadow=ref_sh)
     got, sh = res.clone(), torch.empty((M, N), dtype=torch.bfloat16, device=dev)
     K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, epi, res=got, gate=gate if epi == "gated32" else None,
-                          rows_per_group=rpg, out=sh)
+                          rows_per_group=rpg, out=sh, kernel=kernel)
     assert torch.equal(got, ref) and torch.equal(sh, ref_sh)
 
 

@@ -2,7 +2,7 @@
 eggroll_lora_linear_pop_epi_sel) at the Sana shapes: attn1 to_out (gated, LoRA r 2), attn2 to_out
 (res, r 2), the FFN point conv (gated, r 0, K 5632).  fp32 residual and bf16 shadow compared bitwise,
 then interleaved timing (median of rounds).
-usage: python tools/epi32_lib_ab.py <libA.so> <libB.so>"""
+usage: python tools/epi32_lib_ab.py <libA.so> <libB.so> [kernelA kernelB]  (8 / 10, default 8 8)"""
 import ctypes
 import json
 import statistics
@@ -17,8 +17,9 @@ from es_lib_ab import bind, timed  # noqa: E402
 from hyperscalees_t2i_amd import kernels as K  # noqa: E402
 
 
-def main(pa, pb, rounds=7):
+def main(pa, pb, ka=8, kb=8, rounds=7):
     libs = [bind(pa), bind(pb)]
+    kern = [int(ka), int(kb)]
     dev = torch.device("cuda:0")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     g = torch.Generator(device=dev).manual_seed(3)
@@ -42,7 +43,7 @@ def main(pa, pb, rounds=7):
             rc = libs[i].eggroll_lora_linear_pop_epi_sel(
                 x.data_ptr(), Kd, W.data_ptr(), Kd, None, tp.data_ptr() if r else None, tp.stride(0) if r else 0,
                 0, r * Kd, r, 4.0, rpm if r else M, M, N, Kd, sh[i].data_ptr(), N, ws.data_ptr() if r else None, epi,
-                res[i].data_ptr(), N, gate.data_ptr() if epi == 5 else None, N, 1024, 8, st)
+                res[i].data_ptr(), N, gate.data_ptr() if epi == 5 else None, N, 1024, kern[i], st)
             assert rc == 0, rc
         run(0, True)
         run(1, True)
@@ -61,4 +62,4 @@ def main(pa, pb, rounds=7):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:])
