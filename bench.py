@@ -68,14 +68,17 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--small", action="store_true", help="tiny architecture (smoke only; not a valid metric)")
     p.add_argument("--aux-out", type=str, default="", help="write per-phase / per-kernel details here")
-    p.add_argument("--workload", choices=("sana", "var_d16", "zimage"), default="sana",
+    p.add_argument("--workload", choices=("sana", "var_d16", "zimage", "infinity"), default="sana",
                    help="var_d16: BASELINE configs[0] (VAR-d16, LoRA r 4, 4 classes x 4 batches) on the GPU path; "
-                        "zimage: configs[3] (Z-Image-Turbo, egg rank 4, one GPU's 16 of pop 128, 384 px, 7 steps)")
+                        "zimage: configs[3] (Z-Image-Turbo, egg rank 4, one GPU's 16 of pop 128, 384 px, 7 steps); "
+                        "infinity: configs[4] (Infinity-8B 512 px, one GPU's 4 of pop 32, 10 scales, cfg 3)")
     a = p.parse_args()
     if a.workload == "var_d16" and a.pop_per_gpu == 8 and "--pop-per-gpu" not in sys.argv:
         a.pop_per_gpu = 4           # configs[0]: pop_size 4
     if a.workload == "zimage" and a.pop_per_gpu == 8 and "--pop-per-gpu" not in sys.argv:
         a.pop_per_gpu = 16          # configs[3]: pop_size 128 across 8 GPUs
+    if a.workload == "infinity" and a.pop_per_gpu == 8 and "--pop-per-gpu" not in sys.argv:
+        a.pop_per_gpu = 4           # configs[4]: pop_size 32 across 8 GPUs
     return a
 
 
@@ -165,7 +168,38 @@ def build_zimage(args, world, rank, device):
     return backend, engine, noiser, theta, pop
 
 
+def build_infinity(args, world, rank, device):
+    """BASELINE configs[4]: Infinity-8B 512 px (pn 0.25M, f8 VAE + 2x2 patchify, 14 bits per VAE pixel),
+    LoRA r 2 / alpha 8 on fc1, egg rank 1, pop_per_gpu (4 = one GPU's share of pop 32) antithetic,
+    4 prompts x 4 batches per member, cfg 3 / tau 1 / top-k 900 / top-p 0.97, micro_batch 2
+    (unifed_es.py:51-61, 422-472 defaults)."""
+    from hyperscalees_t2i_amd.backend import InfinityBackend, InfinityConfig
+    from hyperscalees_t2i_amd.es import EggRollNoiser, flatten_params
+    from hyperscalees_t2i_amd.es_step import DistInfo, ESConfig, ESEngine
+    from hyperscalees_t2i_amd.infinity import InfinityArch
+    from hyperscalees_t2i_amd.rewards import RewardModels
+
+    cfg = InfinityConfig(synthetic_weights=True)
+    if args.small:
+        cfg.arch = InfinityArch(depth=2, embed_dim=256, num_heads=2, block_chunks=2, text_channels=256,
+                                codebook_dim=4, spatial_patchify=1, vae_widths=(32, 32, 64, 64))
+        cfg.pn = "0.06M"
+    backend = InfinityBackend(device=str(device), cfg=cfg)
+    backend.init_and_attach_lora()
+    params, shapes = backend.collect_lora_params()
+    theta = flatten_params(params).to(device=device, dtype=torch.float32)
+    noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=1, use_antithetic=True)
+    rewards = RewardModels.build(device, tiny=args.small, synthetic=True)
+    pop = args.pop_per_gpu * world
+    es_cfg = ESConfig(pop_size=pop, sigma=1e-2, lr_scale=1e-1, egg_rank=1, use_antithetic=True, promptnorm=True,
+                      theta_max_norm=40.0, max_step_norm=0.0)
+    engine = ESEngine(backend, rewards, noiser, es_cfg, device, DistInfo(rank, world, None))
+    return backend, engine, noiser, theta, pop
+
+
 def build(args, world, rank, device):
+    if args.workload == "infinity":
+        return build_infinity(args, world, rank, device)
     if args.workload == "var_d16":
         return build_var(args, world, rank, device)
     if args.workload == "zimage":
@@ -334,6 +368,27 @@ def main():
                        "steps": c.num_inference_steps, "guidance": c.guidance_scale, "egg_rank": 4, "lora_r": c.lora_r,
                        "lora_alpha": c.lora_alpha, "theta_D": noiser.num_params,
                        "parallelism": f"member-shard x{world} (S all-gather)"},
+            "roofline": roofline, "cpu_baseline": None, "phases_ms": phases, "aux_kernels": aux,
+            "model_kernels": model_kernels,
+        }
+        print(json.dumps(line), flush=True)
+        if args.aux_out:
+            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
+    elif rank == 0 and args.workload == "infinity":
+        c = backend.cfg
+        line = {
+            "metric": "ES member-evals/sec Infinity-8B 512px (BASELINE configs[4], pop 32 over 8 GPUs)",
+            "value": value, "unit": "member-evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init Infinity-8B / BSQ-VAE decoder / CLIP weights, synthetic T5 prompt features)",
+            "config": {"workload": "tiny-arch smoke (INVALID as metric)" if args.small else "infinity_8b_512px_es_epoch",
+                       "pop_per_gpu": args.pop_per_gpu, "pop_total": pop,
+                       "images_per_member": c.prompts_per_gen * c.batches_per_gen, "pn": c.pn,
+                       "scales": len(backend.es_model.scale_schedule), "cfg": c.cfg_list, "tau": c.tau_list,
+                       "top_k": c.top_k, "top_p": c.top_p, "micro_batch": c.micro_batch, "egg_rank": 1,
+                       "lora_r": c.lora_r, "lora_alpha": c.lora_alpha, "lora_targets": c.lora_target_modules,
+                       "theta_D": noiser.num_params, "parallelism": f"member-shard x{world} (S all-gather)"},
             "roofline": roofline, "cpu_baseline": None, "phases_ms": phases, "aux_kernels": aux,
             "model_kernels": model_kernels,
         }

@@ -522,3 +522,183 @@ class ZImageBackend(ESBackend):
         c = self.cfg
         return self.es_model.generate_population([self._dev_prompts[p] for p in uniq], idx, theta_pop, seed,
                                                  guidance_scale, c.width_px, c.height_px, c.num_inference_steps)
+
+
+# ---------------------------------------------------------------------------------------
+# Infinity (BASELINE configs[4]): es_backend.py:680-1023
+# ---------------------------------------------------------------------------------------
+@dataclass
+class InfinityConfig:
+    """es_backend.py:680-733; defaults = the reference CLI's 8b_512 variant (unifed_es.py:51-61, 422-472,
+    micro_batch from --max_batch 2) + build knobs."""
+
+    model_path: str = "Infinity/weights/infinity_8b_512x512_weights"
+    text_encoder_ckpt: str = "google/flan-t5-xl"
+    vae_path: str = "Infinity/weights/infinity_vae_d56_f8_14_patchify.pth"
+    pn: str = "0.25M"
+    model_type: str = "infinity_8b"
+    vae_type: int = 14
+    h_div_w_template: float = 1.0
+    text_channels: int = 2048
+    apply_spatial_patchify: int = 1
+    use_flex_attn: int = 0
+    bf16: int = 1
+    checkpoint_type: str = "torch_shard"
+    prompts_txt_path: str = "untitled1.txt"
+    encoded_prompt_path: str = ""
+    auto_encode_if_missing: bool = False
+    encode_batch_size: int = 16
+    drop_text_encoder_after_encode: bool = True
+    prompts_per_gen: int = 4
+    batches_per_gen: int = 4
+    max_log_batches: int = 1
+    cfg_list: Any = 3.0
+    tau_list: Any = 1.0
+    cfg_insertion_layer: int = 0
+    sampling_per_bits: int = 1
+    enable_positive_prompt: int = 0
+    top_k: int = 900
+    top_p: float = 0.97
+    micro_batch: int = 2
+    lora_r: int = 2
+    lora_alpha: int = 8
+    lora_dropout: float = 0.0
+    lora_target_modules: List[str] = field(default_factory=lambda: ["fc1"])
+    torch_compile: bool = False
+    compile_mode: str = "max-autotune"
+    compile_fullgraph: bool = False
+    compile_vae: bool = False
+    guidance_scale: float = 3.0              # --inf_guidance_scale (cfg_sc; the per-scale cfg_list applies)
+    # build-specific
+    arch: Any = None                         # None: arch_for(model_type, vae_type, apply_spatial_patchify)
+    vae_chunk: int = 16
+    kv_budget_gb: float = 120.0
+    synthetic_prompts: int = 4               # used when encoded_prompt_path is empty
+    synthetic_prompt_lens: Tuple[int, int] = (16, 100)
+    lora_b_std: float = 0.02
+    lora_seed: int = 1234
+    weight_seed: int = 0
+    synthetic_weights: bool = False          # no Infinity checkpoint loader: True is required (explicit opt-in)
+
+
+def synthetic_infinity_prompt_data(P: int = 4, lens: Tuple[int, int] = (16, 100), dim: int = 2048,
+                                   seed: int = 0) -> Dict[str, Any]:
+    """Same dict format as InfinityES.encode_prompts (models/Infinity.py:267-335): prompts,
+    kv_compact_list (per-prompt [L_i, dim] fp16 CPU tensors, L_i ~ U[lens]) and lens_list."""
+    g = torch.Generator().manual_seed(seed)
+    T = torch.randint(lens[0], lens[1] + 1, (P,), generator=g).tolist()
+    kv = [(torch.randn(t, dim, generator=g) * 0.2).to(torch.float16) for t in T]
+    return {"prompts": [f"synthetic prompt {i}: a detailed photo of object {i}" for i in range(P)],
+            "kv_compact_list": kv, "lens_list": [int(t) for t in T]}
+
+
+class InfinityBackend(ESBackend):
+    """es_backend.py:735-1023."""
+
+    def __init__(self, device: str, cfg: InfinityConfig):
+        self.name = "infinity"
+        self.device = device
+        self.cfg = cfg
+        self.es_model = None
+        self.prompt_data = None
+        self.kv_compact_list = None
+        self.lens_list = None
+        self.prompts_list = None
+        self.image_pil_mode = 2          # rewards: Infinity's bf16 (x + 1) / 2 * 255 -> uint8
+
+    def _load_or_encode_prompts(self):
+        """es_backend.py:749-801 (no T5 offline: an encoded file, or the synthetic set when no path is set)."""
+        c = self.cfg
+        if c.encoded_prompt_path:
+            enc = Path(c.encoded_prompt_path)
+            if not enc.is_file():
+                if not c.auto_encode_if_missing:
+                    raise FileNotFoundError(f"encoded_prompt_path not found and auto_encode disabled: {enc}")
+                raise FileNotFoundError(f"encoded_prompt_path not found and the T5 encoder is not available "
+                                        f"offline: {enc}")
+            self.prompt_data = torch.load(enc, map_location="cpu", weights_only=True)
+        else:
+            a = c.arch
+            self.prompt_data = synthetic_infinity_prompt_data(c.synthetic_prompts, c.synthetic_prompt_lens,
+                                                              a.text_channels if a is not None else c.text_channels)
+        self.prompts_list = self.prompt_data["prompts"]
+        self.kv_compact_list = self.prompt_data["kv_compact_list"]
+        self.lens_list = self.prompt_data["lens_list"]
+        self._dev_kv = [kv.to(self.device) for kv in self.kv_compact_list]
+
+    def init_and_attach_lora(self) -> None:
+        from .infinity_pipeline import InfinityES
+        c = self.cfg
+        self._load_or_encode_prompts()
+        self.es_model = InfinityES(model_path=c.model_path, text_encoder_ckpt=c.text_encoder_ckpt, vae_path=c.vae_path,
+                                   vae_type=int(c.vae_type), pn=c.pn, model_type=c.model_type,
+                                   h_div_w_template=float(c.h_div_w_template), text_channels=int(c.text_channels),
+                                   apply_spatial_patchify=int(c.apply_spatial_patchify),
+                                   use_flex_attn=int(c.use_flex_attn), bf16=bool(c.bf16),
+                                   checkpoint_type=c.checkpoint_type,
+                                   enable_positive_prompt=int(c.enable_positive_prompt), top_k=int(c.top_k),
+                                   top_p=float(c.top_p), cfg_insertion_layer=int(c.cfg_insertion_layer),
+                                   sampling_per_bits=int(c.sampling_per_bits), device=self.device,
+                                   synthetic_weights=c.synthetic_weights, arch=c.arch, weight_seed=c.weight_seed,
+                                   vae_chunk=c.vae_chunk, kv_budget_gb=c.kv_budget_gb)
+        n = attach_lora(self.es_model.transformer, c.lora_r, c.lora_alpha, c.lora_target_modules)
+        if n == 0:
+            raise RuntimeError("no LoRA target module matched")
+        g = torch.Generator(device=self.device).manual_seed(c.lora_seed)
+        for m in lora_modules(self.es_model.transformer):
+            m.reset_lora(g, b_std=c.lora_b_std)
+        self.es_model.infinity = self.es_model.transformer
+        self.es_model.transformer.eval()
+        self.es_model.drop_text_encoder()
+
+    def compile_if_requested(self) -> None:
+        return   # no tracing compiler on this stack: the hot ops are explicit libeggroll kernels
+
+    def collect_lora_params(self):
+        return get_trainable_params_and_shapes(self.es_model.transformer)
+
+    def save_lora(self, save_dir: Path) -> None:
+        """es_backend.py:820-822: the PEFT adapter of the transformer in save_dir."""
+        c = self.cfg
+        _save_adapter(self.es_model.transformer, Path(save_dir),
+                      {"peft_type": "LORA", "r": c.lora_r, "lora_alpha": c.lora_alpha, "lora_dropout": c.lora_dropout,
+                       "target_modules": list(c.lora_target_modules), "base_model_name_or_path": c.model_path,
+                       "bias": "none", "task_type": None})
+
+    def load_lora(self, save_dir: Path) -> None:
+        _load_adapter(self.es_model.transformer, Path(save_dir))
+
+    def step_sampling_info(self, seed: int) -> Dict[str, Any]:
+        """es_backend.py:824-852."""
+        P = int(len(self.kv_compact_list))
+        unique_ids = sample_indices_unique(seed=seed, total=P, k=int(self.cfg.prompts_per_gen))
+        flat_ids = repeat_batches(unique_ids, repeats=int(self.cfg.batches_per_gen))
+        m = len(unique_ids)
+        log_batches = int(max(0, min(int(self.cfg.max_log_batches), int(self.cfg.batches_per_gen))))
+        return dict(unique_ids=unique_ids, flat_ids=flat_ids,
+                    unique_texts=[self.prompts_list[p] for p in unique_ids],
+                    flat_texts=[self.prompts_list[p] for p in flat_ids], pid_to_j={p: j for j, p in enumerate(unique_ids)},
+                    m=m, total_imgs_per_indiv=len(flat_ids), total_imgs_for_logging=log_batches * m,
+                    log_batches=log_batches)
+
+    def generate_flat(self, flat_ids: List[int], seed: int, guidance_scale: float) -> List[Any]:
+        """es_backend.py:893-1022: one member (the transformer's own LoRA params); micro_batch <= 0 or
+        >= N is one call, else chunks of micro_batch images, each call reseeded with `seed`."""
+        c = self.cfg
+        if len(flat_ids) == 0:
+            return []
+        return self.es_model.generate_one_batch_from_compacts(
+            kv_compact_list=[self._dev_kv[p] for p in flat_ids], lens_list=[int(self.lens_list[p]) for p in flat_ids],
+            seed=seed, guidance_scale=guidance_scale, cfg_list=c.cfg_list, tau_list=c.tau_list,
+            cfg_insertion_layer=int(c.cfg_insertion_layer), sampling_per_bits=int(c.sampling_per_bits),
+            vae_type=int(c.vae_type), top_k=int(c.top_k), top_p=float(c.top_p), micro_batch=int(c.micro_batch))
+
+    def generate_population(self, flat_ids: List[int], seed: int, guidance_scale: float,
+                            theta_pop: torch.Tensor) -> torch.Tensor:
+        """Every member's images in one batch per scale; the text path runs once per distinct prompt."""
+        c = self.cfg
+        uniq = list(dict.fromkeys(int(f) for f in flat_ids))
+        idx = torch.tensor([uniq.index(int(f)) for f in flat_ids], device=self.device)
+        return self.es_model.generate_population([self._dev_kv[p] for p in uniq], [int(self.lens_list[p]) for p in uniq],
+                                                 idx, theta_pop, seed, c.cfg_list, c.tau_list, int(c.top_k),
+                                                 float(c.top_p), int(c.micro_batch))

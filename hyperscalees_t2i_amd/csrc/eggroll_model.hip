@@ -1013,7 +1013,8 @@ using namespace eggroll;
 // CLIP image preprocessing, bit-exact with transformers' CLIPImageProcessor (PIL backend) on the
 // PIL image the reference would build from the decoder output (rewards.py:86-90, 133-147):
 //   u8 = PixArt postprocess (mode 0: rint((x/2 + 0.5).clamp(0,1) * 255), Sana) or the VAR PIL
-//        path (mode 1: fp16 ((x+1)*0.5).clamp(0,1) * 255 truncated, models/VAR.py:190, 245-259);
+//        path (mode 1: fp16 ((x+1)*0.5).clamp(0,1) * 255 truncated, models/VAR.py:190, 245-259) or
+//        Infinity's (mode 2: bf16 (x+1)/2*255 truncated);
 //   Pillow BICUBIC resize in 8-bit fixed point (Resample.c: int32 taps of 22 fractional bits,
 //   horizontal pass first, each pass rounded + clipped to 8 bits), center crop, then
 //   (u8 / 255 - mean[c]) / std[c] in fp32 (IEEE division, as torch).
@@ -1025,6 +1026,14 @@ __device__ __forceinline__ int clip_u8_of(float x, int mode) {
     if (mode == 0) {
         float v = fminf(fmaxf(x * 0.5f + 0.5f, 0.0f), 1.0f);
         return (int)rintf(v * 255.0f);
+    }
+    if (mode == 2) {
+        // Infinity (models/Infinity.py img postprocess under bf16 autocast): (x + 1) / 2 * 255, every op
+        // rounded to bf16, clamped (the decoder output is in [-1, 1]), .to(uint8) truncates
+        auto r = [](float v) { return b2f(f2b(v)); };
+        float v = r(r(r(x + 1.0f) * 0.5f) * 255.0f);
+        v = fminf(fmaxf(v, 0.0f), 255.0f);
+        return (int)v;
     }
     // fp16 arithmetic of the reference's autocast output: every op rounded to half
     _Float16 h = (_Float16)x;
@@ -1719,7 +1728,8 @@ extern "C" int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, in
                                        int32_t ktw, int32_t kth, int64_t RW, int64_t RH, int64_t out_size,
                                        const float* mean, const float* stdv, void* tmp, void* out, void* stream) {
     EGG_CHECK_ARG(n >= 0 && H > 0 && W > 0 && out_size > 0 && RW >= out_size && RH >= out_size, "clip_preprocess: bad sizes");
-    EGG_CHECK_ARG(mode == 0 || mode == 1, "clip_preprocess: mode %d (0 PixArt round, 1 VAR fp16 trunc)", mode);
+    EGG_CHECK_ARG(mode >= 0 && mode <= 2, "clip_preprocess: mode %d (0 PixArt round, 1 VAR fp16 trunc, 2 Infinity bf16 trunc)",
+                  mode);
     EGG_CHECK_ARG(ktw > 0 && kth > 0 && ktw <= 64 && kth <= 64, "clip_preprocess: tap counts out of range");
     if (n == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(img && tab_w && tab_h && mean && stdv && tmp && out, "clip_preprocess: NULL pointer");

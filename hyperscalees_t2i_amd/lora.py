@@ -182,6 +182,11 @@ class LoRALinear(nn.Module):
                                       self.r, self.scale, rpm, epi, res=res2, gate=gate, rows_per_group=rows_per_group,
                                       T_ws=ws, out=sh2)
                 return res
+            if (FUSE_EPILOGUES and not self.r and not GemmTimer.active and M >= 4096 and self.in_features % 64 == 0
+                    and epi in ("res", "gated")):   # plain linear (no LoRA), epilogue fused (Infinity's proj / fc2)
+                K.lora_linear_pop_epi(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M, epi, res=res2, gate=gate,
+                                      rows_per_group=rows_per_group)
+                return res
             y = self.forward(x).view(M, self.out_features)   # the same ops, unfused
             if epi == "res":
                 res2.add_(y)

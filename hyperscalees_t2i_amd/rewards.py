@@ -180,7 +180,7 @@ def clip_pixels(images: torch.Tensor, pil_mode: int = 0, size: int = 224, mean: 
                 std: Sequence[float] = CLIP_STD) -> torch.Tensor:
     """Decoder images [n,3,H,W] (bf16, any strides) -> CLIP pixel values [n,3,size,size] fp32 on the
     HIP path (eggroll_clip_preprocess): the uint8 PIL conversion of the backend (pil_mode 0: PixArt
-    postprocess, rounding; 1: the VAR PIL path, fp16 + truncation), Pillow's bicubic resize of the
+    postprocess, rounding; 1: the VAR PIL path, fp16 + truncation; 2: Infinity's, bf16 + truncation), Pillow's bicubic resize of the
     short edge, center crop, CLIP normalisation — bitwise equal to
     clip_preprocess(postprocess_uint8(images)) / clip_preprocess(quantize_uint8_var(images))."""
     from . import _lib

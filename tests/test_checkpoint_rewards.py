@@ -116,12 +116,14 @@ def test_clip_pixels_hip_bitexact(dev, H, W):
     """eggroll_clip_preprocess (one HIP pass per resize direction, int32 Pillow taps, fused uint8
     conversion and normalisation) == the torch restatement on the CPU, which
     test_clip_preprocess_matches_transformers_processor pins to transformers bit for bit; both PIL
-    conversions (0: PixArt rounding, Sana; 1: fp16 + truncation, VAR); NHWC-strided input."""
+    conversions (0: PixArt rounding, Sana; 1: fp16 + truncation, VAR; 2: bf16 + truncation, Infinity);
+    NHWC-strided input."""
     from hyperscalees_t2i_amd.rewards import clip_pixels
     from hyperscalees_t2i_amd.var import quantize_uint8_var
     x = _images(3, H, W, H * 3 + W).to(torch.bfloat16)
     xd = x.to(dev).contiguous(memory_format=torch.channels_last)
-    for mode, to_u8 in ((0, lambda t: postprocess_uint8(t)), (1, quantize_uint8_var)):
+    from hyperscalees_t2i_amd.infinity_pipeline import images_to_uint8
+    for mode, to_u8 in ((0, lambda t: postprocess_uint8(t)), (1, quantize_uint8_var), (2, images_to_uint8)):
         ref = clip_preprocess(to_u8(x)).numpy()
         ours = clip_pixels(xd, mode).cpu().numpy()
         assert ours.shape == ref.shape == (3, 3, 224, 224)
