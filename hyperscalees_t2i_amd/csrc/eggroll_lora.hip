@@ -780,7 +780,8 @@ __device__ __forceinline__ void lora_epilogue(f32x4 (&acc)[WTM / 16][WTN / 16], 
 //   EPI_RES32   : res = res + float(y)                     (x = x + attn2(...))
 //   EPI_GATED32 : res = fma(gate32[row / rpg], float(y), res)  (x += gate * attn1(...); gate fp32)
 // The same expressions as eggroll_gated_residual_f32, so fused == unfused bit for bit.
-enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3, EPI_RES32 = 4, EPI_GATED32 = 5 };
+//   EPI_GELU  : out = bf16(gelu_tanh(y))                   (Infinity / VAR ffn: fc1 -> GELU(tanh))
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3, EPI_RES32 = 4, EPI_GATED32 = 5, EPI_GELU = 6 };
 struct EpiArgs {
     const unsigned short* res;
     int64_t ldr;
@@ -789,6 +790,15 @@ struct EpiArgs {
     int64_t rpg;
 };
 __device__ __forceinline__ float epi_silu(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
+// GELU, approximate = "tanh": 0.5 x (1 + tanh(k)) = x * sigmoid(2k), k = sqrt(2/pi) (x + 0.044715 x^3),
+// with the hardware exp2 / rcp as the SiLU epilogue (ocml's tanhf made the fc1 store phase 15 % of the
+// GEMM: tools/gelu_epi_probe.py); within 1 bf16 ulp of torch's tanh form
+__device__ __forceinline__ float epi_gelu(float x) {
+    constexpr float kBeta2L = (float)(M_SQRT2 * M_2_SQRTPI * 0.5 * 2.0 * 1.4426950408889634);
+    constexpr float kKappa = 0.044715f;
+    const float u = x + kKappa * (x * x * x);
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-kBeta2L * u));
+}
 
 // x * sigmoid(x) on two values: the multiplies / add as packed fp32 ops (v_pk_mul_f32 / v_pk_add_f32),
 // exp2 and rcp per value: the same operations, value by value, as x * rcp(1 + __expf(-x)) (v_mul by
@@ -814,6 +824,9 @@ __device__ __forceinline__ u16x8 epi_apply(u16x8 v, int row, int col, const EpiA
             v[u] = f32_to_bf16(t.x);
             v[u + 1] = f32_to_bf16(t.y);
         }
+    } else if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(epi_gelu(bf16_to_f32(v[u])));
     } else if constexpr (EPI == EPI_RES || EPI == EPI_GATED) {
         const u16x8 r = *reinterpret_cast<const u16x8*>(ea.res + (int64_t)row * ea.ldr + col);
         if constexpr (EPI == EPI_RES) {
@@ -868,6 +881,7 @@ __device__ __forceinline__ void epi_store32_1(unsigned short v, int row, int col
 template <int EPI>
 __device__ __forceinline__ unsigned short epi_apply1(unsigned short v, int row, int col, const EpiArgs& ea) {
     if constexpr (EPI == EPI_SILU) return f32_to_bf16(epi_silu(bf16_to_f32(v)));
+    if constexpr (EPI == EPI_GELU) return f32_to_bf16(epi_gelu(bf16_to_f32(v)));
     if constexpr (EPI == EPI_RES) return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) + bf16_to_f32(v));
     if constexpr (EPI == EPI_GATED)
         return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) +
@@ -898,7 +912,7 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
     constexpr bool E32 = EPI == EPI_RES32 || EPI == EPI_GATED32;
     const bool full = m0 + rbase + 128 <= M && n0 + cbase + 64 <= N && (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0;
-    const bool epi_vec = EPI == EPI_NONE || EPI == EPI_SILU ||
+    const bool epi_vec = EPI == EPI_NONE || EPI == EPI_SILU || EPI == EPI_GELU ||
                          ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
                           ((EPI != EPI_GATED && EPI != EPI_GATED32) ||
                            ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0)));
@@ -1530,7 +1544,7 @@ __device__ __forceinline__ void store_tile_wg(f32x4 (&acc)[8][5], char* smem, in
     __syncthreads();
     constexpr bool E32 = EPI == EPI_RES32 || EPI == EPI_GATED32;
     const bool vec = (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0 &&
-                     (EPI == EPI_NONE || EPI == EPI_SILU ||
+                     (EPI == EPI_NONE || EPI == EPI_SILU || EPI == EPI_GELU ||
                       ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
                        ((EPI != EPI_GATED && EPI != EPI_GATED32) ||
                         ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0))));
@@ -2063,6 +2077,7 @@ static int launch_gemm8_epi(const void* X, int64_t ldx, const void* W, int64_t l
     }
     switch (epi) {
         case EPI_SILU: EGG_GEMM8E_R(EPI_SILU); break;
+        case EPI_GELU: EGG_GEMM8E_R(EPI_GELU); break;
         case EPI_RES: EGG_GEMM8E_R(EPI_RES); break;
         case EPI_GATED: EGG_GEMM8E_R(EPI_GATED); break;
         case EPI_RES32: EGG_GEMM8E_R(EPI_RES32); break;
@@ -2113,6 +2128,7 @@ static int launch_gemm8n(const void* X, int64_t ldx, const void* W, int64_t ldw,
     switch (epi) {
         case EPI_NONE: EGG_GEMM8N_R(EPI_NONE); break;
         case EPI_SILU: EGG_GEMM8N_R(EPI_SILU); break;
+        case EPI_GELU: EGG_GEMM8N_R(EPI_GELU); break;
         case EPI_RES: EGG_GEMM8N_R(EPI_RES); break;
         case EPI_GATED: EGG_GEMM8N_R(EPI_GATED); break;
         case EPI_RES32: EGG_GEMM8N_R(EPI_RES32); break;
@@ -3297,17 +3313,17 @@ int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, i
     if (epi == EPI_NONE)
         return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
                                            rows_per_member, M, N, K, Y, ldy, T_ws, kernel, stream);
-    EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_GATED32, "lora_linear_pop_epi: epi=%d unknown", epi);
+    EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_GELU, "lora_linear_pop_epi: epi=%d unknown", epi);
     EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
     EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
     EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "lora_linear_pop_epi: need K %% 64 == 0");
     EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop_epi: bad strides");
     EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_linear_pop_epi: M/N too large");
-    EGG_CHECK_ARG(epi == EPI_SILU || (res && ldr >= N), "lora_linear_pop_epi: res NULL or ldr < N");
+    EGG_CHECK_ARG(epi == EPI_SILU || epi == EPI_GELU || (res && ldr >= N), "lora_linear_pop_epi: res NULL or ldr < N");
     EGG_CHECK_ARG((epi != EPI_GATED && epi != EPI_GATED32) || (gate && gstride >= N && rows_per_group > 0),
                   "lora_linear_pop_epi: bad gate");
     if (M == 0) return EGGROLL_OK;
-    EGG_CHECK_ARG(X && W && (Y || epi >= EPI_RES32), "lora_linear_pop_epi: NULL pointer");
+    EGG_CHECK_ARG(X && W && (Y || epi == EPI_RES32 || epi == EPI_GATED32), "lora_linear_pop_epi: NULL pointer");
     EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_linear_pop_epi: operand > 2 GiB");
     if (r > 0) {
         EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop_epi: theta_pop / T_ws NULL with r > 0");

@@ -370,7 +370,7 @@ class InfinityPopulationInfer:
         o = F.scaled_dot_product_attention(q, cak, cav, attn_mask=cabias, scale=hd ** -0.5)
         blk.ca.proj(o.transpose(1, 2).reshape(N2 * l, C), epi="res", res=x)
         h = K.rownorm(x, a.norm_eps, layer=True, mscale=mod32[:, 3], mshift=mod32[:, 5], rows_per_group=l)
-        f = F.gelu(blk.ffn.fc1(h), approximate="tanh")
+        f = blk.ffn.fc1(h, epi="gelu")          # GELU(tanh) in the GEMM epilogue where it applies
         blk.ffn.fc2(f, epi="gated", res=x, gate=mod16[:, 1], rows_per_group=l)
 
     @torch.no_grad()

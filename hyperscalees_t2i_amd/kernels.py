@@ -301,7 +301,7 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
     return out
 
 
-EPI = {None: 0, "silu": 1, "res": 2, "gated": 3, "res32": 4, "gated32": 5}
+EPI = {None: 0, "silu": 1, "res": 2, "gated": 3, "res32": 4, "gated32": 5, "gelu": 6}
 
 
 def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], theta_pop: Optional[torch.Tensor],
@@ -310,7 +310,7 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
                         rows_per_group: int = 1, out: Optional[torch.Tensor] = None,
                         T_ws: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
     """lora_linear_pop with an epilogue op on the bf16 output y (eggroll_lora_linear_pop_epi_sel):
-    "silu": silu(y); "res": res + y; "gated": res + gate[row // rows_per_group] * y.  With res given and
+    "silu": silu(y); "gelu": gelu(y, approximate="tanh"); "res": res + y; "gated": res + gate[row // rows_per_group] * y.  With res given and
     out None the result is written into res (in place, as the residual adds it replaces).
     "res32" / "gated32": res is the fp32 residual stream, updated in place (res + y /
     fma(gate, y, res), gate fp32); out (optional) receives its bf16 shadow; returns res.
@@ -320,11 +320,12 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
     M, Kd = x.shape
     N = W.shape[0]
     code = EPI[epi]
+    f32res = code in (4, 5)
     if res is not None:
-        _dev(res, "lora_linear_pop_epi(res)", torch.float32 if code >= 4 else torch.bfloat16)
+        _dev(res, "lora_linear_pop_epi(res)", torch.float32 if f32res else torch.bfloat16)
         if res.shape[-1] != N or res.numel() != M * N:
             raise ValueError(f"res {tuple(res.shape)} does not match [{M}, {N}]")
-    if code >= 4:
+    if f32res:
         if res is None or (code == 5 and (gate is None or gate.dtype != torch.float32)):
             raise ValueError(f"lora_linear_pop_epi({epi}): needs an fp32 res (and an fp32 gate)")
         if out is not None:
@@ -341,7 +342,7 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
               _p(theta_pop) if r > 0 else None, theta_pop.stride(0) if r > 0 else 0, offA, offB, r, float(scale),
               rows_per_member, M, N, Kd, _p(out), N, _p(T_ws) if r > 0 else None, code,
               _p(res), N if res is not None else 0, pg, gst or N, int(rows_per_group), int(kernel), _stream(x.device))
-    return res if code >= 4 else out
+    return res if f32res else out
 
 
 def lora_workspace_numel(M: int, K: int, r: int, rows_per_member: int) -> int:

@@ -159,16 +159,18 @@ class LoRALinear(nn.Module):
         ctx = self.ctx
         if M * self.in_features * 2 >= GEMM_OPERAND_LIMIT:   # the GEMMs address X with 32-bit buffer offsets
             return self._forward_chunked(x2, shp, epi, res, gate, rows_per_group, T, shadow)
-        if epi == "silu":   # silu of the bf16-rounded output, in the GEMM epilogue where it applies
+        if epi in ("silu", "gelu"):   # silu / gelu(tanh) of the bf16-rounded output, in the GEMM epilogue where it applies
             if (FUSE_EPILOGUES and ctx is not None and ctx.theta_pop is not None and self.r <= 2 and not GemmTimer.active
                     and M % ctx.n_members == 0 and (self.r == 0 or M // ctx.n_members >= 256)
                     and self.in_features % 64 == 0):
                 rpm = M // ctx.n_members
                 ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device) if self.r else None
                 y = K.lora_linear_pop_epi(x2, self.weight, self.bias, ctx.theta_pop if self.r else None,
-                                          self.theta_off_A, self.theta_off_B, self.r, self.scale, rpm, "silu", T_ws=ws)
-            else:
+                                          self.theta_off_A, self.theta_off_B, self.r, self.scale, rpm, epi, T_ws=ws)
+            elif epi == "silu":
                 y = torch.nn.functional.silu(self.forward(x).view(M, self.out_features))
+            else:
+                y = torch.nn.functional.gelu(self.forward(x).view(M, self.out_features), approximate="tanh")
             return y.view(*shp[:-1], self.out_features)
         if epi is not None:
             res2 = res.view(M, self.out_features)
