@@ -144,6 +144,7 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
  *   epi 3: Y = bf16(res + gate[row/rpg, :] * y)    x += gate_msa * attn1(...) (eggroll_gated_residual)
  *   epi 4: res = res + y                           the same on the fp32 residual stream (res fp32)
  *   epi 5: res = fma(gate[row/rpg, :], y, res)     (res fp32, gate fp32; eggroll_gated_residual_f32)
+ *   epi 6: Y = bf16(gelu_tanh(y))                  Infinity ffn fc1 -> GELU(tanh) (x * sigmoid(2k), <= 1 ulp)
  * res [M, ldr] bf16 may alias Y; gate rows gstride apart.  epi 4 / 5: res is an fp32 stream updated in
  * place and Y (may be NULL) receives bf16(res).  Requires r <= 2 (and rows_per_member >= 256 when
  * r > 0) and K % 64 == 0: always an MFMA-addend 8-phase kernel.  epi 0 = linear_pop.               */
@@ -371,6 +372,7 @@ int eggroll_linear_attention(const void* q, const void* k, const void* v, int64_
  * CLIPImageProcessor (PIL backend) on the PIL image the reference builds (rewards.py:86-90,133-147):
  *   u8 = mode 0: rint((x/2 + 0.5).clamp(0,1) * 255)    (PixArtImageProcessor.postprocess, Sana)
  *        mode 1: fp16 ((x+1)*0.5).clamp(0,1) * 255, truncated  (models/VAR.py:190, 245-259)
+ *        mode 2: bf16 (x+1)/2*255, clamped, truncated        (Infinity's image postprocess)
  *   Pillow BICUBIC 8-bit fixed-point resize to RH x RW (horizontal pass first, clip8 per pass),
  *   center crop out_size^2, out = (u8/255 - mean[c]) / std[c]  fp32 [n, 3, out, out].
  * img: bf16, element (i, c, y, x) at img[i*sn + c*sc + y*sh + x*sw]; tab_w [RW][1+ktw] / tab_h
