@@ -1753,6 +1753,212 @@ extern "C" int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, in
     return EGGROLL_OK;
 }
 
+// ------------------------------------------------------------------------------------
+// Flash attention, head dim 128 (Z-Image self-attention; Infinity's cosine attention over the KV cache):
+//   o[b, n, h, :] = softmax_j(scale * q[b,n,h,:] . k[b,j,h,:]) @ v[b, :, h, :],  j < Lk, no mask.
+// q / k / v / o: [B][rows][heads * 128] bf16 views with their own batch and row strides (a KV cache
+// [B][ltot][C] is read in place).  Workgroup = (b, h, 128-query block), 4 waves x 32 queries; keys in
+// blocks of 64 staged in LDS (k and v [64][136] bf16), the next block held in registers while this one
+// computes.  Per key block and wave, MFMA 16x16x32 bf16, fp32 accumulation, the k_cross_attn layout:
+//   S^T = K Q^T   (Q^T fragments stay in registers for the whole key sweep; each lane: 4 keys of ONE query)
+//   online softmax in base 2: m' = max(m, rowmax), O *= 2^(m - m'), P = 2^(S - m'), per-lane partial row
+//                 sums rescaled the same way and reduced over the 4 lane groups once at the end
+//   O^T += V^T P^T  (P^T packed from the C registers, V^T read with ds_read_tr16_b64 in the matching key order)
+// ------------------------------------------------------------------------------------
+constexpr int FA_HD = 128, FA_KB = 64, FA_RS = FA_HD + 8;
+
+template <int QF>
+__global__ __launch_bounds__(256, QF == 2 ? 2 : 1) void k_flash_attn(const unsigned short* __restrict__ q, int64_t q_bs, int64_t ldq,
+                                                    const unsigned short* __restrict__ k, int64_t k_bs, int64_t ldk,
+                                                    const unsigned short* __restrict__ v, int64_t v_bs, int64_t ldv,
+                                                    int heads, int Nq, int Lk, int nqb, float scale_log2,
+                                                    unsigned short* __restrict__ o, int64_t o_bs, int64_t ldo) {
+    constexpr int QW = 16 * QF, KSN = FA_HD / 32, DF = FA_HD / 16, KF = FA_KB / 16, CH = FA_HD / 8;
+    constexpr int UNITS = 2 * FA_KB * CH / 256;   // 16-B chunks of k + v per thread per key block (8)
+    __shared__ __attribute__((aligned(16))) unsigned short sk[FA_KB * FA_RS];
+    __shared__ __attribute__((aligned(16))) unsigned short sv[FA_KB * FA_RS];
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int qb = bid % nqb, bh = bid / nqb;
+    const int b = bh / heads, h = bh - b * heads;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+    const unsigned short* kb_ = k + (int64_t)b * k_bs + (int64_t)h * FA_HD;
+    const unsigned short* vb_ = v + (int64_t)b * v_bs + (int64_t)h * FA_HD;
+    // Q^T fragments (B operand): dims 32 ks + 8 g .. +7 of query 16 x + r16 of this wave's 32
+    la_bf16x8 bq[QF][KSN];
+    const int q0 = qb * (4 * QW) + w * QW;
+#pragma unroll
+    for (int x = 0; x < QF; ++x) {
+        const int qr = q0 + 16 * x + r16;
+#pragma unroll
+        for (int ks = 0; ks < KSN; ++ks) {
+            u16x8m t = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+            if (qr < Nq)
+                t = *reinterpret_cast<const u16x8m*>(q + (int64_t)b * q_bs + (int64_t)qr * ldq + (int64_t)h * FA_HD +
+                                                     32 * ks + 8 * g);
+            bq[x][ks] = __builtin_bit_cast(la_bf16x8, t);
+        }
+    }
+    u16x8m pre[UNITS];
+    auto load_blk = [&](int key0) {
+#pragma unroll
+        for (int i = 0; i < UNITS; ++i) {
+            const int c = tid + 256 * i;             // [k | v][row][chunk]
+            const int kv = c / (FA_KB * CH), rc = c - kv * (FA_KB * CH);
+            const int r = rc / CH, cc = rc - r * CH;
+            pre[i] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+            if (key0 + r < Lk) {
+                const unsigned short* src = kv ? vb_ + (int64_t)(key0 + r) * ldv : kb_ + (int64_t)(key0 + r) * ldk;
+                pre[i] = *reinterpret_cast<const u16x8m*>(src + cc * 8);
+            }
+        }
+    };
+    auto store_blk = [&]() {
+#pragma unroll
+        for (int i = 0; i < UNITS; ++i) {
+            const int c = tid + 256 * i;
+            const int kv = c / (FA_KB * CH), rc = c - kv * (FA_KB * CH);
+            const int r = rc / CH, cc = rc - r * CH;
+            *reinterpret_cast<u16x8m*>((kv ? sv : sk) + r * FA_RS + cc * 8) = pre[i];
+        }
+    };
+    la_f32x4 oc[QF][DF];
+    float m[QF], l[QF];
+#pragma unroll
+    for (int x = 0; x < QF; ++x) {
+        m[x] = -INFINITY;
+        l[x] = 0.0f;
+#pragma unroll
+        for (int d = 0; d < DF; ++d) oc[x][d] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int nkb = (Lk + FA_KB - 1) / FA_KB;
+    load_blk(0);
+    for (int kb = 0; kb < nkb; ++kb) {
+        __syncthreads();   // every wave is done reading the previous block
+        store_blk();
+        __syncthreads();
+        if (kb + 1 < nkb) load_blk((kb + 1) * FA_KB);   // in flight under this block's MFMAs
+        la_f32x4 sf[QF][KF];
+#pragma unroll
+        for (int f = 0; f < KF; ++f) {
+#pragma unroll
+            for (int x = 0; x < QF; ++x) sf[x][f] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KSN; ++ks) {
+                const la_bf16x8 a = *reinterpret_cast<const la_bf16x8*>(sk + (16 * f + r16) * FA_RS + 32 * ks + 8 * g);
+#pragma unroll
+                for (int x = 0; x < QF; ++x) sf[x][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[x][ks], sf[x][f], 0, 0, 0);
+            }
+        }
+        const int key0 = kb * FA_KB;
+        float mb[QF];
+#pragma unroll
+        for (int x = 0; x < QF; ++x) mb[x] = -INFINITY;
+#pragma unroll
+        for (int f = 0; f < KF; ++f)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = key0 + 16 * f + 4 * g + e < Lk;
+#pragma unroll
+                for (int x = 0; x < QF; ++x) {
+                    const float t = ok ? sf[x][f][e] * scale_log2 : -INFINITY;
+                    sf[x][f][e] = t;
+                    mb[x] = fmaxf(mb[x], t);
+                }
+            }
+#pragma unroll
+        for (int x = 0; x < QF; ++x) {
+            mb[x] = fmaxf(mb[x], __shfl_xor(mb[x], 16));
+            mb[x] = fmaxf(mb[x], __shfl_xor(mb[x], 32));
+            const float mn = fmaxf(m[x], mb[x]);
+            const float alpha = __builtin_amdgcn_exp2f(m[x] - mn);   // 0 on the first block (m = -inf)
+            m[x] = mn;
+            l[x] *= alpha;
+#pragma unroll
+            for (int d = 0; d < DF; ++d)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) oc[x][d][e] *= alpha;
+#pragma unroll
+            for (int f = 0; f < KF; ++f)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float pe = __builtin_amdgcn_exp2f(sf[x][f][e] - mn);
+                    sf[x][f][e] = pe;
+                    l[x] += pe;
+                }
+        }
+#pragma unroll
+        for (int j = 0; j < KF / 2; ++j) {
+            la_bf16x8 bp[QF];
+#pragma unroll
+            for (int x = 0; x < QF; ++x)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    bp[x][e] = (__bf16)sf[x][2 * j][e];
+                    bp[x][4 + e] = (__bf16)sf[x][2 * j + 1][e];
+                }
+#pragma unroll
+            for (int d = 0; d < DF; ++d) {
+                const la_bf16x8 av = xa_tr8_perm<FA_RS>(sv + (32 * j) * FA_RS + 16 * d, lane);
+#pragma unroll
+                for (int x = 0; x < QF; ++x) oc[x][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bp[x], oc[x][d], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int x = 0; x < QF; ++x) {
+        float sum = l[x];
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        const int qr = q0 + 16 * x + r16;
+        if (qr < Nq) {
+            const float inv = 1.0f / sum;
+            unsigned short* dst = o + (int64_t)b * o_bs + (int64_t)qr * ldo + (int64_t)h * FA_HD + 4 * g;
+#pragma unroll
+            for (int d = 0; d < DF; ++d) {
+                u16x4m t;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t[e] = f2b(oc[x][d][e] * inv);
+                *reinterpret_cast<u16x4m*>(dst + 16 * d) = t;
+            }
+        }
+    }
+}
+
+extern "C" int eggroll_flash_attention_sel(const void* q, int64_t q_bs, int64_t ldq, const void* k, int64_t k_bs,
+                                           int64_t ldk, const void* v, int64_t v_bs, int64_t ldv, int64_t B,
+                                           int64_t heads, int64_t Nq, int64_t Lk, int64_t head_dim, float scale, void* o,
+                                           int64_t o_bs, int64_t ldo, int32_t qf, void* stream) {
+    EGG_CHECK_ARG(qf == 0 || qf == 2 || qf == 4, "flash_attention: qf must be 0 (auto), 2 or 4");
+    if (qf == 0) qf = 2;
+    EGG_CHECK_ARG(head_dim == FA_HD, "flash_attention: head_dim %lld unsupported (128)", (long long)head_dim);
+    EGG_CHECK_ARG(B >= 0 && heads > 0 && Nq >= 0 && Lk >= 1, "flash_attention: bad sizes");
+    EGG_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0 && q_bs % 8 == 0 && k_bs % 8 == 0 &&
+                  v_bs % 8 == 0 && o_bs % 4 == 0 && ldq >= heads * FA_HD && ldk >= heads * FA_HD &&
+                  ldv >= heads * FA_HD && ldo >= heads * FA_HD, "flash_attention: bad strides");
+    if (B == 0 || Nq == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(q && k && v && o, "flash_attention: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)q & 15) == 0 && ((uintptr_t)k & 15) == 0 && ((uintptr_t)v & 15) == 0 && ((uintptr_t)o & 7) == 0,
+                  "flash_attention: q/k/v must be 16-byte aligned, o 8-byte aligned");
+    EGG_CHECK_ARG(Nq < (1ll << 31) && Lk < (1ll << 31), "flash_attention: sequence too long");
+    const int64_t qwg = 4 * 16 * qf, nqb = (Nq + qwg - 1) / qwg;
+    EGG_CHECK_ARG(B * heads * nqb < (1ll << 31), "flash_attention: grid too large");
+    auto* kern = qf == 4 ? k_flash_attn<4> : k_flash_attn<2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(B * heads * nqb)), dim3(256), 0, as_stream(stream),
+                       (const unsigned short*)q, q_bs, ldq, (const unsigned short*)k, k_bs, ldk,
+                       (const unsigned short*)v, v_bs, ldv, (int)heads, (int)Nq, (int)Lk, (int)nqb,
+                       scale * 1.4426950408889634f, (unsigned short*)o, o_bs, ldo);
+    EGG_CHECK_LAUNCH("flash_attention");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_flash_attention(const void* q, int64_t q_bs, int64_t ldq, const void* k, int64_t k_bs,
+                                       int64_t ldk, const void* v, int64_t v_bs, int64_t ldv, int64_t B, int64_t heads,
+                                       int64_t Nq, int64_t Lk, int64_t head_dim, float scale, void* o, int64_t o_bs,
+                                       int64_t ldo, void* stream) {
+    return eggroll_flash_attention_sel(q, q_bs, ldq, k, k_bs, ldk, v, v_bs, ldv, B, heads, Nq, Lk, head_dim, scale, o,
+                                       o_bs, ldo, 0, stream);
+}
+
 extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
                                        const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
                                        int64_t heads, int64_t head_dim, int64_t L, int64_t U, float scale, void* o,

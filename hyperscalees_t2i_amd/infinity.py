@@ -18,8 +18,8 @@ MI355X layout: all members of a pass, both CFG halves and all images in ONE batc
 member-major ([member][cond | uncond][image][token]) so every linear is one libeggroll population
 GEMM (fc1 carries the per-member LoRA; sa.proj / ffn.fc2 fold the gated residual and ca.proj the
 residual add into their epilogues); q / k L2 norm + 2-D RoPE in one in-place pass
-(eggroll_qk_norm_rope); the per-block KV cache [2, rows, tokens, C] preallocated for the whole
-schedule; everything text-side (member-independent: no LoRA there) computed once per distinct
+(eggroll_qk_norm_rope); attention over the per-block KV cache [2, rows, tokens, C] (preallocated for
+the whole schedule, read in place) on eggroll_flash_attention; everything text-side (member-independent: no LoRA there) computed once per distinct
 prompt.  The reference's generator semantics are kept per micro-batch (es_backend.py:951-1022: every
 micro-batch call reseeds with the same seed), so member k's bits equal those of the reference's own
 per-member calls given the same logits.
@@ -306,7 +306,7 @@ class InfinityPopulationInfer:
 
     def __init__(self, tr: InfinityTransformer, vae: FluxVAEDecoder):
         self.tr, self.vae = tr, vae
-        self.use_kernel = True    # eggroll_qk_norm_rope for head dim 128 (False: the torch form)
+        self.use_kernel = True    # eggroll_qk_norm_rope + eggroll_flash_attention at head dim 128 (False: torch forms)
 
     # ---- text side (member-independent) ------------------------------------------------
     def _text(self, kv_list: Sequence[torch.Tensor], lens: Sequence[int]):
@@ -358,10 +358,13 @@ class InfinityPopulationInfer:
         q = (qkv.view(N2, l, 3, H, hd)[:, :, 0] * qs.view(1, 1, H, 1).to(torch.bfloat16))
         kv[0, :, cur:cur + l] = k2.view(N2, l, C)
         kv[1, :, cur:cur + l] = qkv.view(N2, l, 3, C)[:, :, 2]
-        ks = kv[0, :, :cur + l].view(N2, cur + l, H, hd).transpose(1, 2)
-        vs = kv[1, :, :cur + l].view(N2, cur + l, H, hd).transpose(1, 2)
-        o = F.scaled_dot_product_attention(q.transpose(1, 2), ks, vs, scale=1.0)
-        o = o.transpose(1, 2).reshape(N2 * l, C)
+        ks = kv[0, :, :cur + l].view(N2, cur + l, H, hd)
+        vs = kv[1, :, :cur + l].view(N2, cur + l, H, hd)
+        if self.use_kernel and hd == 128:     # eggroll_flash_attention reads the cache in place
+            o = K.flash_attention(q, ks, vs, 1.0).view(N2 * l, C)
+        else:
+            o = F.scaled_dot_product_attention(q.transpose(1, 2), ks.transpose(1, 2), vs.transpose(1, 2), scale=1.0)
+            o = o.transpose(1, 2).reshape(N2 * l, C)
         sa.proj(o, epi="gated", res=x, gate=mod16[:, 0], rows_per_group=l)
         # cross-attention to the text (keys: this row's prompt, cond or uncond)
         cn = blk.ca_norm

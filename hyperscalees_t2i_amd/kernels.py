@@ -938,3 +938,28 @@ def cross_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, N
     OpTimer.end(e0, "cross_attention", 2.0 * (2 * B * N * heads * head_dim + 2 * k.shape[0] * heads * head_dim),
                 f"B{B} N{N} L{L}")
     return out
+
+
+def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float,
+                    out: Optional[torch.Tensor] = None, qf: int = 0) -> torch.Tensor:
+    """softmax(scale * q k^T) v on MFMA (eggroll_flash_attention), head dim 128, no mask.  q [B, Nq, H, 128],
+    k / v [B, Lk, H, 128] bf16 views with unit inner stride and heads 128 apart (batch and row strides
+    free: a KV-cache slice is read in place).  Returns [B, Nq, H, 128] bf16 (or writes `out`)."""
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        if t.device.type != "cuda" or t.dtype != torch.bfloat16 or t.dim() != 4 or t.stride(3) != 1 or t.stride(2) != 128:
+            raise _lib.EggrollError(f"flash_attention({nm}): expected a bf16 device view [B, S, H, 128] with heads "
+                                    f"128 apart, got {tuple(t.shape)} / {t.stride()}")
+    B, Nq, H, D = q.shape
+    if D != 128 or k.shape[0] != B or v.shape[0] != B or k.shape[2] != H or v.shape[2] != H or k.shape[1] != v.shape[1]:
+        raise ValueError(f"flash_attention: q {tuple(q.shape)}, k {tuple(k.shape)}, v {tuple(v.shape)}")
+    if out is None:
+        out = torch.empty((B, Nq, H, D), dtype=torch.bfloat16, device=q.device)
+    elif out.dtype != torch.bfloat16 or out.stride(3) != 1 or out.stride(2) != 128 or tuple(out.shape) != (B, Nq, H, D):
+        raise ValueError("flash_attention: out must be a bf16 [B, Nq, H, 128] view with heads 128 apart")
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_flash_attention_sel", q.data_ptr(), q.stride(0), q.stride(1), k.data_ptr(), k.stride(0),
+              k.stride(1), v.data_ptr(), v.stride(0), v.stride(1), B, H, Nq, k.shape[1], 128, float(scale), out.data_ptr(),
+              out.stride(0), out.stride(1), int(qf), _stream(q.device))
+    OpTimer.end(e0, "flash_attention", 2.0 * B * H * 128 * (2 * Nq + 2 * k.shape[1]), f"B{B} Nq{Nq} Lk{k.shape[1]} h{H}",
+                flops=4.0 * B * H * Nq * k.shape[1] * 128)
+    return out

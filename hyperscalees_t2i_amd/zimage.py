@@ -16,7 +16,8 @@ throughput of configs[3] depends on.
 
 Every linear runs on libeggroll's population GEMM (LoRA'd or plain); the q/k norm + RoPE on
 `eggroll_qk_norm_rope` (one in-place pass per tensor); every RMSNorm / modulation / gated residual on
-`eggroll_rownorm`; attention on SDPA; the FFN's silu(w1 x) on the GEMM's SiLU epilogue.
+`eggroll_rownorm`; attention on `eggroll_flash_attention` (head dim 128, no mask); the FFN's
+silu(w1 x) on the GEMM's SiLU epilogue.
 """
 from __future__ import annotations
 
@@ -104,7 +105,7 @@ class ZAttention(nn.Module):
         self.norm_q = RMSNorm(a.head_dim, a.norm_eps)
         self.norm_k = RMSNorm(a.head_dim, a.norm_eps)
         self.to_out = nn.ModuleList([LoRALinear(a.dim, a.dim, bias=False, lora=False)])
-        self.use_kernel = True   # eggroll_qk_norm_rope; False: rownorm + torch rotation (A/B, tests)
+        self.use_kernel = True   # eggroll_qk_norm_rope + eggroll_flash_attention; False: torch forms (A/B, tests)
 
     def forward(self, x, cos, sin, n_rep: int, key_bias: Optional[torch.Tensor]):
         """x [B, S, dim]; key_bias [B, 1, 1, S] additive (batch padding) or None."""
@@ -122,6 +123,9 @@ class ZAttention(nn.Module):
             q = apply_rope(q.view(B, S, self.heads, self.hd), cos, sin, n_rep)
             k = apply_rope(k.view(B, S, self.heads, self.hd), cos, sin, n_rep)
         v = self.to_v(x, T=Tv).view(B, S, self.heads, self.hd)
+        if self.use_kernel and self.hd == 128 and key_bias is None:   # eggroll_flash_attention
+            o = K.flash_attention(q, k, v, self.hd ** -0.5)
+            return self.to_out[0](o.view(B, S, D))
         o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
                                            attn_mask=key_bias, scale=self.hd ** -0.5)
         return self.to_out[0](o.transpose(1, 2).reshape(B, S, D))

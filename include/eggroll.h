@@ -394,6 +394,20 @@ int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const voi
                             const int32_t* enc_index, int64_t B, int64_t N, int64_t heads, int64_t head_dim,
                             int64_t L, int64_t U, float scale, void* o, int64_t ldo, void* stream);
 
+/* Flash attention, head dim 128, no mask (Z-Image self-attention, Infinity's attention over its KV cache):
+ *   o[b,n,h,:] = softmax_j(scale * q[b,n,h,:] . k[b,j,h,:]) @ v[b,:,h,:],  n < Nq, j < Lk
+ * q / k / v / o bf16, element (b, row, h, d) at X[b * X_bs + row * ldX + h * 128 + d] (a KV cache read in
+ * place through its batch stride).  Online softmax in fp32, P rounded to bf16 for the PV MFMA.         */
+int eggroll_flash_attention(const void* q, int64_t q_bs, int64_t ldq, const void* k, int64_t k_bs, int64_t ldk,
+                            const void* v, int64_t v_bs, int64_t ldv, int64_t B, int64_t heads, int64_t Nq,
+                            int64_t Lk, int64_t head_dim, float scale, void* o, int64_t o_bs, int64_t ldo,
+                            void* stream);
+/* The same with the queries per wave chosen (qf 2: 32, qf 4: 64; 0: automatic) — A/B measurement. */
+int eggroll_flash_attention_sel(const void* q, int64_t q_bs, int64_t ldq, const void* k, int64_t k_bs, int64_t ldk,
+                                const void* v, int64_t v_bs, int64_t ldv, int64_t B, int64_t heads, int64_t Nq,
+                                int64_t Lk, int64_t head_dim, float scale, void* o, int64_t o_bs, int64_t ldo, int32_t qf,
+                                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1228,3 +1228,27 @@ def test_dcae_high_res_chunking_is_exact(dev, fp32_stages):
         want = torch.cat([vae(z[s:s + 2]) for s in range(0, 6, 2)])
     assert got.shape == want.shape
     assert (got.float() - want.float()).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("B,Nq,Lk,H,strided", [(2, 676, 676, 3, False), (3, 1, 1, 2, False), (2, 100, 2521, 2, True),
+                                               (1, 257, 130, 1, True), (4, 64, 64, 2, False)])
+def test_flash_attention_vs_sdpa(dev, B, Nq, Lk, H, strided):
+    """eggroll_flash_attention (head dim 128, online softmax over 64-key blocks, P in bf16 for the PV MFMA) vs
+    fp32 SDPA on the same bf16 inputs; k / v optionally a slice of a longer [B, ltot, H*128] cache (batch
+    stride != rows * row stride), ragged query / key counts."""
+    g = torch.Generator(device=dev).manual_seed(Nq * 7 + Lk)
+    q = (torch.randn(B, Nq, H, 128, generator=g, device=dev) * 0.3).bfloat16()
+    if strided:
+        cache = (torch.randn(2, B, Lk + 37, H * 128, generator=g, device=dev) * 0.3).bfloat16()
+        k = cache[0, :, :Lk].view(B, Lk, H, 128)
+        v = cache[1, :, :Lk].view(B, Lk, H, 128)
+    else:
+        k = (torch.randn(B, Lk, H, 128, generator=g, device=dev) * 0.3).bfloat16()
+        v = torch.randn(B, Lk, H, 128, generator=g, device=dev).bfloat16()
+    scale = 128 ** -0.5 * 3
+    got = K.flash_attention(q, k, v, scale).float()
+    ref = torch.nn.functional.scaled_dot_product_attention(q.float().transpose(1, 2), k.float().transpose(1, 2),
+                                                           v.float().transpose(1, 2), scale=scale).transpose(1, 2)
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+    assert (got - ref).abs().max().item() < 0.05
