@@ -781,7 +781,8 @@ __device__ __forceinline__ void lora_epilogue(f32x4 (&acc)[WTM / 16][WTN / 16], 
 //   EPI_GATED32 : res = fma(gate32[row / rpg], float(y), res)  (x += gate * attn1(...); gate fp32)
 // The same expressions as eggroll_gated_residual_f32, so fused == unfused bit for bit.
 //   EPI_GELU  : out = bf16(gelu_tanh(y))                   (Infinity / VAR ffn: fc1 -> GELU(tanh))
-enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3, EPI_RES32 = 4, EPI_GATED32 = 5, EPI_GELU = 6 };
+//   EPI_MUL   : out = bf16(res * y)                        (Z-Image SwiGLU: silu(w1 x) * w3 x)
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3, EPI_RES32 = 4, EPI_GATED32 = 5, EPI_GELU = 6, EPI_MUL = 7 };
 struct EpiArgs {
     const unsigned short* res;
     int64_t ldr;
@@ -827,9 +828,12 @@ __device__ __forceinline__ u16x8 epi_apply(u16x8 v, int row, int col, const EpiA
     } else if constexpr (EPI == EPI_GELU) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(epi_gelu(bf16_to_f32(v[u])));
-    } else if constexpr (EPI == EPI_RES || EPI == EPI_GATED) {
+    } else if constexpr (EPI == EPI_RES || EPI == EPI_GATED || EPI == EPI_MUL) {
         const u16x8 r = *reinterpret_cast<const u16x8*>(ea.res + (int64_t)row * ea.ldr + col);
-        if constexpr (EPI == EPI_RES) {
+        if constexpr (EPI == EPI_MUL) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(bf16_to_f32(r[u]) * bf16_to_f32(v[u]));
+        } else if constexpr (EPI == EPI_RES) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(bf16_to_f32(r[u]) + bf16_to_f32(v[u]));
         } else {
@@ -883,6 +887,7 @@ __device__ __forceinline__ unsigned short epi_apply1(unsigned short v, int row, 
     if constexpr (EPI == EPI_SILU) return f32_to_bf16(epi_silu(bf16_to_f32(v)));
     if constexpr (EPI == EPI_GELU) return f32_to_bf16(epi_gelu(bf16_to_f32(v)));
     if constexpr (EPI == EPI_RES) return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) + bf16_to_f32(v));
+    if constexpr (EPI == EPI_MUL) return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) * bf16_to_f32(v));
     if constexpr (EPI == EPI_GATED)
         return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) +
                            bf16_to_f32(ea.gate[(row / ea.rpg) * ea.gstride + col]) * bf16_to_f32(v));
@@ -2078,6 +2083,7 @@ static int launch_gemm8_epi(const void* X, int64_t ldx, const void* W, int64_t l
     switch (epi) {
         case EPI_SILU: EGG_GEMM8E_R(EPI_SILU); break;
         case EPI_GELU: EGG_GEMM8E_R(EPI_GELU); break;
+        case EPI_MUL: EGG_GEMM8E_R(EPI_MUL); break;
         case EPI_RES: EGG_GEMM8E_R(EPI_RES); break;
         case EPI_GATED: EGG_GEMM8E_R(EPI_GATED); break;
         case EPI_RES32: EGG_GEMM8E_R(EPI_RES32); break;
@@ -2101,7 +2107,7 @@ static int gemm8_auto(int64_t M, int64_t N, int32_t r, int64_t rows_per_member, 
     // the bf16 residual epilogues stay on 8 (their per-chunk loads slow kernel 10's store phase); the fp32
     // ones load in batches and run equal (to_out) or 3 % faster (FFN point conv, K 5632) on 10
     // (profiles/r05h_epi32_kernel8_vs_10_ab.log)
-    if (!gemm8n_ok(r, rows_per_member) || epi == EPI_RES || epi == EPI_GATED) return 8;
+    if (!gemm8n_ok(r, rows_per_member) || epi == EPI_RES || epi == EPI_GATED || epi == EPI_MUL) return 8;
     const int64_t tm = (M + 255) / 256;
     const int64_t rounds8 = (tm * ((N + 255) / 256) + 255) / 256, rounds10 = (tm * ((N + 319) / 320) + 255) / 256;
     return 122 * rounds10 < 100 * rounds8 ? 10 : 8;
@@ -2129,6 +2135,7 @@ static int launch_gemm8n(const void* X, int64_t ldx, const void* W, int64_t ldw,
         case EPI_NONE: EGG_GEMM8N_R(EPI_NONE); break;
         case EPI_SILU: EGG_GEMM8N_R(EPI_SILU); break;
         case EPI_GELU: EGG_GEMM8N_R(EPI_GELU); break;
+        case EPI_MUL: EGG_GEMM8N_R(EPI_MUL); break;
         case EPI_RES: EGG_GEMM8N_R(EPI_RES); break;
         case EPI_GATED: EGG_GEMM8N_R(EPI_GATED); break;
         case EPI_RES32: EGG_GEMM8N_R(EPI_RES32); break;
@@ -3313,7 +3320,7 @@ int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, i
     if (epi == EPI_NONE)
         return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
                                            rows_per_member, M, N, K, Y, ldy, T_ws, kernel, stream);
-    EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_GELU, "lora_linear_pop_epi: epi=%d unknown", epi);
+    EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_MUL, "lora_linear_pop_epi: epi=%d unknown", epi);
     EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
     EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
     EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "lora_linear_pop_epi: need K %% 64 == 0");

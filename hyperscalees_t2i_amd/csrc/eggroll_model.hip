@@ -1805,11 +1805,11 @@ __global__ __launch_bounds__(256, QF == 2 ? 2 : 1) void k_flash_attn(const unsig
             const int c = tid + 256 * i;             // [k | v][row][chunk]
             const int kv = c / (FA_KB * CH), rc = c - kv * (FA_KB * CH);
             const int r = rc / CH, cc = rc - r * CH;
-            pre[i] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
-            if (key0 + r < Lk) {
-                const unsigned short* src = kv ? vb_ + (int64_t)(key0 + r) * ldv : kb_ + (int64_t)(key0 + r) * ldk;
-                pre[i] = *reinterpret_cast<const u16x8m*>(src + cc * 8);
-            }
+            // branch-free: rows past Lk read the last key (in bounds) and are zeroed by a select
+            const int row = min(key0 + r, Lk - 1);
+            const unsigned short* src = kv ? vb_ + (int64_t)row * ldv : kb_ + (int64_t)row * ldk;
+            const u16x8m t = *reinterpret_cast<const u16x8m*>(src + cc * 8);
+            pre[i] = key0 + r < Lk ? t : u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
         }
     };
     auto store_blk = [&]() {
@@ -1841,30 +1841,44 @@ __global__ __launch_bounds__(256, QF == 2 ? 2 : 1) void k_flash_attn(const unsig
 #pragma unroll
         for (int f = 0; f < KF; ++f) {
 #pragma unroll
-            for (int x = 0; x < QF; ++x) sf[x][f] = la_f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
             for (int ks = 0; ks < KSN; ++ks) {
                 const la_bf16x8 a = *reinterpret_cast<const la_bf16x8*>(sk + (16 * f + r16) * FA_RS + 32 * ks + 8 * g);
+                // the first k-step takes a literal zero accumulator (no per-block zeroing of 32 registers)
 #pragma unroll
-                for (int x = 0; x < QF; ++x) sf[x][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[x][ks], sf[x][f], 0, 0, 0);
+                for (int x = 0; x < QF; ++x)
+                    sf[x][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[x][ks], ks ? sf[x][f] : la_f32x4{0.f, 0.f, 0.f, 0.f},
+                                                                       0, 0, 0);
             }
         }
         const int key0 = kb * FA_KB;
         float mb[QF];
 #pragma unroll
         for (int x = 0; x < QF; ++x) mb[x] = -INFINITY;
+        if (key0 + FA_KB <= Lk) {   // full block (uniform branch): no key mask
 #pragma unroll
-        for (int f = 0; f < KF; ++f)
+            for (int f = 0; f < KF; ++f)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const bool ok = key0 + 16 * f + 4 * g + e < Lk;
+                for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int x = 0; x < QF; ++x) {
-                    const float t = ok ? sf[x][f][e] * scale_log2 : -INFINITY;
-                    sf[x][f][e] = t;
-                    mb[x] = fmaxf(mb[x], t);
+                    for (int x = 0; x < QF; ++x) {
+                        const float t = sf[x][f][e] * scale_log2;
+                        sf[x][f][e] = t;
+                        mb[x] = fmaxf(mb[x], t);
+                    }
+        } else {
+#pragma unroll
+            for (int f = 0; f < KF; ++f)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const bool ok = key0 + 16 * f + 4 * g + e < Lk;
+#pragma unroll
+                    for (int x = 0; x < QF; ++x) {
+                        const float t = ok ? sf[x][f][e] * scale_log2 : -INFINITY;
+                        sf[x][f][e] = t;
+                        mb[x] = fmaxf(mb[x], t);
+                    }
                 }
-            }
+        }
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
             mb[x] = fmaxf(mb[x], __shfl_xor(mb[x], 16));

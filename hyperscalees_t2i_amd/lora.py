@@ -146,7 +146,7 @@ class LoRALinear(nn.Module):
                 T: Optional[torch.Tensor] = None, shadow: Optional[torch.Tensor] = None) -> torch.Tensor:
         """epi (optional): an elementwise op on the output, fused into the GEMM epilogue on the
         population path (kernels.lora_linear_pop_epi): "res" -> res + y, "gated" -> res + gate[g] * y,
-        both written into `res` in place and returned; "res32" / "gated32": the same on an fp32 residual
+        "mul" -> res * y, written into `res` in place and returned; "res32" / "gated32": the same on an fp32 residual
         stream `res` (gate fp32), `shadow` (optional bf16) receiving bf16(res).  T (optional, population
         path): this linear's X A_k^T already computed by shared_projection — only the GEMM + LoRA
         epilogue run here."""
@@ -185,13 +185,15 @@ class LoRALinear(nn.Module):
                                       T_ws=ws, out=sh2)
                 return res
             if (FUSE_EPILOGUES and not self.r and not GemmTimer.active and M >= 4096 and self.in_features % 64 == 0
-                    and epi in ("res", "gated")):   # plain linear (no LoRA), epilogue fused (Infinity's proj / fc2)
+                    and epi in ("res", "gated", "mul")):   # plain linear (no LoRA), epilogue fused (Infinity's proj / fc2)
                 K.lora_linear_pop_epi(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M, epi, res=res2, gate=gate,
                                       rows_per_group=rows_per_group)
                 return res
             y = self.forward(x).view(M, self.out_features)   # the same ops, unfused
             if epi == "res":
                 res2.add_(y)
+            elif epi == "mul":
+                res2.mul_(y)
             elif epi == "gated":
                 K.gated_residual_(res2, y, gate, rows_per_group=rows_per_group)
             elif epi in ("res32", "gated32"):

@@ -132,8 +132,8 @@ class ZAttention(nn.Module):
 
 
 class ZFeedForward(nn.Module):
-    """w2(silu(w1 x) * w3 x); silu(w1 x) comes out of the GEMM's SiLU epilogue (the same bf16 values as
-    torch's silu of the rounded output), the product is one bf16 multiply pass."""
+    """w2(silu(w1 x) * w3 x); silu(w1 x) comes out of w1's SiLU epilogue (the same bf16 values as torch's
+    silu of the rounded output) and the product out of w3's multiply epilogue (bf16(h * y), torch's mul)."""
 
     def __init__(self, a: ZImageArch):
         super().__init__()
@@ -143,7 +143,7 @@ class ZFeedForward(nn.Module):
 
     def forward(self, x):
         h = self.w1(x, epi="silu")
-        h.mul_(self.w3(x))
+        self.w3(x, epi="mul", res=h)          # h *= w3 x in the w3 GEMM's epilogue
         return self.w2(h)
 
 

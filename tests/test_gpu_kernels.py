@@ -929,7 +929,8 @@ def test_full_size_sana_layout_properties(dev, pop):
 @pytest.mark.parametrize("epi,r,M,N,Kd,rpm", [("silu", 0, 16384, 2304, 512, 16384), ("res", 2, 4 * 4096, 2240, 2240, 4096),
                                              ("gated", 2, 4 * 4096, 2240, 2240, 4096), ("gated", 1, 3 * 1000 + 200, 384, 256, 1000),
                                              ("res", 0, 777, 200, 128, 777), ("gelu", 2, 2 * 8192, 2304, 512, 8192),
-                                             ("gelu", 0, 777, 200, 128, 777)])
+                                             ("gelu", 0, 777, 200, 128, 777), ("mul", 2, 4 * 4096, 2240, 2240, 4096),
+                                             ("mul", 0, 777, 200, 128, 777)])
 def test_lora_linear_pop_epilogue_bitexact(dev, epi, r, M, N, Kd, rpm):
     """eggroll_lora_linear_pop_epi == the same 8-phase GEMM (kernel 8) followed by the separate op it
     fuses (SiLU of the bf16 output / residual add / eggroll_gated_residual), bit for bit; ragged M, N."""
@@ -967,7 +968,10 @@ def test_lora_linear_pop_epilogue_bitexact(dev, epi, r, M, N, Kd, rpm):
         assert (diff <= ref.float().abs() * 2 ** -7 + 1e-5).all(), float(diff.max())
         assert (diff == 0).float().mean().item() > 0.99
         return
-    if epi == "res":
+    if epi == "mul":
+        ref = res * y
+        out = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, "mul", res=res.clone())
+    elif epi == "res":
         ref = (res.float() + y.float()).to(torch.bfloat16)
         out = K.lora_linear_pop_epi(x, W, bias, tp, offA, offB, r, 2.0, rpm, "res", res=res.clone())
     else:
