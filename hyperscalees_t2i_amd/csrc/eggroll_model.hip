@@ -1768,7 +1768,7 @@ extern "C" int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, in
 constexpr int FA_HD = 128, FA_KB = 64, FA_RS = FA_HD + 8;
 
 template <int QF>
-__global__ __launch_bounds__(256, QF == 2 ? 2 : 1) void k_flash_attn(const unsigned short* __restrict__ q, int64_t q_bs, int64_t ldq,
+__global__ __launch_bounds__(256, QF == 1 ? 3 : (QF == 2 ? 2 : 1)) void k_flash_attn(const unsigned short* __restrict__ q, int64_t q_bs, int64_t ldq,
                                                     const unsigned short* __restrict__ k, int64_t k_bs, int64_t ldk,
                                                     const unsigned short* __restrict__ v, int64_t v_bs, int64_t ldv,
                                                     int heads, int Nq, int Lk, int nqb, float scale_log2,
@@ -1942,7 +1942,7 @@ extern "C" int eggroll_flash_attention_sel(const void* q, int64_t q_bs, int64_t 
                                            int64_t ldk, const void* v, int64_t v_bs, int64_t ldv, int64_t B,
                                            int64_t heads, int64_t Nq, int64_t Lk, int64_t head_dim, float scale, void* o,
                                            int64_t o_bs, int64_t ldo, int32_t qf, void* stream) {
-    EGG_CHECK_ARG(qf == 0 || qf == 2 || qf == 4, "flash_attention: qf must be 0 (auto), 2 or 4");
+    EGG_CHECK_ARG(qf == 0 || qf == 1 || qf == 2 || qf == 4, "flash_attention: qf must be 0 (auto), 1, 2 or 4");
     if (qf == 0) qf = 2;
     EGG_CHECK_ARG(head_dim == FA_HD, "flash_attention: head_dim %lld unsupported (128)", (long long)head_dim);
     EGG_CHECK_ARG(B >= 0 && heads > 0 && Nq >= 0 && Lk >= 1, "flash_attention: bad sizes");
@@ -1956,7 +1956,7 @@ extern "C" int eggroll_flash_attention_sel(const void* q, int64_t q_bs, int64_t 
     EGG_CHECK_ARG(Nq < (1ll << 31) && Lk < (1ll << 31), "flash_attention: sequence too long");
     const int64_t qwg = 4 * 16 * qf, nqb = (Nq + qwg - 1) / qwg;
     EGG_CHECK_ARG(B * heads * nqb < (1ll << 31), "flash_attention: grid too large");
-    auto* kern = qf == 4 ? k_flash_attn<4> : k_flash_attn<2>;
+    auto* kern = qf == 4 ? k_flash_attn<4> : (qf == 1 ? k_flash_attn<1> : k_flash_attn<2>);
     hipLaunchKernelGGL(kern, dim3((unsigned)(B * heads * nqb)), dim3(256), 0, as_stream(stream),
                        (const unsigned short*)q, q_bs, ldq, (const unsigned short*)k, k_bs, ldk,
                        (const unsigned short*)v, v_bs, ldv, (int)heads, (int)Nq, (int)Lk, (int)nqb,

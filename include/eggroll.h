@@ -403,7 +403,7 @@ int eggroll_flash_attention(const void* q, int64_t q_bs, int64_t ldq, const void
                             const void* v, int64_t v_bs, int64_t ldv, int64_t B, int64_t heads, int64_t Nq,
                             int64_t Lk, int64_t head_dim, float scale, void* o, int64_t o_bs, int64_t ldo,
                             void* stream);
-/* The same with the queries per wave chosen (qf 2: 32, qf 4: 64; 0: automatic) — A/B measurement. */
+/* The same with the queries per wave chosen (qf 1: 16, 2: 32, 4: 64; 0: automatic) — A/B measurement. */
 int eggroll_flash_attention_sel(const void* q, int64_t q_bs, int64_t ldq, const void* k, int64_t k_bs, int64_t ldk,
                                 const void* v, int64_t v_bs, int64_t ldv, int64_t B, int64_t heads, int64_t Nq,
                                 int64_t Lk, int64_t head_dim, float scale, void* o, int64_t o_bs, int64_t ldo, int32_t qf,
