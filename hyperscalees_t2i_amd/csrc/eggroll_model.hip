@@ -1973,6 +1973,156 @@ extern "C" int eggroll_flash_attention(const void* q, int64_t q_bs, int64_t ldq,
                                        o_bs, ldo, 0, stream);
 }
 
+// ------------------------------------------------------------------------------------
+// GroupNorm (+ SiLU) on NHWC bf16 activations (the FLUX / Infinity VAE decoders' GroupNorm(32)):
+//   y[b, p, c] = act((x - mean[b, g]) * rstd[b, g] * w[c] + bias[c]),  g = c / (C / G),
+// statistics over the H*W pixels and C/G channels of (b, g), biased variance, fp32 data path.
+// Three launches: (1) per (image, pixel chunk) partial per-group sums / sums of squares (fp32 over at most
+// 256 x C/G values, reduced in a fixed order), (2) per (image, group) the chunks combined in fp64 ->
+// mean, rstd, (3) normalise + affine + act, 16-B loads / stores.  The torch form (an fp32 copy,
+// Welford statistics, four elementwise passes) moved ~10x the bytes.
+// ------------------------------------------------------------------------------------
+constexpr int GN_PASSES = 16;   // pixel passes per block: pixels per chunk = (256 / (C / 8)) * GN_PASSES
+
+__global__ __launch_bounds__(256) void k_gn_stats(const unsigned short* __restrict__ x, int64_t HW, int C, int G,
+                                                  int ppc, int nch, float2* __restrict__ part) {
+    __shared__ float red[256][17];
+    __shared__ float chs[2048][2];
+    const int tid = threadIdx.x, tpp = C / 8, pps = 256 / tpp;   // threads per pixel, pixels per pass
+    const int b = blockIdx.x / nch, ch = blockIdx.x - b * nch;
+    const int slot = tid % tpp, pl = tid / tpp;
+    float s[8], q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = q[i] = 0.f;
+    if (pl < pps) {
+        const int64_t p0 = (int64_t)ch * ppc;
+#pragma unroll 4
+        for (int k = 0; k < GN_PASSES; ++k) {
+            const int64_t p = p0 + (int64_t)k * pps + pl;
+            if (p < HW) {
+                const u16x8m v = *reinterpret_cast<const u16x8m*>(x + ((int64_t)b * HW + p) * C + slot * 8);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float f = b2f(v[i]);
+                    s[i] += f;
+                    q[i] += f * f;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        red[tid][i] = s[i];
+        red[tid][8 + i] = q[i];
+    }
+    __syncthreads();
+    // channel c = 8 slot + i: sum over the pixel lanes pl (fixed order)
+    for (int c = tid; c < C; c += 256) {
+        const int sl = c >> 3, i = c & 7;
+        float a = 0.f, a2 = 0.f;
+        for (int l = 0; l < pps; ++l) {
+            a += red[l * tpp + sl][i];
+            a2 += red[l * tpp + sl][8 + i];
+        }
+        chs[c][0] = a;
+        chs[c][1] = a2;
+    }
+    __syncthreads();
+    const int cpg = C / G;
+    for (int g = tid; g < G; g += 256) {
+        float a = 0.f, a2 = 0.f;
+        for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+            a += chs[c][0];
+            a2 += chs[c][1];
+        }
+        part[((int64_t)b * nch + ch) * G + g] = float2{a, a2};
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gn_finalize(const float2* __restrict__ part, int B, int G, int nch,
+                                                     double count, float eps, float2* __restrict__ stats) {
+    const int i = blockIdx.x * 256 + threadIdx.x;   // (b, g)
+    if (i >= B * G) return;
+    const int b = i / G, g = i - b * G;
+    double a = 0.0, a2 = 0.0;
+    for (int c = 0; c < nch; ++c) {
+        const float2 v = part[((int64_t)b * nch + c) * G + g];
+        a += v.x;
+        a2 += v.y;
+    }
+    const double mean = a / count;
+    double var = a2 / count - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    stats[i] = float2{(float)mean, (float)(1.0 / sqrt(var + (double)eps))};
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256) void k_gn_apply(const unsigned short* __restrict__ x, int64_t HW, int C, int G,
+                                                  const float2* __restrict__ stats,
+                                                  const unsigned short* __restrict__ w,
+                                                  const unsigned short* __restrict__ bias, int64_t total8,
+                                                  unsigned short* __restrict__ y) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;   // 8-channel unit
+    if (u >= total8) return;
+    const int tpp = C / 8, cpg = C / G;
+    const int64_t pix = u / tpp;
+    const int slot = (int)(u - pix * tpp);
+    const int b = (int)(pix / HW);
+    const u16x8m v = *reinterpret_cast<const u16x8m*>(x + u * 8);
+    const u16x8m wv = *reinterpret_cast<const u16x8m*>(w + slot * 8);
+    const u16x8m bv = *reinterpret_cast<const u16x8m*>(bias + slot * 8);
+    u16x8m o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int c = slot * 8 + i;
+        const float2 st = stats[(int64_t)b * G + c / cpg];
+        float t = (b2f(v[i]) - st.x) * st.y;
+        t = t * b2f(wv[i]) + b2f(bv[i]);
+        if (ACT == 1) t = silu(t);
+        o[i] = f2b(t);
+    }
+    *reinterpret_cast<u16x8m*>(y + u * 8) = o;
+}
+
+static int64_t gn_chunks(int64_t HW, int C, int* ppc_out) {
+    const int ppc = (256 / (C / 8)) * GN_PASSES;
+    if (ppc_out) *ppc_out = ppc;
+    return (HW + ppc - 1) / ppc;
+}
+
+extern "C" int64_t eggroll_group_norm_workspace_bytes(int64_t B, int64_t HW, int32_t C, int32_t G) {
+    if (B < 0 || HW < 0 || C < 8 || C % 8 || G < 1 || C % G) return 0;
+    return (B * gn_chunks(HW, C, nullptr) * G + B * G) * (int64_t)sizeof(float2);
+}
+
+extern "C" int eggroll_group_norm_nhwc(const void* x, int64_t B, int64_t HW, int32_t C, int32_t G, float eps,
+                                       const void* w, const void* bias, int32_t act, void* y, void* workspace,
+                                       void* stream) {
+    EGG_CHECK_ARG(C >= 8 && C <= 2048 && C % 8 == 0 && G >= 1 && C % G == 0, "group_norm: need C %% 8 == 0, C <= 2048, "
+                  "C %% G == 0 (C=%d G=%d)", C, G);
+    EGG_CHECK_ARG(B >= 0 && HW >= 0 && act >= 0 && act <= 1, "group_norm: bad sizes / act");
+    if (B == 0 || HW == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(x && w && bias && y && workspace, "group_norm: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)w & 15) == 0 &&
+                  ((uintptr_t)bias & 15) == 0 && ((uintptr_t)workspace & 7) == 0, "group_norm: misaligned pointer");
+    int ppc = 0;
+    const int64_t nch = gn_chunks(HW, C, &ppc);
+    EGG_CHECK_ARG(B * nch < (1ll << 31) && B * HW * C / 8 / 256 < (1ll << 31), "group_norm: grid too large");
+    float2* part = reinterpret_cast<float2*>(workspace);
+    float2* stats = part + B * nch * G;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_gn_stats, dim3((unsigned)(B * nch)), dim3(256), 0, st, (const unsigned short*)x, HW, C, G, ppc,
+                       (int)nch, part);
+    hipLaunchKernelGGL(k_gn_finalize, dim3((unsigned)((B * G + 255) / 256)), dim3(256), 0, st, part, (int)B, G, (int)nch,
+                       (double)HW * (double)(C / G), eps, stats);
+    const int64_t total8 = B * HW * C / 8;
+    auto* k = act ? k_gn_apply<1> : k_gn_apply<0>;
+    hipLaunchKernelGGL(k, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, st, (const unsigned short*)x, HW, C, G,
+                       stats, (const unsigned short*)w, (const unsigned short*)bias, total8, (unsigned short*)y);
+    EGG_CHECK_LAUNCH("group_norm");
+    return EGGROLL_OK;
+}
+
 extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
                                        const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
                                        int64_t heads, int64_t head_dim, int64_t L, int64_t U, float scale, void* o,

@@ -7,7 +7,7 @@ Reference: `ZImagePipeline` decodes `latents / scaling_factor + shift_factor` wi
 (models/zImageTurbo.py:96-101).  Restated from the published config; no weights offline, parity with
 diffusers UNPINNED.  Execution: the dense 3x3 convs whose widths fit run as libeggroll's implicit-GEMM
 MFMA kernel (eggroll_conv_nhwc), conv_in / conv_out (16 / 3 channels) and the 1x1 shortcut on MIOpen /
-hipBLASLt, GroupNorm + SiLU as fp32 torch reductions, the mid-block attention on SDPA.
+hipBLASLt, GroupNorm + SiLU on eggroll_group_norm_nhwc (fp32 statistics), the mid-block attention on SDPA.
 """
 from __future__ import annotations
 
@@ -31,9 +31,12 @@ class GroupNorm(nn.Module):
         super().__init__()
         self.groups, self.eps = groups, eps
         self.weight, self.bias = _p(c), _p(c)
+        self.use_kernel = True   # False: the fp32 torch form below (A/B, tests)
 
     def forward(self, x, silu: bool = True):  # NHWC bf16 -> NHWC bf16: GroupNorm (fp32 statistics) [+ SiLU]
         B, H, W, C = x.shape
+        if self.use_kernel and x.is_cuda and C % 8 == 0 and C <= 2048:   # eggroll_group_norm_nhwc
+            return K.group_norm_nhwc(x.contiguous(), self.groups, self.weight, self.bias, self.eps, silu)
         xf = x.float().view(B, H * W, self.groups, C // self.groups)
         var, mean = torch.var_mean(xf, dim=(1, 3), unbiased=False, keepdim=True)
         y = ((xf - mean) * torch.rsqrt(var + self.eps)).view(B, H, W, C) * self.weight.float() + self.bias.float()

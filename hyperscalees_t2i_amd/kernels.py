@@ -963,3 +963,22 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: fl
     OpTimer.end(e0, "flash_attention", 2.0 * B * H * 128 * (2 * Nq + 2 * k.shape[1]), f"B{B} Nq{Nq} Lk{k.shape[1]} h{H}",
                 flops=4.0 * B * H * Nq * k.shape[1] * 128)
     return out
+
+
+def group_norm_nhwc(x: torch.Tensor, groups: int, w: torch.Tensor, b: torch.Tensor, eps: float,
+                    silu: bool = False) -> torch.Tensor:
+    """GroupNorm over an NHWC bf16 tensor [B, H, W, C] (+ SiLU), fp32 statistics
+    (eggroll_group_norm_nhwc).  Returns a new contiguous [B, H, W, C] bf16 tensor."""
+    _dev(x, "group_norm(x)", torch.bfloat16)
+    _dev(w, "group_norm(w)", torch.bfloat16)
+    _dev(b, "group_norm(b)", torch.bfloat16)
+    B, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // max(B * C, 1)
+    out = torch.empty_like(x)
+    nb = int(_lib.load().eggroll_group_norm_workspace_bytes(B, HW, C, groups))
+    ws = torch.empty(max(1, -(-nb // 8)), dtype=torch.float64, device=x.device)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_group_norm_nhwc", x.data_ptr(), B, HW, C, int(groups), float(eps), w.data_ptr(), b.data_ptr(),
+              int(bool(silu)), out.data_ptr(), ws.data_ptr(), _stream(x.device))
+    OpTimer.end(e0, f"group_norm(C={C})", 6.0 * x.numel(), f"B{B} HW{HW}")
+    return out

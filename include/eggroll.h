@@ -395,6 +395,15 @@ int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const voi
                             const int32_t* enc_index, int64_t B, int64_t N, int64_t heads, int64_t head_dim,
                             int64_t L, int64_t U, float scale, void* o, int64_t ldo, void* stream);
 
+/* GroupNorm over NHWC bf16 activations (+ SiLU when act = 1):
+ *   y[b,p,c] = act((x[b,p,c] - mean[b,g]) * rstd[b,g] * w[c] + bias[c]),  g = c / (C / G)
+ * statistics over the HW pixels x C/G channels of (b, g) (biased variance, fp32 partial sums combined in
+ * fp64); x / y [B][HW][C] bf16 (16-byte aligned, C % 8 == 0, C <= 2048, C % G == 0), w / bias [C] bf16;
+ * workspace of eggroll_group_norm_workspace_bytes(B, HW, C, G) bytes (8-byte aligned).  Three launches. */
+int64_t eggroll_group_norm_workspace_bytes(int64_t B, int64_t HW, int32_t C, int32_t G);
+int eggroll_group_norm_nhwc(const void* x, int64_t B, int64_t HW, int32_t C, int32_t G, float eps, const void* w,
+                            const void* bias, int32_t act, void* y, void* workspace, void* stream);
+
 /* Flash attention, head dim 128, no mask (Z-Image self-attention, Infinity's attention over its KV cache):
  *   o[b,n,h,:] = softmax_j(scale * q[b,n,h,:] . k[b,j,h,:]) @ v[b,:,h,:],  n < Nq, j < Lk
  * q / k / v / o bf16, element (b, row, h, d) at X[b * X_bs + row * ldX + h * 128 + d] (a KV cache read in

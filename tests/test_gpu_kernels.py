@@ -1256,3 +1256,22 @@ def test_flash_attention_vs_sdpa(dev, B, Nq, Lk, H, strided):
     err = ((got - ref).norm() / ref.norm()).item()
     assert err < 1e-2, err
     assert (got - ref).abs().max().item() < 0.05
+
+
+@pytest.mark.parametrize("B,H,W,C,G,silu", [(2, 48, 40, 128, 32, True), (3, 17, 9, 160, 32, False), (1, 64, 64, 640, 32, True),
+                                            (2, 5, 7, 64, 8, True)])
+def test_group_norm_nhwc_vs_torch(dev, B, H, W, C, G, silu):
+    """eggroll_group_norm_nhwc vs fp32 torch.group_norm (+ silu) on the same bf16 input: within one bf16
+    rounding of the output (the stats are fp32 partial sums combined in fp64, torch's are Welford)."""
+    from hyperscalees_t2i_amd import kernels as Kk
+    g = torch.Generator(device=dev).manual_seed(C + H)
+    x = (torch.randn(B, H, W, C, generator=g, device=dev) * 3 + 1.5).bfloat16()
+    w = (1 + 0.2 * torch.randn(C, generator=g, device=dev)).bfloat16()
+    b = (0.3 * torch.randn(C, generator=g, device=dev)).bfloat16()
+    ref = torch.nn.functional.group_norm(x.float().permute(0, 3, 1, 2), G, w.float(), b.float(), 1e-6)
+    if silu:
+        ref = torch.nn.functional.silu(ref)
+    ref = ref.permute(0, 2, 3, 1)
+    got = Kk.group_norm_nhwc(x, G, w, b, 1e-6, silu=silu).float()
+    err = (got - ref).abs()
+    assert (err <= ref.abs() * 2 ** -7 + 2e-3).all(), float(err.max())
