@@ -2039,21 +2039,33 @@ __global__ __launch_bounds__(256) void k_gn_stats(const unsigned short* __restri
     }
 }
 
-__global__ __launch_bounds__(256) void k_gn_finalize(const float2* __restrict__ part, int B, int G, int nch,
-                                                     double count, float eps, float2* __restrict__ stats) {
-    const int i = blockIdx.x * 256 + threadIdx.x;   // (b, g)
-    if (i >= B * G) return;
-    const int b = i / G, g = i - b * G;
+__global__ __launch_bounds__(256) void k_gn_finalize(const float2* __restrict__ part, int G, int nch, double count,
+                                                     float eps, float2* __restrict__ stats) {
+    // one workgroup per (image, group): the chunk partials strided over the threads, then a fixed tree
+    __shared__ double sa[256], sq[256];
+    const int i = blockIdx.x, b = i / G, g = i - b * G, tid = threadIdx.x;
     double a = 0.0, a2 = 0.0;
-    for (int c = 0; c < nch; ++c) {
+    for (int c = tid; c < nch; c += 256) {
         const float2 v = part[((int64_t)b * nch + c) * G + g];
         a += v.x;
         a2 += v.y;
     }
-    const double mean = a / count;
-    double var = a2 / count - mean * mean;
-    var = var > 0.0 ? var : 0.0;
-    stats[i] = float2{(float)mean, (float)(1.0 / sqrt(var + (double)eps))};
+    sa[tid] = a;
+    sq[tid] = a2;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (tid < h) {
+            sa[tid] += sa[tid + h];
+            sq[tid] += sq[tid + h];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const double mean = sa[0] / count;
+        double var = sq[0] / count - mean * mean;
+        var = var > 0.0 ? var : 0.0;
+        stats[i] = float2{(float)mean, (float)(1.0 / sqrt(var + (double)eps))};
+    }
 }
 
 template <int ACT>
@@ -2107,13 +2119,14 @@ extern "C" int eggroll_group_norm_nhwc(const void* x, int64_t B, int64_t HW, int
                   ((uintptr_t)bias & 15) == 0 && ((uintptr_t)workspace & 7) == 0, "group_norm: misaligned pointer");
     int ppc = 0;
     const int64_t nch = gn_chunks(HW, C, &ppc);
-    EGG_CHECK_ARG(B * nch < (1ll << 31) && B * HW * C / 8 / 256 < (1ll << 31), "group_norm: grid too large");
+    EGG_CHECK_ARG(B * nch < (1ll << 31) && B * G < (1ll << 31) && B * HW * C / 8 / 256 < (1ll << 31),
+                  "group_norm: grid too large");
     float2* part = reinterpret_cast<float2*>(workspace);
     float2* stats = part + B * nch * G;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_gn_stats, dim3((unsigned)(B * nch)), dim3(256), 0, st, (const unsigned short*)x, HW, C, G, ppc,
                        (int)nch, part);
-    hipLaunchKernelGGL(k_gn_finalize, dim3((unsigned)((B * G + 255) / 256)), dim3(256), 0, st, part, (int)B, G, (int)nch,
+    hipLaunchKernelGGL(k_gn_finalize, dim3((unsigned)(B * G)), dim3(256), 0, st, part, G, (int)nch,
                        (double)HW * (double)(C / G), eps, stats);
     const int64_t total8 = B * HW * C / 8;
     auto* k = act ? k_gn_apply<1> : k_gn_apply<0>;
