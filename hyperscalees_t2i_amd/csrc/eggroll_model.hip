@@ -1765,7 +1765,12 @@ extern "C" int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, in
 //                 sums rescaled the same way and reduced over the 4 lane groups once at the end
 //   O^T += V^T P^T  (P^T packed from the C registers, V^T read with ds_read_tr16_b64 in the matching key order)
 // ------------------------------------------------------------------------------------
-constexpr int FA_HD = 128, FA_KB = 64, FA_RS = FA_HD + 8;
+// LDS row stride 144 bf16 = 288 B = 72 dwords: consecutive rows start 8 banks apart, so the S^T k reads
+// (ds_read_b128, lane groups {0-3,12-15,20-27}...: 8 rows x 2 chunks) and the V^T reads (ds_read_b64_tr_b16,
+// 32-lane groups: 8 rows x 32 B) both cover 64 distinct banks; the first form's 136 (4 banks apart) left
+// 38 % of the LDS cycles to bank conflicts (PMC SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE)
+constexpr int FA_HD = 128, FA_KB = 64, FA_RS = FA_HD + 16;
+typedef float fa_f32x2 __attribute__((ext_vector_type(2)));
 
 template <int QF>
 __global__ __launch_bounds__(256, QF == 1 ? 3 : (QF == 2 ? 2 : 1)) void k_flash_attn(const unsigned short* __restrict__ q, int64_t q_bs, int64_t ldq,
@@ -1838,10 +1843,12 @@ __global__ __launch_bounds__(256, QF == 1 ? 3 : (QF == 2 ? 2 : 1)) void k_flash_
         __syncthreads();
         if (kb + 1 < nkb) load_blk((kb + 1) * FA_KB);   // in flight under this block's MFMAs
         la_f32x4 sf[QF][KF];
+        // k-step outer, key fragment inner: 4 x QF independent accumulations between two dependent MFMAs
+        // (f outer put each chain's next MFMA right behind it: PMC issue stalls ~35 % of wave cycles)
 #pragma unroll
-        for (int f = 0; f < KF; ++f) {
+        for (int ks = 0; ks < KSN; ++ks) {
 #pragma unroll
-            for (int ks = 0; ks < KSN; ++ks) {
+            for (int f = 0; f < KF; ++f) {
                 const la_bf16x8 a = *reinterpret_cast<const la_bf16x8*>(sk + (16 * f + r16) * FA_RS + 32 * ks + 8 * g);
                 // the first k-step takes a literal zero accumulator (no per-block zeroing of 32 registers)
 #pragma unroll
@@ -1851,54 +1858,51 @@ __global__ __launch_bounds__(256, QF == 1 ? 3 : (QF == 2 ? 2 : 1)) void k_flash_
             }
         }
         const int key0 = kb * FA_KB;
-        float mb[QF];
-#pragma unroll
-        for (int x = 0; x < QF; ++x) mb[x] = -INFINITY;
-        if (key0 + FA_KB <= Lk) {   // full block (uniform branch): no key mask
-#pragma unroll
-            for (int f = 0; f < KF; ++f)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int x = 0; x < QF; ++x) {
-                        const float t = sf[x][f][e] * scale_log2;
-                        sf[x][f][e] = t;
-                        mb[x] = fmaxf(mb[x], t);
-                    }
-        } else {
+        // the VALU side is the bound here (PMC: ~6 VALU instructions per MFMA), so the softmax runs on
+        // raw scores: max of raw S (scale > 0 commutes with max), then p = 2^(s * scale_log2 - m) as one
+        // packed FMA per pair + exp2; O is rescaled only when some lane's running max moved
+        if (key0 + FA_KB > Lk) {   // the partial last block: keys >= Lk -> -inf (uniform branch)
 #pragma unroll
             for (int f = 0; f < KF; ++f)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const bool ok = key0 + 16 * f + 4 * g + e < Lk;
 #pragma unroll
-                    for (int x = 0; x < QF; ++x) {
-                        const float t = ok ? sf[x][f][e] * scale_log2 : -INFINITY;
-                        sf[x][f][e] = t;
-                        mb[x] = fmaxf(mb[x], t);
-                    }
+                    for (int x = 0; x < QF; ++x) sf[x][f][e] = ok ? sf[x][f][e] : -INFINITY;
                 }
         }
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
-            mb[x] = fmaxf(mb[x], __shfl_xor(mb[x], 16));
-            mb[x] = fmaxf(mb[x], __shfl_xor(mb[x], 32));
-            const float mn = fmaxf(m[x], mb[x]);
-            const float alpha = __builtin_amdgcn_exp2f(m[x] - mn);   // 0 on the first block (m = -inf)
-            m[x] = mn;
-            l[x] *= alpha;
+            float mb = fmaxf(fmaxf(sf[x][0][0], sf[x][0][1]), fmaxf(sf[x][0][2], sf[x][0][3]));
 #pragma unroll
-            for (int d = 0; d < DF; ++d)
+            for (int f = 1; f < KF; ++f)
+                mb = fmaxf(fmaxf(mb, fmaxf(sf[x][f][0], sf[x][f][1])), fmaxf(sf[x][f][2], sf[x][f][3]));
+            mb = fmaxf(mb, __shfl_xor(mb, 16));
+            mb = fmaxf(mb, __shfl_xor(mb, 32));
+            const float mn = fmaxf(m[x], mb * scale_log2);
+            if (__builtin_amdgcn_ballot_w64(mn != m[x])) {   // a running max moved: rescale this query set
+                const float alpha = __builtin_amdgcn_exp2f(m[x] - mn);   // 0 on the first block (m = -inf)
+                l[x] *= alpha;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) oc[x][d][e] *= alpha;
+                for (int d = 0; d < DF; ++d)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) oc[x][d][e] *= alpha;
+                m[x] = mn;
+            }
+            const fa_f32x2 sc2 = {scale_log2, scale_log2}, nm2 = {-mn, -mn};
+            fa_f32x2 acc2 = {0.f, 0.f};
 #pragma unroll
             for (int f = 0; f < KF; ++f)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float pe = __builtin_amdgcn_exp2f(sf[x][f][e] - mn);
-                    sf[x][f][e] = pe;
-                    l[x] += pe;
+                for (int e = 0; e < 4; e += 2) {
+                    fa_f32x2 t = (fa_f32x2){sf[x][f][e], sf[x][f][e + 1]} * sc2 + nm2;
+                    t.x = __builtin_amdgcn_exp2f(t.x);
+                    t.y = __builtin_amdgcn_exp2f(t.y);
+                    sf[x][f][e] = t.x;
+                    sf[x][f][e + 1] = t.y;
+                    acc2 = acc2 + t;
                 }
+            l[x] += acc2.x + acc2.y;
         }
 #pragma unroll
         for (int j = 0; j < KF / 2; ++j) {
