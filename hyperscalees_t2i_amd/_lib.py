@@ -53,6 +53,7 @@ SIGNATURES = {
     "eggroll_dwconv_pw_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i32, vp, vp]),
     "eggroll_dwconv_nhwc_sel": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i32, i32, i32, vp, i32, vp]),
     "eggroll_qk_norm_rope": (C.c_int, [vp, i64, i64, i32, i32, f32, vp, vp, vp, i64, vp]),
+    "eggroll_qk_norm_rope_kv": (C.c_int, [vp, i64, i64, i32, i32, f32, vp, vp, vp, i64, vp, vp, i64, i64, i64, i64, vp, i64, vp, vp]),
     "eggroll_group_norm_workspace_bytes": (C.c_int64, [i64, i64, i32, i32]),
     "eggroll_group_norm_nhwc": (C.c_int, [vp, i64, i64, i32, i32, f32, vp, vp, i32, vp, vp, vp]),
     "eggroll_flash_attention": (C.c_int, [vp, i64, i64, vp, i64, i64, vp, i64, i64, i64, i64, i64, i64, i64, f32, vp, i64, i64, vp]),

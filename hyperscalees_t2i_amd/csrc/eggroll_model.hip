@@ -1361,10 +1361,16 @@ extern "C" int eggroll_rownorm_ex(const void* x, int32_t x_f32, int64_t rows, in
 // 4 rotation pairs per lane, fp32 throughout and one bf16 rounding.  Replaces the norm pass and torch's
 // fp32 rotation (~10 full passes over q and k per attention).
 // ------------------------------------------------------------------------------------
+// out == NULL: in place on x.  Otherwise the result goes to out at row (row / rps) * out_bs + (row0 +
+// row % rps) * out_ld (a KV cache [seq][ltot][C] slice), and vin (when given) is copied to vout at the same
+// row (the values of the same tokens); hscale (optional, fp32 [heads]) multiplies head h's output.
 __global__ __launch_bounds__(256) void k_qk_norm_rope(unsigned short* __restrict__ x, int64_t ldx, int heads,
                                                       float eps, const unsigned short* __restrict__ w,
                                                       const float* __restrict__ cosb, const float* __restrict__ sinb,
-                                                      int64_t tab_rows, int64_t segs) {
+                                                      int64_t tab_rows, int64_t segs, const float* __restrict__ hscale,
+                                                      unsigned short* __restrict__ out, int64_t out_bs, int64_t out_ld,
+                                                      int64_t rps, int64_t row0, const unsigned short* __restrict__ vin,
+                                                      int64_t ldv, unsigned short* __restrict__ vout) {
     const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const int l = threadIdx.x & 15;
     const bool live = seg < segs;
@@ -1388,14 +1394,26 @@ __global__ __launch_bounds__(256) void k_qk_norm_rope(unsigned short* __restrict
     const float4 c4 = *reinterpret_cast<const float4*>(cosb + tr * 64 + l * 4);
     const float4 s4 = *reinterpret_cast<const float4*>(sinb + tr * 64 + l * 4);
     const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+    const float hs = hscale ? hscale[h] : 1.0f;
     u16x8m o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const float y0 = f[2 * j] * r * b2f(wv[2 * j]), y1 = f[2 * j + 1] * r * b2f(wv[2 * j + 1]);
-        o[2 * j] = f2b(y0 * cs[j] - y1 * sn[j]);
-        o[2 * j + 1] = f2b(y0 * sn[j] + y1 * cs[j]);
+        if (hscale) {
+            o[2 * j] = f2b(b2f(f2b(y0 * cs[j] - y1 * sn[j])) * hs);
+            o[2 * j + 1] = f2b(b2f(f2b(y0 * sn[j] + y1 * cs[j])) * hs);
+        } else {
+            o[2 * j] = f2b(y0 * cs[j] - y1 * sn[j]);
+            o[2 * j + 1] = f2b(y0 * sn[j] + y1 * cs[j]);
+        }
     }
-    *reinterpret_cast<u16x8m*>(p) = o;
+    if (!out) {
+        *reinterpret_cast<u16x8m*>(p) = o;
+        return;
+    }
+    const int64_t orow = (row / rps) * out_bs + (row0 + row % rps) * out_ld + h * 128 + l * 8;
+    *reinterpret_cast<u16x8m*>(out + orow) = o;
+    if (vin) *reinterpret_cast<u16x8m*>(vout + orow) = *reinterpret_cast<const u16x8m*>(vin + row * ldv + h * 128 + l * 8);
 }
 
 extern "C" int eggroll_qk_norm_rope(void* x, int64_t ldx, int64_t rows, int32_t heads, int32_t head_dim, float eps,
@@ -1413,8 +1431,37 @@ extern "C" int eggroll_qk_norm_rope(void* x, int64_t ldx, int64_t rows, int32_t 
     EGG_CHECK_ARG(segs < (1ll << 31) / 16, "qk_norm_rope: too many rows");
     hipLaunchKernelGGL(k_qk_norm_rope, dim3((unsigned)((segs * 16 + 255) / 256)), dim3(256), 0, as_stream(stream),
                        (unsigned short*)x, ldx, (int)heads, eps, (const unsigned short*)w, cos_tab, sin_tab, tab_rows,
-                       segs);
+                       segs, nullptr, nullptr, 0, 0, 1, 0, nullptr, 0, nullptr);
     EGG_CHECK_LAUNCH("qk_norm_rope");
+    return EGGROLL_OK;
+}
+
+extern "C" int eggroll_qk_norm_rope_kv(void* x, int64_t ldx, int64_t rows, int32_t heads, int32_t head_dim, float eps,
+                                       const void* w, const float* cos_tab, const float* sin_tab, int64_t tab_rows,
+                                       const float* hscale, void* out, int64_t out_bs, int64_t out_ld,
+                                       int64_t rows_per_seq, int64_t row0, const void* vin, int64_t ldv, void* vout,
+                                       void* stream) {
+    EGG_CHECK_ARG(head_dim == 128, "qk_norm_rope_kv: head_dim must be 128 (got %d)", head_dim);
+    EGG_CHECK_ARG(rows >= 0 && heads > 0 && ldx >= (int64_t)heads * 128 && ldx % 8 == 0 && tab_rows > 0,
+                  "qk_norm_rope_kv: bad sizes / strides");
+    EGG_CHECK_ARG(!out || (rows_per_seq > 0 && row0 >= 0 && out_ld >= (int64_t)heads * 128 && out_ld % 8 == 0 &&
+                           out_bs % 8 == 0 && out_bs >= (row0 + rows_per_seq) * out_ld),
+                  "qk_norm_rope_kv: bad output geometry");
+    EGG_CHECK_ARG(!vin || (out && vout && ldv >= (int64_t)heads * 128 && ldv % 8 == 0),
+                  "qk_norm_rope_kv: the value copy needs out, vout and ldv");
+    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)cos_tab & 15) == 0 &&
+                      ((uintptr_t)sin_tab & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)vin & 15) == 0 &&
+                      ((uintptr_t)vout & 15) == 0,
+                  "qk_norm_rope_kv: pointers must be 16-byte aligned");
+    if (rows == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(x && w && cos_tab && sin_tab, "qk_norm_rope_kv: NULL pointer");
+    const int64_t segs = rows * heads;
+    EGG_CHECK_ARG(segs < (1ll << 31) / 16, "qk_norm_rope_kv: too many rows");
+    hipLaunchKernelGGL(k_qk_norm_rope, dim3((unsigned)((segs * 16 + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       (unsigned short*)x, ldx, (int)heads, eps, (const unsigned short*)w, cos_tab, sin_tab, tab_rows,
+                       segs, hscale, (unsigned short*)out, out_bs, out_ld, out ? rows_per_seq : 1, row0,
+                       (const unsigned short*)vin, ldv, (unsigned short*)vout);
+    EGG_CHECK_LAUNCH("qk_norm_rope_kv");
     return EGGROLL_OK;
 }
 

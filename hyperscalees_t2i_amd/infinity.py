@@ -205,6 +205,11 @@ class InfinityTransformer(nn.Module):
         self.head_nm = nn.Module()
         self.head_nm.ada_lin = nn.ModuleList([nn.SiLU(), LoRALinear(C, 2 * C, bias=True, lora=False)])
         self.head = LoRALinear(C, 2 * a.d_tok, bias=True, lora=False)
+        # the early scales' plain GEMMs (64 .. 9216 rows at 8B widths) run 1.0-3.9x faster on hipBLASLt's
+        # split-K kernels than on the 8-phase / 128-tile kernels (profiles/r07b_small_m_gemm_probe.jsonl)
+        for m in self.modules():
+            if isinstance(m, LoRALinear):
+                m.lib_small_m = 16384
 
     def blocks(self) -> List[CrossAttnBlock]:
         return [b for ch in self.block_chunks for b in ch.module]
@@ -338,6 +343,15 @@ class InfinityPopulationInfer:
         cat = ca[2](F.gelu(ca[0](t.to(torch.bfloat16)), approximate="tanh"))          # [2U, Lt, C]
         return bias, sos, cat
 
+    def _qscale(self, sa: SelfAttention, H: int, hd: int) -> torch.Tensor:
+        """exp(min(s_h, log 100)) / hd per head, bf16-rounded (the factor torch's bf16 multiply applies),
+        held as fp32; cached per module (the log-scales are frozen)."""
+        key = (sa.scale_mul_1H11._version, sa.scale_mul_1H11.data_ptr())
+        if getattr(sa, "_qs_key", None) != key:
+            qs = sa.scale_mul_1H11.view(H).clamp(max=math.log(100.0)).exp() / hd
+            sa._qs, sa._qs_key = qs.to(torch.bfloat16).float().contiguous(), key
+        return sa._qs
+
     # ---- one scale step through the blocks ----------------------------------------------
     def _block(self, blk: CrossAttnBlock, x, l, cur, kv, mod32, mod16, cak, cav, cabias, cos, sin):
         a = self.tr.arch
@@ -347,20 +361,23 @@ class InfinityPopulationInfer:
         h = K.rownorm(x, a.norm_eps, layer=True, mscale=mod32[:, 2], mshift=mod32[:, 4], rows_per_group=l)
         qkv = sa.mat_qkv(h)                                                             # [N2*l, 3C]
         q2, k2 = qkv[:, :C], qkv[:, C:2 * C]
+        # RMS-normalised rows have norm sqrt(hd): logits = exp(s_h) cos(q, k) = (q * exp(s_h) / hd) . k
         if self.use_kernel and hd == 128:
-            K.qk_norm_rope_(q2, sa._ones, 1e-12, cos, sin, H)
-            K.qk_norm_rope_(k2, sa._ones, 1e-12, cos, sin, H)
+            # q: norm + RoPE + the per-head scale in place; k: norm + RoPE written straight into the cache
+            # slice, the values copied alongside (no separate scale / copy passes)
+            K.qk_norm_rope_kv(q2, sa._ones, 1e-12, cos, sin, H, hscale=self._qscale(sa, H, hd))
+            K.qk_norm_rope_kv(k2, sa._ones, 1e-12, cos, sin, H, out=kv[0], rows_per_seq=l, row0=cur,
+                              vin=qkv[:, 2 * C:], vout=kv[1])
+            q = qkv.view(N2, l, 3, H, hd)[:, :, 0]
         else:
             _rms_rope_torch(q2, H, hd, 1e-12, cos, sin)
             _rms_rope_torch(k2, H, hd, 1e-12, cos, sin)
-        # RMS-normalised rows have norm sqrt(hd): logits = exp(s_h) cos(q, k) = (q * exp(s_h) / hd) . k
-        qs = sa.scale_mul_1H11.view(H).clamp(max=math.log(100.0)).exp() / hd
-        q = (qkv.view(N2, l, 3, H, hd)[:, :, 0] * qs.view(1, 1, H, 1).to(torch.bfloat16))
-        kv[0, :, cur:cur + l] = k2.view(N2, l, C)
-        kv[1, :, cur:cur + l] = qkv.view(N2, l, 3, C)[:, :, 2]
+            q = qkv.view(N2, l, 3, H, hd)[:, :, 0] * self._qscale(sa, H, hd).to(torch.bfloat16).view(1, 1, H, 1)
+            kv[0, :, cur:cur + l] = k2.view(N2, l, C)
+            kv[1, :, cur:cur + l] = qkv.view(N2, l, 3, C)[:, :, 2]
         ks = kv[0, :, :cur + l].view(N2, cur + l, H, hd)
         vs = kv[1, :, :cur + l].view(N2, cur + l, H, hd)
-        if self.use_kernel and hd == 128:     # eggroll_flash_attention reads the cache in place
+        if self.use_kernel and hd == 128:     # eggroll_flash_attention reads q from qkv and the cache in place
             o = K.flash_attention(q, ks, vs, 1.0).view(N2 * l, C)
         else:
             o = F.scaled_dot_product_attention(q.transpose(1, 2), ks.transpose(1, 2), vs.transpose(1, 2), scale=1.0)

@@ -616,6 +616,37 @@ def qk_norm_rope_(x: torch.Tensor, w: torch.Tensor, eps: float, cos: torch.Tenso
     return x
 
 
+def qk_norm_rope_kv(x: torch.Tensor, w: torch.Tensor, eps: float, cos: torch.Tensor, sin: torch.Tensor, heads: int,
+                    hscale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, rows_per_seq: int = 1,
+                    row0: int = 0, vin: Optional[torch.Tensor] = None, vout: Optional[torch.Tensor] = None) -> None:
+    """eggroll_qk_norm_rope_kv: x [rows, >= heads*128] bf16 (row stride x.stride(0)); hscale fp32 [heads]
+    (optional output multiplier); out (optional) a [seq, ltot, C] bf16 cache: row r goes to
+    out[r // rows_per_seq, row0 + r % rows_per_seq]; vin (optional, [rows, ...] like x) copied into vout
+    (same geometry as out) at the same positions."""
+    _dev(x, "qk_norm_rope_kv(x)", torch.bfloat16, contiguous=False)
+    _dev(w, "qk_norm_rope_kv(w)", torch.bfloat16)
+    if x.dim() != 2 or x.stride(1) != 1 or cos.shape != sin.shape or cos.shape[-1] != 64 or w.numel() != 128:
+        raise ValueError(f"qk_norm_rope_kv: x {tuple(x.shape)}, w {tuple(w.shape)}, tables {tuple(cos.shape)}")
+    if hscale is not None:
+        _dev(hscale, "qk_norm_rope_kv(hscale)", torch.float32)
+    ob = ol = 0
+    if out is not None:
+        _dev(out, "qk_norm_rope_kv(out)", torch.bfloat16)
+        if out.dim() != 3 or out.shape[0] * rows_per_seq != x.shape[0] or row0 + rows_per_seq > out.shape[1]:
+            raise ValueError(f"qk_norm_rope_kv: out {tuple(out.shape)} vs {x.shape[0]} rows of {rows_per_seq}")
+        ob, ol = out.stride(0), out.stride(1)
+    if vin is not None:
+        _dev(vin, "qk_norm_rope_kv(vin)", torch.bfloat16, contiguous=False)
+        if vout is None or vout.shape != out.shape or vout.stride() != out.stride() or vin.shape[0] != x.shape[0]:
+            raise ValueError("qk_norm_rope_kv: vin needs a vout shaped like out")
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_qk_norm_rope_kv", x.data_ptr(), x.stride(0), x.shape[0], int(heads), 128, float(eps), w.data_ptr(),
+              cos.data_ptr(), sin.data_ptr(), cos.numel() // 64, _p(hscale), _p(out), ob, ol, int(rows_per_seq),
+              int(row0), _p(vin), vin.stride(0) if vin is not None else 0, _p(vout), _stream(x.device))
+    OpTimer.end(e0, "qk_norm_rope", (4.0 + (4.0 if vin is not None else 0.0)) * x.shape[0] * heads * 128,
+                f"rows{x.shape[0]}")
+
+
 def gated_residual_(x: torch.Tensor, y: torch.Tensor, gate: torch.Tensor, rows_per_group: int) -> torch.Tensor:
     """x += gate[g] * y in place (g = row // rows_per_group); gate a [groups, C] view."""
     _dev(x, "gated_residual(x)", torch.bfloat16)

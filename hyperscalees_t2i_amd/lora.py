@@ -125,6 +125,9 @@ class LoRALinear(nn.Module):
             self.lora_A = _Weight((r, in_features))
             self.lora_B = _Weight((out_features, r))
         self.ctx: Optional[PopulationContext] = None
+        # plain (r = 0) GEMMs with at most this many rows go to the vendor library (F.linear -> hipBLASLt),
+        # which splits K for short, wide problems; 0 = never (set per model: tools/small_m_gemm_probe.py)
+        self.lib_small_m = 0
         self.theta_off_A = -1  # element offsets of lora_A / lora_B inside theta (set by bind_theta_layout)
         self.theta_off_B = -1
 
@@ -184,7 +187,8 @@ class LoRALinear(nn.Module):
                                       self.r, self.scale, rpm, epi, res=res2, gate=gate, rows_per_group=rows_per_group,
                                       T_ws=ws, out=sh2)
                 return res
-            if (FUSE_EPILOGUES and not self.r and not GemmTimer.active and M >= 4096 and self.in_features % 64 == 0
+            if (FUSE_EPILOGUES and not self.r and not GemmTimer.active and M >= max(4096, self.lib_small_m + 1)
+                    and self.in_features % 64 == 0
                     and epi in ("res", "gated", "mul")):   # plain linear (no LoRA), epilogue fused (Infinity's proj / fc2)
                 K.lora_linear_pop_epi(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M, epi, res=res2, gate=gate,
                                       rows_per_group=rows_per_group)
@@ -231,6 +235,8 @@ class LoRALinear(nn.Module):
             y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
             T = K.lora_project(x2, A.contiguous().view(1, -1), 0, self.r, M)
             K.lora_expand(T, B.contiguous().view(1, -1), 0, self.r, self.scale, M, y)
+        elif M <= self.lib_small_m:
+            y = torch.nn.functional.linear(x2, self.weight, self.bias)
         else:
             y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
         return y.view(*shp[:-1], self.out_features)

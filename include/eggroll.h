@@ -272,6 +272,14 @@ int eggroll_gated_residual(void* x, const void* y, const void* gate, int64_t gst
  * Z-Image q / k path (diffusers ZImageTransformer2DModel: norm_q / norm_k then the 3-axis RoPE).    */
 int eggroll_qk_norm_rope(void* x, int64_t ldx, int64_t rows, int32_t heads, int32_t head_dim, float eps,
                          const void* w, const float* cos_tab, const float* sin_tab, int64_t tab_rows, void* stream);
+/* The same with (all optional) a per-head output multiplier hscale [heads] fp32, an output other than x —
+ * row r of x goes to out[(r / rows_per_seq) * out_bs + (row0 + r % rows_per_seq) * out_ld], a KV-cache
+ * slice [seq][ltot][C] — and vin row r (ldv apart) copied to vout at the same position (Infinity's cache
+ * append of the tokens' keys and values).                                                              */
+int eggroll_qk_norm_rope_kv(void* x, int64_t ldx, int64_t rows, int32_t heads, int32_t head_dim, float eps,
+                            const void* w, const float* cos_tab, const float* sin_tab, int64_t tab_rows,
+                            const float* hscale, void* out, int64_t out_bs, int64_t out_ld, int64_t rows_per_seq,
+                            int64_t row0, const void* vin, int64_t ldv, void* vout, void* stream);
 /* The same row normalisation with dtype options: x_f32 = 1: fp32 input x (the fp32 residual stream of
  * the Sana blocks); mod_f32 = 1: fp32 modulation vectors (the fp32 AdaLN modulation); res_f32 = 1: fp32
  * res; out_f32 = 1: fp32 output (the DC-AE fp32 residual stream, out = norm(x)·w + b + res, may alias

@@ -151,3 +151,35 @@ def test_generate_flat_returns_pil(setup):
     finally:
         be.cfg.micro_batch = 0
     assert len(imgs) == 3 and imgs[0].size == (256, 256) and imgs[0].mode == "RGB"
+
+
+def test_qk_norm_rope_kv_cache_append(dev):
+    """eggroll_qk_norm_rope_kv: q normalised + rotated + per-head scaled in place, k written into a cache
+    slice at [seq, row0 + t] with the values copied alongside == the torch form (within one bf16 rounding;
+    the cache outside the slice untouched)."""
+    from hyperscalees_t2i_amd import kernels as K
+    from hyperscalees_t2i_amd.infinity import _rms_rope_torch
+    g = torch.Generator(device=dev).manual_seed(3)
+    S, l, H, C, ltot, row0 = 3, 20, 2, 256, 57, 11
+    qkv = torch.randn(S * l, 3 * C, generator=g, device=dev).bfloat16()
+    ang = torch.rand(l, 64, generator=g, device=dev) * 6.3
+    cos, sin = torch.cos(ang).contiguous(), torch.sin(ang).contiguous()
+    hs = (torch.rand(H, generator=g, device=dev) + 0.5).bfloat16().float()
+    ones = torch.ones(128, device=dev, dtype=torch.bfloat16)
+    cache = torch.randn(2, S, ltot, C, generator=g, device=dev).bfloat16()
+    ref_q = qkv[:, :C].clone()
+    _rms_rope_torch(ref_q, H, 128, 1e-12, cos, sin)
+    ref_q = (ref_q.view(-1, H, 128) * hs.bfloat16().view(1, H, 1)).view(-1, C)
+    ref_k = qkv[:, C:2 * C].clone()
+    _rms_rope_torch(ref_k, H, 128, 1e-12, cos, sin)
+    ref_cache = cache.clone()
+    ref_cache[0, :, row0:row0 + l] = ref_k.view(S, l, C)
+    ref_cache[1, :, row0:row0 + l] = qkv[:, 2 * C:].view(S, l, C)
+    x = qkv.clone()
+    K.qk_norm_rope_kv(x[:, :C], ones, 1e-12, cos, sin, H, hscale=hs)
+    K.qk_norm_rope_kv(x[:, C:2 * C], ones, 1e-12, cos, sin, H, out=cache[0], rows_per_seq=l, row0=row0,
+                      vin=x[:, 2 * C:], vout=cache[1])
+    tol = lambda a, b: ((a.float() - b.float()).abs() <= b.float().abs() * 2 ** -7 + 1e-6).all()  # noqa: E731
+    assert tol(x[:, :C], ref_q)
+    assert tol(cache, ref_cache)
+    assert torch.equal(cache[:, :, :row0], ref_cache[:, :, :row0]) and torch.equal(cache[1], ref_cache[1])
