@@ -333,7 +333,9 @@ def main():
     dom_name = max(variants, key=lambda k: variants[k]["total_ms"]) if variants else "all"
     dom = gemm.get(dom_name, {"launches": 0, "flops": 0.0, "avg_us": float("nan"), "tflops": float("nan")})
     achieved = dom["tflops"]
-    pmc = load_pmc_traffic()
+    # PMC traffic was collected on the Sana epoch's LoRA-GEMM launch mix (tools/lora_epoch_driver.py):
+    # it belongs to that workload's line only
+    pmc = load_pmc_traffic() if args.workload == "sana" and not args.small else None
     roofline = {"kernel": f"{dom_name} (population LoRA GEMM + fused LoRA epilogue)", "bound": "mfma",
                 "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / BF16_DENSE_PEAK_TFLOPS,
