@@ -890,9 +890,14 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
 // 10 x 18-pixel halo tile of x is loaded with every 16-B load in flight, RMS-normalised per pixel
 // (16-lane shuffle reduction over 128 channels), written to LDS as bf16; then 36 MFMA k-steps
 // (9 taps x 4 x 32 channels) of 16 pixels x 16 outputs (3 real) per output row.  HBM: x read once
-// (+halo L2 hits), y written once — the conv is ~free on MFMA.
+// (+halo L2 hits), y written once — the conv is ~free on MFMA.  Round 4: a block walks EGG_HEAD_TPB
+// bands down its tile column with the next band's loads in flight under the current band's conv:
+// 1217 -> 1014 us at 8 x 1024^2 x 128, bitwise equal (profiles/r07i_dcae_head_band_walk_ab.jsonl).
 // ------------------------------------------------------------------------------------
 constexpr int HD_C = 128;                // input channels (the decoder's widths[0])
+#ifndef EGG_HEAD_TPB
+#define EGG_HEAD_TPB 8                   // output bands walked per block (A/B knob; 1 = the round-2 form)
+#endif
 constexpr int HD_TH = 8, HD_TW = 16;     // output tile
 constexpr int HD_TR = HD_TH + 2, HD_TC = HD_TW + 2;
 constexpr int HD_PSTR = HD_C * 2;        // LDS bytes per staged pixel: 16-B chunk c of pixel p sits at slot
@@ -908,38 +913,50 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
                                                    const unsigned short* __restrict__ nb,
                                                    const unsigned short* __restrict__ wc,   // [3][3][3][C]
                                                    const unsigned short* __restrict__ cb,   // [3] or null
-                                                   int xtiles, int bands, unsigned short* __restrict__ y) {
+                                                   int xtiles, int bands, int tpb, unsigned short* __restrict__ y) {
     __shared__ __attribute__((aligned(16))) char tile[HD_TR * HD_TC * HD_PSTR];
     __shared__ __attribute__((aligned(16))) unsigned short wl[3 * 9 * HD_C];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // XCD-contiguous tile ranges: horizontally adjacent tiles (sharing 2 halo columns) on one L2
+    // XCD-contiguous tile ranges: horizontally adjacent tiles (sharing 2 halo columns) on one L2.  A block
+    // walks tpb bands down its tile column; the next band's halo loads are issued as soon as the current
+    // band's raw values have been normalised into LDS, so they are in flight during its conv and stores
+    // (the one-band form waited a full memory latency per tile with only 3 blocks per CU to cover it)
+    const int bgroups = (bands + tpb - 1) / tpb;
     int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int xt = bid % xtiles;
     bid /= xtiles;
-    const int band = bid % bands;
-    const int b = bid / bands;
-    const int y0 = band * HD_TH, x0 = xt * HD_TW;
+    const int bg = bid % bgroups;
+    const int b = bid / bgroups;
+    const int band_lo = bg * tpb, band_hi = min(bands, band_lo + tpb);
+    const int x0 = xt * HD_TW;
     const unsigned short* img = x + (int64_t)b * H * W * HD_C;
-    // conv weights -> LDS (6.75 KiB)
+    // conv weights -> LDS (6.75 KiB), once per block
     for (int u = tid; u < 3 * 9 * HD_C / 8; u += 256)
         *reinterpret_cast<u16x8m*>(wl + u * 8) = *reinterpret_cast<const u16x8m*>(wc + u * 8);
-    // stage the halo tile: unit u = (pixel u / 16, 16-B chunk u % 16); a pixel's 16 chunks are 16
-    // consecutive lanes, so its sum of squares is a 16-lane shuffle reduction
+    // halo tile unit u = (pixel u / 16, 16-B chunk u % 16); a pixel's 16 chunks are 16 consecutive
+    // lanes, so its sum of squares is a 16-lane shuffle reduction
     constexpr int UNITS = HD_TR * HD_TC * 16;
     constexpr int PER = (UNITS + 255) / 256;
     u16x8m v[PER];
-    bool inb[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
+    auto in_b = [&](int k, int y0) {
         const int u = tid + k * 256;
-        const int pix = u >> 4, ch = u & 15;
+        const int pix = u >> 4;
         const int ty = pix / HD_TC, tx = pix - ty * HD_TC;
         const int gy = y0 + ty - 1, gx = x0 + tx - 1;
-        inb[k] = u < UNITS && gy >= 0 && gy < H && gx >= 0 && gx < W;
-        v[k] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
-        if (inb[k]) v[k] = *reinterpret_cast<const u16x8m*>(img + ((int64_t)gy * W + gx) * HD_C + ch * 8);
-    }
+        return u < UNITS && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    };
+    auto load = [&](int y0) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int u = tid + k * 256;
+            const int pix = u >> 4, ch = u & 15;
+            const int ty = pix / HD_TC, tx = pix - ty * HD_TC;
+            const int gy = y0 + ty - 1, gx = x0 + tx - 1;
+            v[k] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+            if (in_b(k, y0)) v[k] = *reinterpret_cast<const u16x8m*>(img + ((int64_t)gy * W + gx) * HD_C + ch * 8);
+        }
+    };
     float wv[8], bv[8];
     {
         const int ch = tid & 15;  // every unit of this thread has the same chunk (256 % 16 == 0)
@@ -948,58 +965,66 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
 #pragma unroll
         for (int i = 0; i < 8; ++i) { wv[i] = b2f(qw[i]); bv[i] = b2f(qb[i]); }
     }
+    const int n = lane & 15, g = lane >> 4;
+    const float bias = (n < 3 && cb) ? b2f(cb[n]) : 0.f;
+    load(band_lo * HD_TH);
+#pragma unroll 1
+    for (int band = band_lo; band < band_hi; ++band) {
+        const int y0 = band * HD_TH;
+        if (band > band_lo) __syncthreads();  // every wave's conv reads of the previous band are done
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int u = tid + k * 256;
-        float f[8], ss = 0.f;
+        for (int k = 0; k < PER; ++k) {
+            const int u = tid + k * 256;
+            float f[8], ss = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { f[i] = b2f(v[k][i]); ss += f[i] * f[i]; }
+            for (int i = 0; i < 8; ++i) { f[i] = b2f(v[k][i]); ss += f[i] * f[i]; }
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);  // within the pixel's 16 lanes
-        const float rstd = rsqrtf(ss / HD_C + eps);
-        u16x8m o8 = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (inb[k]) {
+            for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);  // within the pixel's 16 lanes
+            const float rstd = rsqrtf(ss / HD_C + eps);
+            u16x8m o8 = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (in_b(k, y0)) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                float t = f[i] * rstd;
-                t *= wv[i];
-                t += bv[i];
-                o8[i] = f2b(t > 0.f ? t : 0.f);
+                for (int i = 0; i < 8; ++i) {
+                    float t = f[i] * rstd;
+                    t *= wv[i];
+                    t += bv[i];
+                    o8[i] = f2b(t > 0.f ? t : 0.f);
+                }
+            }
+            if (u < UNITS) *reinterpret_cast<u16x8m*>(tile + hd_slot(u >> 4, u & 15)) = o8;
+        }
+        if (band + 1 < band_hi) load(y0 + HD_TH);
+        __syncthreads();
+        // conv: wave w computes output rows 2w, 2w+1 (one 16-pixel M-tile each)
+        hd_f32x4 acc[2] = {hd_f32x4{0.f, 0.f, 0.f, 0.f}, hd_f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 4
+        for (int s = 0; s < 36; ++s) {
+            const int tap = s >> 2, cq = s & 3, dy = tap / 3, dx = tap - 3 * (tap / 3);
+            hd_bf16x8 bf;
+            if (n < 3) {
+                bf = *reinterpret_cast<const hd_bf16x8*>(wl + (n * 9 + tap) * HD_C + cq * 32 + g * 8);
+            } else {
+                const u16x8m z = {0, 0, 0, 0, 0, 0, 0, 0};
+                bf = __builtin_bit_cast(hd_bf16x8, z);
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int oy = wave * 2 + r;
+                const hd_bf16x8 af =
+                    *reinterpret_cast<const hd_bf16x8*>(tile + hd_slot((oy + dy) * HD_TC + n + dx, cq * 4 + g));
+                acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[r], 0, 0, 0);
             }
         }
-        if (u < UNITS) *reinterpret_cast<u16x8m*>(tile + hd_slot(u >> 4, u & 15)) = o8;
-    }
-    __syncthreads();
-    // conv: wave w computes output rows 2w, 2w+1 (one 16-pixel M-tile each)
-    const int n = lane & 15, g = lane >> 4;
-    hd_f32x4 acc[2] = {hd_f32x4{0.f, 0.f, 0.f, 0.f}, hd_f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll 4
-    for (int s = 0; s < 36; ++s) {
-        const int tap = s >> 2, cq = s & 3, dy = tap / 3, dx = tap - 3 * (tap / 3);
-        hd_bf16x8 bf;
+        // C[m = pixel 4g + e][col = output channel n]
         if (n < 3) {
-            bf = *reinterpret_cast<const hd_bf16x8*>(wl + (n * 9 + tap) * HD_C + cq * 32 + g * 8);
-        } else {
-            const u16x8m z = {0, 0, 0, 0, 0, 0, 0, 0};
-            bf = __builtin_bit_cast(hd_bf16x8, z);
-        }
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int oy = wave * 2 + r;
-            const hd_bf16x8 af = *reinterpret_cast<const hd_bf16x8*>(tile + hd_slot((oy + dy) * HD_TC + n + dx, cq * 4 + g));
-            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[r], 0, 0, 0);
-        }
-    }
-    // C[m = pixel 4g + e][col = output channel n]
-    if (n < 3) {
-        const float bias = cb ? b2f(cb[n]) : 0.f;
+            for (int r = 0; r < 2; ++r) {
+                const int yy = y0 + wave * 2 + r;
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int yy = y0 + wave * 2 + r;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int xx = x0 + 4 * g + e;
-                if (yy < H && xx < W) y[(((int64_t)b * H + yy) * W + xx) * 3 + n] = f2b(acc[r][e] + bias);
+                for (int e = 0; e < 4; ++e) {
+                    const int xx = x0 + 4 * g + e;
+                    if (yy < H && xx < W) y[(((int64_t)b * H + yy) * W + xx) * 3 + n] = f2b(acc[r][e] + bias);
+                }
             }
         }
     }
@@ -1760,11 +1785,13 @@ extern "C" int eggroll_dcae_head(const void* x, int64_t B, int64_t H, int64_t W,
     EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)norm_w & 15) == 0 && ((uintptr_t)norm_b & 15) == 0 &&
                   ((uintptr_t)conv_w & 15) == 0, "dcae_head: pointers must be 16-byte aligned");
     const int64_t bands = (H + HD_TH - 1) / HD_TH, xtiles = (W + HD_TW - 1) / HD_TW;
-    const int64_t nblk = B * bands * xtiles;
+    // bands per block: enough blocks to fill 256 CUs x 3 many times over, the rest walked in-block
+    const int64_t tpb = EGG_HEAD_TPB;
+    const int64_t nblk = B * ((bands + tpb - 1) / tpb) * xtiles;
     EGG_CHECK_ARG(nblk < (1ll << 31), "dcae_head: grid too large");
     hipLaunchKernelGGL(k_dcae_head, dim3((unsigned)nblk), dim3(256), 0, as_stream(stream), (const unsigned short*)x,
                        (int)H, (int)W, eps, (const unsigned short*)norm_w, (const unsigned short*)norm_b,
-                       (const unsigned short*)conv_w, (const unsigned short*)conv_b, (int)xtiles, (int)bands,
+                       (const unsigned short*)conv_w, (const unsigned short*)conv_b, (int)xtiles, (int)bands, (int)tpb,
                        (unsigned short*)y);
     EGG_CHECK_LAUNCH("dcae_head");
     return EGGROLL_OK;
