@@ -1146,7 +1146,7 @@ __global__ __launch_bounds__(256) void k_clip_resize_v(const unsigned char* __re
 #define EGG_XA_PREFETCH 1
 #endif
 constexpr int XA_LMAX = 320;          // keys per (caption, head) staged in LDS
-constexpr int XA_KF = XA_LMAX / 16;   // key fragments
+constexpr int XA_LMAX_128 = 256;      // the same at head dim 128 (2 x 256 x 136 x 2 B of k / v)
 
 template <int RS>
 __device__ __forceinline__ la_bf16x8 xa_tr8_perm(const unsigned short* base, int lane) {
@@ -1160,7 +1160,7 @@ __device__ __forceinline__ la_bf16x8 xa_tr8_perm(const unsigned short* base, int
     return __builtin_bit_cast(la_bf16x8, f);
 }
 
-template <int HD, int NWAVE, int QF>
+template <int HD, int NWAVE, int QF, int LM = XA_LMAX>
 __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short* __restrict__ q, int64_t ldq,
                                                     const unsigned short* __restrict__ k,
                                                     const unsigned short* __restrict__ v, int64_t ldkv,
@@ -1170,10 +1170,10 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     // NWAVE waves sweep the image's queries in blocks of 16 * QF (QF query fragments share every k / v
     // fragment read from LDS)
     constexpr int RS = HD + 8, KSN = (HD + 31) / 32, DF = HD / 16;  // LDS row stride, Q.K k-steps, PV dim frags
-    static_assert(HD % 16 == 0 && HD <= 128, "head dim");
-    __shared__ __attribute__((aligned(16))) unsigned short sk[XA_LMAX * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short sv[XA_LMAX * RS];
-    __shared__ float sb[XA_LMAX];
+    static_assert(HD % 16 == 0 && HD <= 128 && LM % 32 == 0, "head dim / key capacity");
+    __shared__ __attribute__((aligned(16))) unsigned short sk[LM * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short sv[LM * RS];
+    __shared__ float sb[LM];
     constexpr int NT = 64 * NWAVE;
     const int bh = xcd_remap(blockIdx.x, gridDim.x);
     const int b = bh / heads, h = bh - b * heads;
@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
     // stage k / v rows of caption u, head h: 14 chunks of 16 B per row; rows >= L are zeros
     constexpr int CH = HD / 8;
-    for (int c = tid; c < XA_LMAX * CH; c += NT) {
+    for (int c = tid; c < LM * CH; c += NT) {
         const int r = c / CH, cc = c - r * CH;
         u16x8m kv = u16x8m{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
         if (r < L) {
@@ -1194,7 +1194,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
         *reinterpret_cast<u16x8m*>(sk + r * RS + cc * 8) = kv;
         *reinterpret_cast<u16x8m*>(sv + r * RS + cc * 8) = vv;
     }
-    for (int r = tid; r < XA_LMAX; r += NT)
+    for (int r = tid; r < LM; r += NT)
         sb[r] = u_bad ? __builtin_nanf("") : r < L ? (bias ? b2f(bias[(int64_t)u * L + r]) : 0.0f) : -INFINITY;
     __syncthreads();
     const int nkf = (L + 15) / 16, nkb = (L + 31) / 32;  // key fragments / 32-key PV steps in use
@@ -1228,12 +1228,12 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
             load_q(qb, bq);
         }
         // S^T[key][query] for every key fragment
-        la_f32x4 sf[QF][XA_KF];
+        la_f32x4 sf[QF][(LM / 16)];
         float mx[QF];
 #pragma unroll
         for (int x = 0; x < QF; ++x) mx[x] = -INFINITY;
 #pragma unroll
-        for (int f = 0; f < XA_KF; ++f) {
+        for (int f = 0; f < (LM / 16); ++f) {
 #pragma unroll
             for (int x = 0; x < QF; ++x) sf[x][f] = la_f32x4{0.f, 0.f, 0.f, 0.f};
             if (f < nkf) {
@@ -1267,7 +1267,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
             sum[x] = 0.0f;
         }
 #pragma unroll
-        for (int f = 0; f < XA_KF; ++f) {
+        for (int f = 0; f < (LM / 16); ++f) {
             if (f < nkf) {
 #pragma unroll
                 for (int x = 0; x < QF; ++x)
@@ -1291,7 +1291,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
 #pragma unroll
             for (int d = 0; d < DF; ++d) oc[x][d] = la_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < XA_KF / 2; ++j) {
+        for (int j = 0; j < (LM / 16) / 2; ++j) {
             if (j < nkb) {
                 la_bf16x8 bp[QF];
 #pragma unroll
@@ -2218,9 +2218,12 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
                                        const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
                                        int64_t heads, int64_t head_dim, int64_t L, int64_t U, float scale, void* o,
                                        int64_t ldo, void* stream) {
-    EGG_CHECK_ARG(head_dim == 64 || head_dim == 80 || head_dim == 112, "cross_attention: head_dim %lld unsupported "
-                  "(64, 80, 112)", (long long)head_dim);
-    EGG_CHECK_ARG(B >= 0 && N > 0 && heads > 0 && L > 0 && L <= XA_LMAX, "cross_attention: bad sizes (L <= %d)", XA_LMAX);
+    EGG_CHECK_ARG(head_dim == 64 || head_dim == 80 || head_dim == 112 || head_dim == 128, "cross_attention: head_dim "
+                  "%lld unsupported (64, 80, 112, 128)", (long long)head_dim);
+    // head dim 128 (Infinity's text cross-attention) stages at most 256 keys: k + v at 320 would not fit 160 KiB
+    const int64_t lmax = head_dim == 128 ? XA_LMAX_128 : XA_LMAX;
+    EGG_CHECK_ARG(B >= 0 && N > 0 && heads > 0 && L > 0 && L <= lmax, "cross_attention: bad sizes (L <= %lld at head "
+                  "dim %lld)", (long long)lmax, (long long)head_dim);
     EGG_CHECK_ARG(U > 0 && U * L < (1ll << 31) && (enc_index || U >= B),
                   "cross_attention: U=%lld caption rows (need U >= B without enc_index)", (long long)U);
     EGG_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldo % 4 == 0 && ldq >= heads * head_dim &&
@@ -2233,14 +2236,15 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
     // 8 waves x 16-query blocks (164 VGPRs, 2 waves per SIMD): measured 0.80 ms at the Sana attn2 shape
     // (B 128, N 1024, 20 heads, L 300) vs 0.94 for 4 waves x 32 queries and 1.27 for 4 x 16 (SDPA on
     // the gathered k / v with the mask: 1.53 ms)
-#define EGG_XA(HD_)                                                                                              \
-    hipLaunchKernelGGL((k_cross_attn<HD_, 8, 1>), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream),  \
+#define EGG_XA(HD_, LM_)                                                                                         \
+    hipLaunchKernelGGL((k_cross_attn<HD_, 8, 1, LM_>), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream), \
                        (const unsigned short*)q, ldq, (const unsigned short*)k, (const unsigned short*)v, ldkv,    \
                        (const unsigned short*)bias, enc_index, (int)heads, (int)N, (int)L, (int)U, scale, (unsigned short*)o, \
                        ldo)
-    if (head_dim == 112) EGG_XA(112);
-    else if (head_dim == 80) EGG_XA(80);
-    else EGG_XA(64);
+    if (head_dim == 112) EGG_XA(112, XA_LMAX);
+    else if (head_dim == 128) EGG_XA(128, XA_LMAX_128);
+    else if (head_dim == 80) EGG_XA(80, XA_LMAX);
+    else EGG_XA(64, XA_LMAX);
 #undef EGG_XA
     EGG_CHECK_LAUNCH("cross_attention");
     return EGGROLL_OK;

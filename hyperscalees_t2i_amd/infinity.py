@@ -386,9 +386,16 @@ class InfinityPopulationInfer:
         # cross-attention to the text (keys: this row's prompt, cond or uncond)
         cn = blk.ca_norm
         h = K.rownorm(x, a.norm_eps, layer=True, w=cn.weight, b=cn.bias)
-        q = blk.ca.mat_q(h).view(N2, l, H, hd).transpose(1, 2)
-        o = F.scaled_dot_product_attention(q, cak, cav, attn_mask=cabias, scale=hd ** -0.5)
-        blk.ca.proj(o.transpose(1, 2).reshape(N2 * l, C), epi="res", res=x)
+        if isinstance(cak, tuple):   # eggroll_cross_attention: k / v read in place from the distinct text rows
+            kvo, drow_i, bias16 = cak
+            Lt = bias16.shape[1]
+            o = K.cross_attention(blk.ca.mat_q(h), kvo[:, :C], kvo[:, C:], N2, l, H, hd, Lt, hd ** -0.5,
+                                  bias=bias16, enc_index=drow_i)
+        else:
+            q = blk.ca.mat_q(h).view(N2, l, H, hd).transpose(1, 2)
+            o = F.scaled_dot_product_attention(q, cak, cav, attn_mask=cabias, scale=hd ** -0.5)
+            o = o.transpose(1, 2).reshape(N2 * l, C)
+        blk.ca.proj(o, epi="res", res=x)
         h = K.rownorm(x, a.norm_eps, layer=True, mscale=mod32[:, 3], mshift=mod32[:, 5], rows_per_group=l)
         f = blk.ffn.fc1(h, epi="gelu")          # GELU(tanh) in the GEMM epilogue where it applies
         blk.ffn.fc2(f, epi="gated", res=x, gate=mod16[:, 1], rows_per_group=l)
@@ -426,10 +433,18 @@ class InfinityPopulationInfer:
         # per-block constants: modulation rows (fp32 for the norms, bf16 gates for the epilogues) and the
         # text keys / values gathered per row
         mods, cas = [], []
+        # text cross-attention on eggroll_cross_attention (head dim 128 stages <= 256 keys): each row's k / v
+        # are its distinct text row's, addressed through enc_index = drow, the mask an additive bf16 bias
+        xa_kernel = self.use_kernel and hd == 128 and Lt <= 256
+        if xa_kernel:
+            drow_i, bias16 = drow.to(torch.int32).contiguous(), bias.to(torch.bfloat16).contiguous()
         for blk in blocks:
             m32 = (blk.ada_gss.view(1, 6, C) + shared.view(-1, 6, C))[drow].contiguous()    # [N2, 6, C]
             m16 = m32[:, :2].to(torch.bfloat16).contiguous()
             mods.append((m32, m16))
+            if xa_kernel:
+                cas.append(((blk.ca.mat_kv(cat.reshape(2 * U * Lt, -1)), drow_i, bias16), None))
+                continue
             kvt = blk.ca.mat_kv(cat).view(2 * U, Lt, 2, H, hd)
             cas.append((kvt[:, :, 0][drow].transpose(1, 2), kvt[:, :, 1][drow].transpose(1, 2)))
         caches = [torch.empty((2, N2, ltot, C), dtype=torch.bfloat16, device=dev) for _ in blocks]

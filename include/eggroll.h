@@ -398,7 +398,8 @@ int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, int64_t W, in
  * q / o bf16 rows b*N + n (head h at columns h*head_dim), k / v bf16 rows u*L + j (U caption rows); bias
  * bf16 [U][L] or NULL; enc_index int32 [B] or NULL (u = b, needs U >= B).  An enc_index entry outside
  * [0, U) gives that image NaN output (no out-of-bounds read).  head_dim 64 / 80 / 112 (112: Sana attn2;
- * 64 / 80: the CLIP towers' self-attention), L <= 320; MFMA, fp32 softmax.                           */
+ * 64 / 80: the CLIP towers' self-attention), L <= 320; head_dim 128 (Infinity's text cross-attention,
+ * models/Infinity.py CrossAttention), L <= 256.  MFMA, fp32 softmax.                                  */
 int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, const void* bias,
                             const int32_t* enc_index, int64_t B, int64_t N, int64_t heads, int64_t head_dim,
                             int64_t L, int64_t U, float scale, void* o, int64_t ldo, void* stream);

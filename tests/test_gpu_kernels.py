@@ -11,7 +11,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from hyperscalees_t2i_amd import kernels as K
+from hyperscalees_t2i_amd import _lib, kernels as K
 from hyperscalees_t2i_amd.es import EggRollNoiser, paper_prompt_normalized_scores, standardize_fitness
 from oracle import eggroll_oracle as O
 
@@ -1079,21 +1079,28 @@ def test_lora_epilogue_fp32_stream_bitexact(dev, epi, r, M, N, Kd, rpm, kernel):
     assert torch.equal(got, ref) and torch.equal(sh, ref_sh)
 
 
-@pytest.mark.parametrize("B,N,H,L,U", [(4, 64, 2, 37, 2), (3, 100, 3, 300, 3), (6, 17, 1, 320, 2), (16, 1024, 20, 300, 4)])
-def test_cross_attention_vs_sdpa(dev, B, N, H, L, U):
+@pytest.mark.parametrize("B,N,H,L,U,hd", [(4, 64, 2, 37, 2, 112), (3, 100, 3, 300, 3, 112), (6, 17, 1, 320, 2, 112),
+                                           (16, 1024, 20, 300, 4, 112),
+                                           # Infinity text cross-attention: head dim 128, k / v interleaved in
+                                           # one [U*L, 2C] row (mat_kv), -inf masks, rows -> text rows
+                                           (8, 36, 4, 77, 4, 128), (6, 145, 2, 256, 3, 128), (5, 1, 3, 20, 2, 128)])
+def test_cross_attention_vs_sdpa(dev, B, N, H, L, U, hd):
     """eggroll_cross_attention (MFMA, caption rows through enc_index, additive mask) vs fp32 SDPA on the
     gathered k / v; ragged N, L not a multiple of 16/32, fully-valid and heavily-masked captions."""
     import torch.nn.functional as F
-    hd = 112
     g = torch.Generator(device=dev).manual_seed(B * 131 + L)
     q = torch.randn((B * N, H * hd), generator=g, device=dev).to(torch.bfloat16)
-    k = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
-    v = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
+    if hd == 128:
+        kv = torch.randn((U * L, 2 * H * hd), generator=g, device=dev).to(torch.bfloat16)
+        k, v = kv[:, :H * hd], kv[:, H * hd:]
+    else:
+        k = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
+        v = torch.randn((U * L, H * hd), generator=g, device=dev).to(torch.bfloat16)
     lens = [L] + [int(x) for x in torch.randint(1, L + 1, (U - 1,), generator=g, device=dev).tolist()]
     bias = torch.zeros((U, L), device=dev, dtype=torch.bfloat16)
     for u, n_valid in enumerate(lens):
-        bias[u, n_valid:] = -10000.0
-    enc_index = torch.arange(B, device=dev) % U
+        bias[u, n_valid:] = float("-inf") if hd == 128 else -10000.0
+    enc_index = torch.arange(B, device=dev) % U if hd != 128 else torch.randint(0, U, (B,), generator=g, device=dev)
     ours = K.cross_attention(q, k, v, B, N, H, hd, L, hd ** -0.5, bias=bias, enc_index=enc_index).float()
     qq = q.view(B, N, H, hd).transpose(1, 2).float()
     kk = k.view(U, L, H, hd)[enc_index].transpose(1, 2).float()
@@ -1125,6 +1132,11 @@ def test_cross_attention_out_of_range_caption_is_nan_not_oob(dev):
     with pytest.raises(ValueError):
         K.cross_attention(q, k, v, B, N, H, hd, L, 0.1, bias=torch.zeros((U, L + 1), device=dev, dtype=torch.bfloat16),
                           enc_index=torch.tensor([0, 1, 1], device=dev))
+    # head dim 128 stages at most 256 keys per (text row, head)
+    q8 = torch.zeros((2, 128), device=dev, dtype=torch.bfloat16)
+    k8 = torch.zeros((257, 128), device=dev, dtype=torch.bfloat16)
+    with pytest.raises(_lib.EggrollError, match="L <= 256"):
+        K.cross_attention(q8, k8, k8, 2, 1, 1, 128, 257, 0.1, enc_index=torch.tensor([0, 0], device=dev))
 
 
 @pytest.mark.parametrize("M,Kd,r,n_lin,rpm", [
