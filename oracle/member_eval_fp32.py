@@ -255,9 +255,10 @@ def _msla(at, x, bf=lambda t, c: t):
 
 
 def generate_fp32(es_model, theta_k, prompt_embeds, prompt_mask, latents, guidance_scale: float,
-                  record: Optional[list] = None, rnd=(), drnd=()):
+                  record: Optional[list] = None, rnd=(), drnd=(), decode_chunk: Optional[int] = None):
     """models/SanaSprint.py:96-160 with the build's weights in fp32: (eps_pred, image); rnd: see
-    transformer_fp32."""
+    transformer_fp32; decode_chunk: decode that many images at a time (the decoder is per image, so
+    chunking changes no value; it bounds the fp32 feature maps at 1024 px)."""
     b = latents.shape[0]
     sd = es_model.sigma_data
     lmi = latents / sd
@@ -268,13 +269,16 @@ def generate_fp32(es_model, theta_k, prompt_embeds, prompt_mask, latents, guidan
     guidance = guidance * es_model.transformer_config.guidance_embeds_scale
     eps = transformer_fp32(es_model.transformer, theta_k, lmi.to(f32), scm, prompt_embeds.to(f32), prompt_mask,
                            guidance.to(f32), record, rnd)
-    return eps, decode_fp32(es_model, eps, latents, drnd)
+    return eps, decode_fp32(es_model, eps, latents, drnd, decode_chunk)
 
 
-def decode_fp32(es_model, eps, latents, drnd=()):
+def decode_fp32(es_model, eps, latents, drnd=(), chunk: Optional[int] = None):
     """models/SanaSprint.py:133-160 after the transformer: nan_to_num, SCM combine (the reference's fp16
     casts), x0, fp32 DC-AE decode.  Also used on the build's bf16 transformer output to split the image
     drift into its transformer and DC-AE parts."""
+    if chunk is not None and eps.shape[0] > chunk:
+        return torch.cat([decode_fp32(es_model, eps[i:i + chunk], latents[i:i + chunk], drnd)
+                          for i in range(0, eps.shape[0], chunk)])
     sd = es_model.sigma_data
     lmi = latents / sd
     se = (torch.sin(torch.tensor(1.571, device=latents.device, dtype=f32))

@@ -311,6 +311,31 @@ def gen_member_eval_injection(u):
     return len(recs)
 
 
+def gen_member_eval_fullsize(u):
+    """g12: reference EggRollNoiser factors captured on the FULL Sana-Sprint 1.6B LoRA theta layout
+    (SanaArch() defaults: 168 targets, 336 matrices, D = 1,515,456; LoRA r 2), pop 2 (one antithetic
+    pair = one base sample), egg rank 1, sigma 1e-2 — the injected noise of the full-size bf16-vs-fp32
+    member-eval test (tests/test_gpu_parity_fullsize.py).  eps itself (2 x D fp32) is not stored: the
+    test checks its reproduction through a sha256 of member 0's eps bytes plus 4096 sampled values."""
+    sys.path.insert(0, str(OUT.parent.parent))
+    import hashlib
+    from hyperscalees_t2i_amd.sana import SanaArch, sana_lora_shapes
+    shapes = sana_lora_shapes(SanaArch())
+    torch.manual_seed(12)
+    noiser = u.EggRollNoiser([torch.Size(s) for s in shapes], sigma=1e-2, lr_scale=0.1, rank=1,
+                             use_antithetic=True)
+    with RandnRecorder() as rr:
+        eps = noiser.sample_eps(2, "cpu")
+    assert torch.equal(eps[1], -eps[0])
+    parts = [t.reshape(1, -1) for t in rr.calls]
+    idx = torch.randperm(eps.shape[1], generator=torch.Generator().manual_seed(3))[:4096].sort()[0]
+    recs = {"shapes": np.array(shapes, np.int64), "factors": torch.cat(parts, dim=1).numpy(),
+            "sigma": np.array(1e-2, np.float32), "eps0_idx": idx.numpy(), "eps0_at_idx": eps[0, idx].numpy(),
+            "eps0_sha256": np.array(hashlib.sha256(eps[0].contiguous().numpy().tobytes()).hexdigest())}
+    np.savez_compressed(OUT / "g12_member_eval_fullsize.npz", **recs)
+    return len(recs)
+
+
 VAR_TARGETS = ["mat_qkv", "proj", "fc1", "fc2", "ada_lin.1", "head_nm.ada_lin.1", "head"]  # unifed_es.py:406
 
 
@@ -546,10 +571,14 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["var_model"]:          # regenerate g11 only
         print("gen_var_model", gen_var_model())
         raise SystemExit(0)
+    if sys.argv[1:] == ["fullsize"]:           # regenerate g12 only
+        torch.set_num_threads(1)
+        print("gen_member_eval_fullsize", gen_member_eval_fullsize(load_reference()))
+        raise SystemExit(0)
     u = load_reference()
     torch.set_num_threads(1)
     for fn in (gen_eps, gen_fitness, gen_update, gen_indices, gen_sampling_info, gen_es_tail, gen_lora,
-               gen_member_eval_injection):
+               gen_member_eval_injection, gen_member_eval_fullsize):
         print(fn.__name__, fn(u))
     print("gen_s_aggregation", gen_s_aggregation())
     print("gen_var", gen_var())

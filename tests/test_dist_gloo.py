@@ -1,7 +1,9 @@
-"""World-size-2 gloo tests of the member sharding and the S all-gather (CPU, no GPU)."""
+"""gloo tests (CPU, no GPU) of the member sharding, the S all-gather and the replica check at world sizes
+2, 3 and 8 (BASELINE configs[2]: pop 64 over 8 ranks)."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -36,7 +38,7 @@ def _worker(rank, world, port, pop, m, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pop,world", [(8, 2), (7, 2), (5, 3)])
+@pytest.mark.parametrize("pop,world", [(8, 2), (7, 2), (5, 3), (64, 8)])
 def test_allgather_members_gloo(pop, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -49,6 +51,75 @@ def test_allgather_members_gloo(pop, world):
         p.join(timeout=60)
     assert all(ok for _, ok, _, _ in res)
     assert len({(tuple(o), fb) for _, _, o, fb in res}) == 1  # identical on all ranks
+
+
+def _epoch_worker(rank, world, port, pop, m, q):
+    """One configs[2]-shaped ES epoch tail on a rank: its members' S rows (each a function of the member
+    index only, as a member's evaluation is), the S all-gather, then fitness -> EGGROLL update -> theta
+    cap on the gathered S with the noise regenerated locally from (seed, base sample) (kernel (1)'s
+    contract, oracle restatement), and the replica check."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        theta, eps = _epoch_inputs(pop)
+        lo, hi = member_shard(pop, rank, world)
+        local = torch.stack([_member_scores(k, m) for k in range(lo, hi)])
+        S = all_gather_members(local, pop, DistInfo(rank, world))
+        after, info = O.ref_es_tail(S.numpy(), eps, theta, promptnorm=True, lr_scale=0.1, sigma=0.01,
+                                    max_step_norm=0.0, theta_max_norm=40.0)
+        verify_theta_replicas(torch.from_numpy(after), DistInfo(rank, world))
+        q.put((rank, hi - lo, after.tobytes(), info["order"].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+SHAPES_SMALL = [(2, 12), (10, 2), (2, 7), (5, 2)]
+
+
+def _epoch_inputs(pop):
+    lay = O.layout(SHAPES_SMALL, 1)
+    fac = O.noise_factors(9, 0, O.n_base_samples(pop, True), lay["factor_len"])
+    # the per-matrix [a | b] factor vector with the device layout's 4-float padding removed
+    eps = O.dev_eps_rows(_unpad(fac, SHAPES_SMALL), SHAPES_SMALL, pop, 1, True, 0, pop)
+    theta = np.random.default_rng(4).standard_normal(eps.shape[1]).astype(np.float32)
+    return theta, eps
+
+
+def _unpad(fac, shapes):
+    parts, off = [], 0
+    for mm, nn in shapes:
+        for n in (mm, nn):
+            parts.append(fac[:, off:off + n])
+            off += -(-n // 4) * 4
+    return np.concatenate(parts, axis=1)
+
+
+def _member_scores(k, m):
+    return torch.randn(m, generator=torch.Generator().manual_seed(1000 + k)) + 20
+
+
+def test_configs2_eight_rank_epoch_gloo():
+    """BASELINE configs[2]'s partition (pop 64 over 8 ranks, 8 members each) on CPU gloo: every rank
+    ends with the same theta' (verify_theta_replicas passes on all 8), equal bit for bit to the
+    single-process epoch tail over the whole population."""
+    pop, world, m = 64, 8, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_epoch_worker, args=(r, world, port, pop, m, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(n for _, n, _, _ in res) == [8] * 8
+    theta, eps = _epoch_inputs(pop)
+    S = torch.stack([_member_scores(k, m) for k in range(pop)]).numpy()
+    after, info = O.ref_es_tail(S, eps, theta, promptnorm=True, lr_scale=0.1, sigma=0.01, max_step_norm=0.0,
+                                theta_max_norm=40.0)
+    assert {b for _, _, b, _ in res} == {after.tobytes()}
+    assert all(o == info["order"].tolist() for _, _, _, o in res)
+    assert not np.array_equal(after, theta)
 
 
 def test_member_shard_partition():
@@ -76,13 +147,13 @@ def _verify_worker(rank, world, port, diverge, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("diverge", [False, True])
-def test_verify_theta_replicas_gloo(diverge):
+@pytest.mark.parametrize("diverge,world", [(False, 2), (True, 2), (False, 8), (True, 8)])
+def test_verify_theta_replicas_gloo(diverge, world):
     """theta checksum all-reduce (SURVEY §8e debug): silent when replicas agree, raises on EVERY rank
     when one rank's theta differs by one ulp in one element."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port, world = _free_port(), 2
+    port = _free_port()
     procs = [ctx.Process(target=_verify_worker, args=(r, world, port, diverge, q)) for r in range(world)]
     for p in procs:
         p.start()

@@ -51,10 +51,11 @@ BOUNDS = {   # ~1.5x the round-4 measurement (fp32 residual streams in the Sana 
 S1_SCORE_ERR = 0.006
 KEYS = ("lora_rel", "eps_rel", "image_rel", "reward_abs", "S_abs")
 # test_rank_fidelity_over_seeds (sigma 1e-2, 12 epochs' seeds x 8 members, 336 member pairs): max |dS| at
-# ~1.5x the measurement; pooled Kendall tau >= 0.95 (VERDICT r2 bar) = up to 8 discordant pairs, 3 more
-# than measured; best / worst member may differ in at most 2 of the 12 epochs (measured: 0 / 1)
-RANK_BOUNDS = {"S_abs": 0.016, "pooled_tau": 0.95,   # measured (round 4, 12 seeds): S_abs 0.0105, pooled tau 0.970
-               "best_worst_misses": 2}
+# ~1.5x the measurement; pooled Kendall tau >= 0.964 = at most 6 discordant pairs (measured 5); best / worst
+# member may differ in at most 1 of the 12 epochs (measured: best 0, worst 1).  The same bars at full model
+# size: tests/test_gpu_parity_fullsize.py
+RANK_BOUNDS = {"S_abs": 0.016, "pooled_tau": 0.964,   # measured (round 4, 12 seeds): S_abs 0.0105, pooled tau 0.970
+               "best_worst_misses": 1}
 
 
 def kendall_tau(a, b):
