@@ -306,6 +306,34 @@ def sample_bits(logits: torch.Tensor, gen: torch.Generator, top_k: int, top_p: f
     return torch.multinomial(logits.softmax(dim=-1).view(-1, V), 1, replacement=True, generator=gen).view(mb, ld)
 
 
+class ChunkedBitSampler:
+    """The reference's generation chunks as separate `autoregressive_infer_cfg` calls (es_backend.py's
+    micro_batch loop): each chunk call of each member seeds its own generator with g_seed, and that
+    generator advances across scales by the chunk's OWN draws.  One generator is replayed per chunk:
+    states[c0] is the state chunk c0's generator holds before the current scale.  Members start every
+    chunk from the same state (each member's calls are independent, unifed_es.py:159-163); a smaller
+    last chunk (B % micro_batch != 0) keeps its own state sequence."""
+
+    def __init__(self, gen: torch.Generator, B: int, mb: int):
+        self.gen, self.B, self.mb = gen, int(B), int(mb)
+        st = gen.get_state()
+        self.states = {c0: st for c0 in range(0, self.B, self.mb)}
+
+    def sample(self, lg: torch.Tensor, top_k: int, top_p: float) -> torch.Tensor:
+        """lg [n, B, l*d, 2] CFG'd logits of one scale -> bits [n, B, l*d] (long)."""
+        n = lg.shape[0]
+        bits = torch.empty(lg.shape[:3], dtype=torch.long, device=lg.device)
+        for c0, pre in self.states.items():
+            c1 = min(self.B, c0 + self.mb)
+            post = None
+            for k in range(n):
+                self.gen.set_state(pre)
+                bits[k, c0:c1] = sample_bits(lg[k, c0:c1], self.gen, top_k, top_p)
+                post = self.gen.get_state()
+            self.states[c0] = post
+        return bits
+
+
 class InfinityPopulationInfer:
     """`autoregressive_infer_cfg` (models/Infinity.py:509-537) for n members at once."""
 
@@ -451,7 +479,7 @@ class InfinityPopulationInfer:
         x = (sos[drow] + tr.pos_start.float().view(1, C)).to(torch.bfloat16).contiguous()   # [N2 * 1, C]
         summed = torch.zeros((n * B, a.codebook_dim, vside, vside), dtype=torch.float32, device=dev)
         mb = B if micro_batch <= 0 or micro_batch >= B else int(micro_batch)
-        gen = torch.Generator(device=dev).manual_seed(int(g_seed))
+        sampler = ChunkedBitSampler(torch.Generator(device=dev).manual_seed(int(g_seed)), B, mb)
         bits_all, logits_all = [], []
         cur = 0
         for si, (_, h, w) in enumerate(schedule):
@@ -473,12 +501,7 @@ class InfinityPopulationInfer:
             if force_bits is not None:
                 bits = force_bits[si].to(dev).view(n, B, l * a.d_tok).long()
             else:
-                st = gen.get_state()
-                bits = torch.empty((n, B, l * a.d_tok), dtype=torch.long, device=dev)
-                for k in range(n):
-                    for c0 in range(0, B, mb):   # each reference chunk call starts from the same state
-                        gen.set_state(st)
-                        bits[k, c0:c0 + mb] = sample_bits(lg[k, c0:c0 + mb], gen, top_k, top_p)
+                bits = sampler.sample(lg, top_k, top_p)
             bits = bits.view(n * B, l, a.d_tok)
             bits_all.append(bits)
             codes = bits_to_codes(bits, a, h, w)

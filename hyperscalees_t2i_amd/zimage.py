@@ -287,6 +287,13 @@ class ZImageTransformer2DModel(nn.Module):
         hp, wp = H // a.patch, W // a.patch
         N, D, dev = hp * wp, a.dim, lat.device
         m = a.seq_multiple
+        if N % m:
+            # diffusers pads the image sequence to a multiple of seq_multiple with x_pad_token; those pad
+            # tokens take part in attention (and their RoPE positions are unpinned here), so an image
+            # whose token count is not a multiple would run a different sequence from the reference
+            raise NotImplementedError(f"{hp} x {wp} = {N} image tokens is not a multiple of seq_multiple {m}: "
+                                      f"image-token padding (x_pad_token) is not implemented; choose a size "
+                                      f"whose patch grid has a multiple of {m} tokens (e.g. 384 or 512 px)")
         real = [int(v) for v in cap_lens.tolist()]
         padl = [-(-r // m) * m for r in real]
         if max(padl) > Lc:

@@ -28,10 +28,15 @@ from .pipeline import to_pil
 from .zimage import ZIMAGE_TURBO, ZImageArch, ZImageTransformer2DModel
 
 
-def flow_sigmas(steps: int, shift: float = 3.0, num_train: int = 1000) -> List[float]:
-    """FlowMatchEulerDiscreteScheduler(shift).set_timesteps(steps).sigmas (static shifting)."""
+def flow_sigmas(steps: int, shift: float = 3.0, num_train: int = 1000,
+                sigma_min: Optional[float] = 0.0) -> List[float]:
+    """FlowMatchEulerDiscreteScheduler(shift).set_timesteps(steps).sigmas (static shifting) as diffusers'
+    ZImagePipeline calls it: the pipeline sets `scheduler.sigma_min = 0.0` before set_timesteps, so the
+    unshifted grid runs linspace(1, 0, steps), is shifted, and a final 0 is appended — the last step has
+    dt = 0 (a no-op update).  sigma_min=None keeps the scheduler's own default, shift(1 / num_train)."""
     sh = lambda s: shift * s / (1.0 + (shift - 1.0) * s)  # noqa: E731
-    s_max, s_min = 1.0, sh(1.0 / num_train)
+    s_max = 1.0
+    s_min = sh(1.0 / num_train) if sigma_min is None else float(sigma_min)
     s = np.linspace(s_max * num_train, s_min * num_train, steps) / num_train
     return [float(v) for v in sh(s)] + [0.0]
 

@@ -15,7 +15,8 @@ from oracle import eggroll_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-TINY = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256)
+TINY = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256,
+                  seq_multiple=16)
 PX = 64     # 8 x 8 latent, 16 image tokens
 
 

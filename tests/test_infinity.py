@@ -112,6 +112,25 @@ def test_sample_bits_top_p_and_chunk_reseeding():
         assert torch.equal(b, sample_bits(lg[c0:c0 + 2].clone(), torch.Generator().manual_seed(7), 900, 0.97))
 
 
+@pytest.mark.parametrize("B,mb", [(5, 2), (4, 2), (7, 3), (3, 4)])
+def test_chunked_sampler_matches_independent_chunk_calls(B, mb):
+    """ChunkedBitSampler over several scales == one fresh generator per (member, chunk) seeded with g_seed
+    that sees only its own chunk's logits, scale after scale (the reference's separate chunk calls),
+    including a smaller last chunk whose draws advance its generator differently."""
+    from hyperscalees_t2i_amd.infinity import ChunkedBitSampler
+    n, seed = 2, 11
+    g = torch.Generator().manual_seed(123)
+    scales = [torch.randn(n, B, ld, 2, generator=g) for ld in (4, 9, 30)]
+    sampler = ChunkedBitSampler(torch.Generator().manual_seed(seed), B, mb)
+    got = [sampler.sample(lg.clone(), 900, 0.97) for lg in scales]
+    for k in range(n):
+        for c0 in range(0, B, mb):
+            ref = torch.Generator().manual_seed(seed)
+            for lg, b in zip(scales, got):
+                want = sample_bits(lg[k, c0:c0 + mb].clone(), ref, 900, 0.97)
+                assert torch.equal(b[k, c0:c0 + mb], want), (k, c0)
+
+
 def test_images_to_uint8_truncates():
     x = torch.tensor([-1.0, 0.0, 0.999, 1.0]).view(1, 1, 1, 4).expand(1, 3, 1, 4)
     u = images_to_uint8(x)

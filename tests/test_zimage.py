@@ -15,7 +15,8 @@ from hyperscalees_t2i_amd.zimage import (ZIMAGE_LORA_TARGETS, ZImageArch, ZImage
                                          zimage_lora_shapes)
 from hyperscalees_t2i_amd.zimage_pipeline import flow_sigmas
 
-TINY = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256)
+TINY = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256,
+                  seq_multiple=16)
 
 
 def test_theta_layout_matches_model_shapes():
@@ -37,13 +38,18 @@ def test_lora_targets_by_name():
 
 
 def test_flow_sigmas():
+    """ZImagePipeline sets scheduler.sigma_min = 0.0 before set_timesteps: shift(linspace(1, 0, steps))
+    then a final 0, so the last Euler step has dt = 0.  sigma_min=None: the scheduler's own default."""
     s = flow_sigmas(7)
-    assert len(s) == 8 and s[0] == 1.0 and s[-1] == 0.0
-    assert all(a > b for a, b in zip(s, s[1:]))
     sh = lambda v: 3 * v / (1 + 2 * v)  # noqa: E731
+    assert len(s) == 8 and s[0] == 1.0 and s[-2] == 0.0 and s[-1] == 0.0
+    assert all(a > b for a, b in zip(s[:-1], s[1:-1]))
+    assert s[1] == pytest.approx(sh(1.0 - 1.0 / 6))
+    assert s[3] == pytest.approx(sh(0.5))
+    d = flow_sigmas(7, sigma_min=None)
     smin = sh(1e-3)
-    assert s[-2] == pytest.approx(sh(smin))
-    assert s[1] == pytest.approx(sh(1.0 - (1.0 - smin) / 6))
+    assert d[-2] == pytest.approx(sh(smin)) and d[-1] == 0.0
+    assert d[1] == pytest.approx(sh(1.0 - (1.0 - smin) / 6))
 
 
 def test_patchify_roundtrip_and_positions():
@@ -108,3 +114,14 @@ def test_fp32_restatement_runs_on_cpu():
     v1 = Z.transformer_fp32(m, lat, t, cap, lens, idx, torch.randn(D) * 0.1)
     assert v0.shape == lat.shape and torch.isfinite(v0).all()
     assert (v0 - v1).abs().max() > 0
+
+
+def test_unpadded_image_token_count_raises():
+    """diffusers pads the image tokens to a multiple of seq_multiple with x_pad_token; the build does not
+    restate that padding and refuses such sizes instead of running a different sequence."""
+    with torch.device("meta"):
+        m = ZImageTransformer2DModel(TINY)
+        lat = torch.empty(1, 16, 10, 10)          # 5 x 5 = 25 image tokens, seq_multiple 16
+        with pytest.raises(NotImplementedError, match="seq_multiple"):
+            m(lat, torch.zeros(1), torch.empty(1, 16, 256), torch.zeros(1, dtype=torch.long),
+              torch.zeros(1, dtype=torch.long))
