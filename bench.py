@@ -33,7 +33,10 @@ sys.path.insert(0, str(ROOT))
 
 import torch  # noqa: E402
 
-torch.backends.cudnn.benchmark = True  # MIOpen Find per conv shape during warmup (FAST mode: 38 vs 700+ TF)
+# MIOpen Find per conv shape during warmup (FAST mode: 38 vs 700+ TF); Find picks solvers by timing, so two
+# processes can pick different ones for the same shape: EGGROLL_MIOPEN_FIND=0 (MIOpen's immediate mode)
+# makes the choice a function of the shape only (tests/test_gpu_bench_dist.py compares processes bitwise)
+torch.backends.cudnn.benchmark = os.environ.get("EGGROLL_MIOPEN_FIND", "1") == "1"
 T_START = time.perf_counter()
 
 
@@ -153,7 +156,8 @@ def build_zimage(args, world, rank, device):
 
     cfg = ZImageConfig(synthetic_weights=True)
     if args.small:
-        cfg.arch = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256)
+        cfg.arch = ZImageArch(dim=256, n_layers=2, n_refiner_layers=1, n_heads=2, ffn=512, cap_feat_dim=256, t_mid=256,
+                              seq_multiple=16)   # 64 px: 16 image tokens
         cfg.vae_widths, cfg.width_px, cfg.height_px, cfg.num_inference_steps = (32, 32, 64, 64), 64, 64, 2
     backend = ZImageBackend(device=str(device), cfg=cfg)
     backend.init_and_attach_lora()
@@ -212,8 +216,11 @@ def build(args, world, rank, device):
 
     cfg = SanaConfig(synthetic_weights=True, width_latent=args.latent, height_latent=args.latent)
     if args.small:
-        cfg.arch = SanaArch(num_attention_heads=4, attention_head_dim=32, num_layers=2, num_cross_attention_heads=2,
-                            cross_attention_head_dim=64, caption_channels=256)
+        # cross-attention head dim 112 as the full model, so attn2 runs eggroll_cross_attention (run-to-run
+        # deterministic) rather than the SDPA fallback (masked SDPA at head dim 64 is not: tools/
+        # sdpa_determinism_probe.py) — the multi-process tests compare theta' across processes bitwise
+        cfg.arch = SanaArch(num_attention_heads=14, attention_head_dim=32, num_layers=2, num_cross_attention_heads=4,
+                            cross_attention_head_dim=112, caption_channels=256)   # inner 448: K % 64 == 0
         cfg.vae_widths, cfg.vae_layers = (16, 32, 32, 64, 64, 64), (1, 1, 1, 1, 1, 1)
     backend = SanaBackend(device=str(device), cfg=cfg)
     backend.init_and_attach_lora()
@@ -302,6 +309,10 @@ def main():
     OpTimer.reset(True)
     theta, _ = engine.step(theta, seed=10_000, guidance_scale=guidance, timing=True)
     OpTimer.active = False
+    # final theta (after every epoch this run made): equal across ranks and to a single-process run of
+    # the same total population (tests/test_gpu_bench_dist.py compares them)
+    import hashlib
+    theta_sha16 = hashlib.sha256(theta.detach().cpu().numpy().tobytes()).hexdigest()[:16]
     phases = dict(engine.timings)
     model_kernels = OpTimer.summary(HBM_PEAK_GBPS)
     from hyperscalees_t2i_amd.measure import aux_kernel_rooflines
@@ -433,6 +444,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "theta_replicas_identical": replicas_identical,
+            "theta_final_sha16": theta_sha16,
             "phases_ms": phases,
             "aux_kernels": aux,
             "aux_kernels_pop64_per_gpu": aux64,

@@ -53,6 +53,11 @@ class ESBackend:
                             theta_pop: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
 
+    def members_per_pass(self) -> Optional[int]:
+        """Largest number of members one generate_population call evaluates (ESEngine splits a rank's
+        members into passes of this size, fixed boundaries from member 0); None = all in one pass."""
+        return None
+
 
 @dataclass
 class SanaConfig:
@@ -84,6 +89,11 @@ class SanaConfig:
     vae_widths: Tuple[int, ...] = (128, 256, 512, 512, 1024, 1024)
     vae_layers: Tuple[int, ...] = (3, 3, 3, 3, 3, 3)
     vae_chunk: int = 8
+    # members per population pass (ESEngine): 8 keeps every GEMM operand of the 1024-px forward under the
+    # 32-bit buffer range (the FFN's 16-image x 1024-token x 5632 hidden map is 184 MB per member: 11
+    # members reach 2 GiB) and fixes the batch a member is evaluated in, so theta' does not depend on how
+    # many ranks share the population (configs[2]: 8 ranks x 8 == one process x 64)
+    members_per_pass: int = 8
     synthetic_prompts: int = 4        # used when encoded_prompt_path is empty
     lora_b_std: float = 0.02          # nonzero B so the LoRA path is live
     lora_seed: int = 1234
@@ -215,6 +225,9 @@ class SanaBackend(ESBackend):
         pe, am = self._gather(uniq)
         return self.es_model.generate_population(pe, am, theta_pop, seed, guidance_scale, self.cfg.width_latent,
                                                  self.cfg.height_latent, prompt_index=idx)
+
+    def members_per_pass(self) -> Optional[int]:
+        return self.cfg.members_per_pass or None
 
 
 # ---------------------------------------------------------------------------------------

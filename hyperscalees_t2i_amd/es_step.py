@@ -172,16 +172,31 @@ class ESEngine:
         mark("perturb")
         if nl == 0:
             return torch.empty((0, m), device=self.device), torch.empty((0, 5), device=self.device), factors, info
-        imgs = self.backend.generate_population(flat_ids, seed, guidance_scale, tp)      # (2) inside
-        mark("generate")
-        feats = self.rewards.prompt_features(info["unique_texts"])
-        j_of_img = torch.tensor([info["pid_to_j"][p] for p in flat_ids], device=self.device).repeat(nl)
-        rew = self.rewards.score(imgs, j_of_img, feats, pil_mode=getattr(self.backend, "image_pil_mode", 0))
-        S_local, raw_local = aggregate_member_rewards(rew, flat_ids, info["pid_to_j"], nl, m)
+        # members in passes of the backend's pass size, boundaries fixed from this rank's first member
+        per = self.backend.members_per_pass() if hasattr(self.backend, "members_per_pass") else None
+        per = nl if not per else min(per, nl)
+        S_parts, raw_parts, logs = [], [], []
+        feats = None
+        for c0 in range(0, nl, per):
+            c1 = min(nl, c0 + per)
+            imgs = self.backend.generate_population(flat_ids, seed, guidance_scale, tp[c0:c1])      # (2) inside
+            mark("generate")
+            if feats is None:
+                feats = self.rewards.prompt_features(info["unique_texts"])
+            j_of_img = torch.tensor([info["pid_to_j"][p] for p in flat_ids], device=self.device).repeat(c1 - c0)
+            rew = self.rewards.score(imgs, j_of_img, feats, pil_mode=getattr(self.backend, "image_pil_mode", 0))
+            S_c, raw_c = aggregate_member_rewards(rew, flat_ids, info["pid_to_j"], c1 - c0, m)
+            S_parts.append(S_c)
+            raw_parts.append(raw_c)
+            if keep_images:
+                n_log = self.log_imgs(info)
+                logs.append(imgs.view(c1 - c0, len(flat_ids), *imgs.shape[1:])[:, :n_log])
+            del imgs
+            mark("reward")
+        S_local = S_parts[0] if len(S_parts) == 1 else torch.cat(S_parts)
+        raw_local = raw_parts[0] if len(raw_parts) == 1 else torch.cat(raw_parts)
         if keep_images:
-            n_log = self.log_imgs(info)
-            self.last_images = imgs.view(nl, len(flat_ids), *imgs.shape[1:])[:, :n_log]
-        mark("reward")
+            self.last_images = logs[0] if len(logs) == 1 else torch.cat(logs)
         return S_local, raw_local, factors, info
 
     @torch.no_grad()
@@ -219,7 +234,9 @@ class ESEngine:
             verify_theta_replicas(theta_new, self.dist)
         if timing:
             torch.cuda.synchronize()
-            self.timings = {ev[i][0]: ev[i - 1][1].elapsed_time(ev[i][1]) for i in range(1, len(ev))}
+            self.timings = {}
+            for i in range(1, len(ev)):   # a phase marked once per member pass sums over the passes
+                self.timings[ev[i][0]] = self.timings.get(ev[i][0], 0.0) + ev[i - 1][1].elapsed_time(ev[i][1])
         return theta_new, stats
 
     def _stats(self, S, raw, fit, info, seed) -> Dict[str, Any]:

@@ -44,6 +44,40 @@ def test_bench_two_ranks_same_device(tmp_path):
     assert "member-shard x2" in line["config"]["parallelism"]
 
 
+def _run_bench(tmp_path, tag, nproc, extra):
+    env = dict(os.environ, EGGROLL_DIST_BACKEND="gloo", EGGROLL_SAME_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               OMP_NUM_THREADS="2", EGGROLL_MIOPEN_FIND="0")
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+               "--gpus", str(nproc)]
+    else:
+        cmd = [sys.executable, str(ROOT / "bench.py")]
+    cmd += ["--steps", "1", "--warmup", "1", "--small", "--no-cpu-baseline"] + extra
+    out, err = tmp_path / f"{tag}.out", tmp_path / f"{tag}.err"
+    with open(out, "w") as fo, open(err, "w") as fe:
+        rc = subprocess.run(cmd, env=env, stdout=fo, stderr=fe, timeout=500, cwd=str(ROOT)).returncode
+    assert rc == 0, err.read_text()[-3000:]
+    lines = [ln for ln in out.read_text().splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, (out.read_text()[-2000:], err.read_text()[-2000:])
+    return json.loads(lines[0])
+
+
+def test_bench_eight_ranks_configs2_partition(tmp_path):
+    """BASELINE configs[2]'s partition — pop 64 as 8 ranks x 8 members — through bench.py itself
+    (tiny architecture, 8 gloo ranks sharing cuda:0): every rank's theta' identical
+    (verify_theta_replicas), and equal bit for bit to ONE process evaluating all 64 members."""
+    eight = _run_bench(tmp_path, "ws8", 8, ["--pop-per-gpu", "8"])
+    one = _run_bench(tmp_path, "ws1", 1, ["--pop-per-gpu", "64"])
+    assert eight["n_gpus"] == 8 and eight["config"]["pop_total"] == 64 and eight["config"]["pop_per_gpu"] == 8
+    assert "member-shard x8" in eight["config"]["parallelism"]
+    assert eight["theta_replicas_identical"] is True
+    assert one["n_gpus"] == 1 and one["config"]["pop_total"] == 64
+    assert eight["theta_final_sha16"] == one["theta_final_sha16"], (eight["theta_final_sha16"], one["theta_final_sha16"])
+    print(f"[ws8] theta' {eight['theta_final_sha16']} == single-process pop 64; "
+          f"{eight['value']:.2f} vs {one['value']:.2f} member-evals/s (tiny arch, shared device)")
+
+
 def test_rccl_collectives_single_rank(tmp_path):
     """RCCL itself on the box: a fresh child process inits the "nccl" backend as bench.py does and runs
     the all-gather / all-reduce / barrier call sites of the N>1 path on CUDA tensors (world size 1)."""
