@@ -27,11 +27,13 @@ SIGNATURES = {
     "eggroll_noise_factors": (C.c_int, [u64, i64, i64, i64, i64, vp, vp]),
     "eggroll_philox_words": (C.c_int, [u64, i64, i64, vp, vp]),
     "eggroll_perturb": (C.c_int, [vp, vp, i64, i64, vp, vp, i64, i64, i32, i32, i32, i64, i64, f32, vp, i64, vp]),
+    "eggroll_perturb_seeded": (C.c_int, [u64, vp, vp, vp, i64, i64, i32, i32, i32, i64, i64, f32, vp, i64, vp]),
     "eggroll_tile_table": (i64, [vp, i32, i32, vp, i64]),
     "eggroll_fitness": (C.c_int, [vp, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp, vp]),
     "eggroll_update_workspace_bytes": (i64, [i64]),
     "eggroll_update": (C.c_int, [vp, vp, i64, i64, vp, vp, i32, i32, vp, vp, i64, i64, i32, f32, f32, f32, vp, vp,
                                  vp]),
+    "eggroll_update_seeded": (C.c_int, [u64, vp, vp, vp, i32, i32, vp, vp, i64, i64, i32, f32, f32, f32, vp, vp, vp]),
     "eggroll_lora_linear_pop": (C.c_int, [vp, i64, vp, i64, vp, vp, i64, i64, i64, i32, f32, i64, i64, i64, i64, vp,
                                           i64, vp, vp]),
     "eggroll_lora_gemm": (C.c_int, [vp, i64, vp, i64, vp, vp, vp, i64, i64, i32, f32, i64, i64, i64, i64, vp, i64, vp]),

@@ -122,6 +122,47 @@ __host__ __device__ __forceinline__ void member_to_base(int64_t k, int32_t pop, 
 }
 
 // ------------------------------------------------------------------------------------
+// Factor source.  Stored (GEN = false): base sample j's factor row j * ld of the buffer k_noise wrote.
+// Regenerated (GEN = true, the seeded entry points): element g of base sample j is recomputed where it
+// is consumed — Philox4x32-10 of counter (g / 4, j, kNoiseTag) under key (k0, k1), then the same
+// Box-Muller as k_noise — so the values are bit-identical to the stored path while no factor byte is
+// written to or read from HBM (north_star kernel (1): "noise is regenerated rather than stored").
+// The fast tiles consume factors in 4-aligned quads (segments are padded to 4 floats), so one Philox
+// call yields exactly the 4 values a 16-byte load would have.
+// ------------------------------------------------------------------------------------
+struct FacSrc {
+    const float* f;  // stored rows (GEN = false)
+    int64_t ld;
+    uint32_t k0, k1; // Philox key = the epoch seed (GEN = true)
+};
+
+template <bool GEN>
+__device__ __forceinline__ float4 fac4(const FacSrc& s, int64_t j, int64_t off) {  // off % 4 == 0
+    if constexpr (GEN) {
+        const int64_t q = off >> 2;
+        const u32x4 c{(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)j, kNoiseTag};
+        const u32x4 w = philox4x32_10_dev(c, s.k0, s.k1);
+        float4 v;
+        box_muller(w.x, w.y, v.x, v.y);
+        box_muller(w.z, w.w, v.z, v.w);
+        return v;
+    } else {
+        return *reinterpret_cast<const float4*>(s.f + j * s.ld + off);
+    }
+}
+
+template <bool GEN>
+__device__ __forceinline__ float fac1(const FacSrc& s, int64_t j, int64_t g) {
+    if constexpr (GEN) {
+        const float4 v = fac4<true>(s, j, g & ~(int64_t)3);
+        const int c = (int)(g & 3);
+        return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+    } else {
+        return s.f[j * s.ld + g];
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Work decomposition shared by perturb and update: a host-built tile table (eggroll_tile_table)
 // gives every workgroup its (matrix, tile) with ONE scalar load — no search over the matrix list.
 // Fast tiles (T_VEC4 / T_WIDE / T_TALL, egg rank 1, 2 or 4) cover 1024 positions of the matrix's
@@ -165,17 +206,17 @@ __device__ __forceinline__ Slots make_slots(const eggroll_mat_t& mt, int64_t cid
 }
 
 // eps of (row, col) of matrix mt for the base-sample factor row fj (utills.py:59-65 restated)
-template <bool VEC1D>
-__device__ __forceinline__ float eps_rc(const eggroll_mat_t& mt, const float* __restrict__ fj, int row, int col,
+template <bool VEC1D, bool GEN>
+__device__ __forceinline__ float eps_rc(const eggroll_mat_t& mt, const FacSrc& src, int64_t j, int row, int col,
                                         int r, float sqrt_r) {
 #pragma clang fp contract(off)
     if constexpr (VEC1D) {
-        return fj[mt.factor_off + row];
+        return fac1<GEN>(src, j, mt.factor_off + row);
     } else {
-        const float* a = fj + mt.factor_off + (int64_t)row * r;
-        const float* b = fj + egg_b_off(mt, r) + (int64_t)col * r;
-        float acc = a[0] * b[0];
-        for (int q = 1; q < r; ++q) acc = acc + a[q] * b[q];
+        const int64_t a = mt.factor_off + (int64_t)row * r;
+        const int64_t b = egg_b_off(mt, r) + (int64_t)col * r;
+        float acc = fac1<GEN>(src, j, a) * fac1<GEN>(src, j, b);
+        for (int q = 1; q < r; ++q) acc = acc + fac1<GEN>(src, j, a + q) * fac1<GEN>(src, j, b + q);
         return r == 1 ? acc : acc / sqrt_r;
     }
 }
@@ -287,13 +328,31 @@ struct PGrp {
     static constexpr int value = (KIND == T_VEC4 || R == 1) ? (UPD ? EGG_UPD_PGRP1 : 8) : (UPD ? EGG_UPD_PGRR : EGG_PTB_PGRR) / R;
 };
 
+// Uniform (short-dimension) factors of one base sample: NW floats from the 4-aligned segment start uo
+// (NW <= the segment's padded length); 1.0 where !use (1-D params, members / base samples past the end).
+template <int KIND, int NW, bool GEN>
+__device__ __forceinline__ void load_uniform(float (&W)[NW], const FacSrc& src, int64_t j, int64_t uo, bool use) {
+    if constexpr (GEN) {
+#pragma unroll
+        for (int w0 = 0; w0 < NW; w0 += 4) {
+            const float4 v = use ? fac4<true>(src, j, uo + w0) : float4{1.0f, 1.0f, 1.0f, 1.0f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (w0 + c < NW) W[w0 + c] = f4(v, c);
+        }
+    } else {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) W[w] = use ? src.f[j * src.ld + uo + w] : 1.0f;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // perturb / materialise: out[k] = theta + sigma * s_k * E_j(k) for the members [lo, lo + n).
 // One workgroup per tile; theta is read once and every member's row is written from registers.
 // ------------------------------------------------------------------------------------
-template <int KIND, int R, int NU, bool V4>
-__device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, const float* __restrict__ factors,
-                                             int64_t ld_f, const eggroll_mat_t& mt, int64_t tidx, float sqrt_r,
+template <int KIND, int R, int NU, bool V4, bool GEN>
+__device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, const FacSrc& src,
+                                             const eggroll_mat_t& mt, int64_t tidx, float sqrt_r,
                                              int32_t pop, int32_t antithetic, int64_t member_lo, int n_members,
                                              float sigma, float* __restrict__ out, int64_t ld_out) {
 #pragma clang fp contract(off)
@@ -319,8 +378,7 @@ __device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, co
             member_to_base(member_lo + g + lane, pop, antithetic, jb, sl);
             const bool mok = g + lane < n_members;
             jl = mok ? (int)jb : 0;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) W[w] = (KIND == T_VEC4 || !mok) ? 1.0f : factors[jb * ld_f + uo + w];
+            load_uniform<KIND, NW, GEN>(W, src, jb, uo, KIND != T_VEC4 && mok);
         }
         const int n = (n_members - g) < 64 ? (n_members - g) : 64;
         constexpr int PG = PGrp<KIND, R>::value;
@@ -331,8 +389,7 @@ __device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, co
                 const int64_t j = __builtin_amdgcn_readlane(jl, (i0 + t) & 63);
                 const bool lok = ok && (i0 + t < n);
 #pragma unroll
-                for (int c = 0; c < NX; ++c)
-                    X[t][c] = lok ? ld4<true>(factors + j * ld_f + xo + 4 * c) : float4{0, 0, 0, 0};
+                for (int c = 0; c < NX; ++c) X[t][c] = lok ? fac4<GEN>(src, j, xo + 4 * c) : float4{0, 0, 0, 0};
             }
 #pragma unroll
             for (int t = 0; t < PG; ++t) {
@@ -366,9 +423,9 @@ __device__ __forceinline__ void perturb_fast(const float* __restrict__ theta, co
     }
 }
 
-template <bool VEC1D>
-__device__ __forceinline__ void perturb_chunk(const float* __restrict__ theta, const float* __restrict__ factors,
-                                              int64_t ld_f, const eggroll_mat_t& mt, int64_t cidx, int r,
+template <bool VEC1D, bool GEN>
+__device__ __forceinline__ void perturb_chunk(const float* __restrict__ theta, const FacSrc& src,
+                                              const eggroll_mat_t& mt, int64_t cidx, int r,
                                               float sqrt_r, int32_t pop, int32_t antithetic, int64_t member_lo,
                                               int n_members, float sigma, float* __restrict__ out, int64_t ld_out) {
 #pragma clang fp contract(off)
@@ -384,12 +441,11 @@ __device__ __forceinline__ void perturb_chunk(const float* __restrict__ theta, c
         int64_t j;
         float sgn;
         member_to_base(member_lo + i, pop, antithetic, j, sgn);
-        const float* fj = factors + j * ld_f;
         float* dst = out + (int64_t)i * ld_out + mt.theta_off;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (!sl.ok[s]) continue;
-            const float eps = sgn * eps_rc<VEC1D>(mt, fj, sl.row[s], sl.col[s], r, sqrt_r);
+            const float eps = sgn * eps_rc<VEC1D, GEN>(mt, src, j, sl.row[s], sl.col[s], r, sqrt_r);
             float v;
             if (theta) {
                 const float t = sigma * eps;
@@ -418,9 +474,9 @@ __device__ __forceinline__ void dispatch_tile(const eggroll_mat_t& mt, int r, Fa
     else gen(std::false_type{});
 }
 
-template <int R, bool V4>
-__global__ __launch_bounds__(256) void k_perturb(const float* __restrict__ theta, const float* __restrict__ factors,
-                                                 int64_t ld_f, const eggroll_mat_t* __restrict__ mats,
+template <int R, bool V4, bool GEN>
+__global__ __launch_bounds__(256) void k_perturb(const float* __restrict__ theta, FacSrc src,
+                                                 const eggroll_mat_t* __restrict__ mats,
                                                  const eggroll_tile_t* __restrict__ tiles, int r, float sqrt_r,
                                                  int32_t pop, int32_t antithetic, int64_t member_lo, int n_members,
                                                  float sigma, float* __restrict__ out, int64_t ld_out) {
@@ -431,15 +487,15 @@ __global__ __launch_bounds__(256) void k_perturb(const float* __restrict__ theta
         [&](auto KD, auto NUv) {
             constexpr int KK = decltype(KD)::value;
             if constexpr (KK == T_VEC4)
-                perturb_fast<T_VEC4, 1, 1, V4>(theta, factors, ld_f, mt, tl.index, sqrt_r, pop, antithetic, member_lo,
-                                               n_members, sigma, out, ld_out);
+                perturb_fast<T_VEC4, 1, 1, V4, GEN>(theta, src, mt, tl.index, sqrt_r, pop, antithetic, member_lo,
+                                                    n_members, sigma, out, ld_out);
             else if constexpr (R > 0)
-                perturb_fast<KK, R, decltype(NUv)::value, V4>(theta, factors, ld_f, mt, tl.index, sqrt_r, pop,
-                                                              antithetic, member_lo, n_members, sigma, out, ld_out);
+                perturb_fast<KK, R, decltype(NUv)::value, V4, GEN>(theta, src, mt, tl.index, sqrt_r, pop,
+                                                                   antithetic, member_lo, n_members, sigma, out, ld_out);
         },
         [&](auto VD) {
-            perturb_chunk<decltype(VD)::value>(theta, factors, ld_f, mt, tl.index, r, sqrt_r, pop, antithetic,
-                                               member_lo, n_members, sigma, out, ld_out);
+            perturb_chunk<decltype(VD)::value, GEN>(theta, src, mt, tl.index, r, sqrt_r, pop, antithetic,
+                                                    member_lo, n_members, sigma, out, ld_out);
         });
 }
 
@@ -578,9 +634,9 @@ __device__ __forceinline__ void norm_acc(double (&part)[4], float v, float th) {
     part[3] += (double)th * (double)th;
 }
 
-template <int KIND, int R, int NU, bool V4, bool NORMS>
-__device__ __forceinline__ void update_fast(const float* __restrict__ theta, const float* __restrict__ factors,
-                                            int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
+template <int KIND, int R, int NU, bool V4, bool NORMS, bool GEN>
+__device__ __forceinline__ void update_fast(const float* __restrict__ theta, const FacSrc& src,
+                                            int64_t n_base, const float* __restrict__ s_c, int nf,
                                             const eggroll_mat_t& mt, int64_t tidx, float sqrt_r, float lr,
                                             float* __restrict__ out, double (&part)[4]) {
 #pragma clang fp contract(off)
@@ -610,11 +666,9 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
                 const int64_t jl = g + lane;
                 const bool jok = jl < n_base;
                 C = jok ? s_c[jl] : 0.0f;
+                load_uniform<KIND, NW, GEN>(W, src, jl, uo, KIND != T_VEC4 && jok);
 #pragma unroll
-                for (int w = 0; w < NW; ++w) {
-                    const float f = (KIND == T_VEC4 || !jok) ? 1.0f : factors[jl * ld_f + uo + w];
-                    W[w] = (R == 1 && KIND != T_VEC4) ? C * f : f;
-                }
+                for (int w = 0; w < NW; ++w) W[w] = (R == 1 && KIND != T_VEC4) ? C * W[w] : W[w];
             }
             const int n = (int)((n_base - g) < 64 ? (n_base - g) : 64);
             constexpr int PG = PGrp<KIND, R, true>::value;
@@ -622,15 +676,14 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
             // group's eps math runs (rank 4 at configs[3]: 559 -> 432 us with one base sample per group,
             // 3 % faster than two; a pure read of the same stream runs 367 us); rank 1 keeps one group in
             // registers (the second set costs an occupancy step there: 24.7 -> 27.0 us at pop 64)
-            constexpr bool PF = EGG_UPD_PREFETCH && R >= 2 && KIND != T_VEC4;
+            constexpr bool PF = EGG_UPD_PREFETCH && R >= 2 && KIND != T_VEC4 && !GEN;  // nothing to prefetch when regenerated
             float4 XN[PF ? PG : 1][NX];
             auto load_grp = [&](float4 (&D)[PF ? PG : 1][NX], int j0) {
 #pragma unroll
                 for (int t = 0; t < (PF ? PG : 1); ++t)
 #pragma unroll
                     for (int c = 0; c < NX; ++c)
-                        D[t][c] = (ok && j0 + t < n) ? ld4<true>(factors + (g + j0 + t) * ld_f + xo + 4 * c)
-                                                     : float4{0, 0, 0, 0};
+                        D[t][c] = (ok && j0 + t < n) ? fac4<GEN>(src, g + j0 + t, xo + 4 * c) : float4{0, 0, 0, 0};
             };
             if constexpr (PF) load_grp(XN, 0);
             for (int j0 = 0; j0 < n; j0 += PG) {
@@ -646,8 +699,7 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
                     for (int t = 0; t < PG; ++t)
 #pragma unroll
                         for (int c = 0; c < NX; ++c)
-                            X[t][c] = (ok && j0 + t < n) ? ld4<true>(factors + (g + j0 + t) * ld_f + xo + 4 * c)
-                                                         : float4{0, 0, 0, 0};
+                            X[t][c] = (ok && j0 + t < n) ? fac4<GEN>(src, g + j0 + t, xo + 4 * c) : float4{0, 0, 0, 0};
                 }
 #pragma unroll
                 for (int t = 0; t < PG; ++t) {
@@ -693,9 +745,9 @@ __device__ __forceinline__ void update_fast(const float* __restrict__ theta, con
     }
 }
 
-template <bool VEC1D, bool NORMS>
-__device__ __forceinline__ void update_chunk(const float* __restrict__ theta, const float* __restrict__ factors,
-                                             int64_t ld_f, int64_t n_base, const float* __restrict__ s_c, int nf,
+template <bool VEC1D, bool NORMS, bool GEN>
+__device__ __forceinline__ void update_chunk(const float* __restrict__ theta, const FacSrc& src,
+                                             int64_t n_base, const float* __restrict__ s_c, int nf,
                                              const eggroll_mat_t& mt, int64_t cidx, int r, float sqrt_r, float lr,
                                              float* __restrict__ out, double (&part)[4]) {
 #pragma clang fp contract(off)
@@ -705,11 +757,11 @@ __device__ __forceinline__ void update_chunk(const float* __restrict__ theta, co
         // sum_j c_j eps_j in base order j = 0, 1, ...
 #pragma unroll 2
         for (int64_t j = 0; j < n_base; ++j) {
-            const float* fj = factors + j * ld_f;
             const float cj = s_c[j];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const float ev = eps_rc<VEC1D>(mt, fj, sl.ok[s] ? sl.row[s] : 0, sl.ok[s] ? sl.col[s] : 0, r, sqrt_r);
+                const float ev = eps_rc<VEC1D, GEN>(mt, src, j, sl.ok[s] ? sl.row[s] : 0, sl.ok[s] ? sl.col[s] : 0, r,
+                                                    sqrt_r);
                 acc[s] = acc[s] + cj * ev;
             }
         }
@@ -730,9 +782,9 @@ __device__ __forceinline__ void update_chunk(const float* __restrict__ theta, co
     }
 }
 
-template <int R, bool V4, bool NORMS>
-__global__ __launch_bounds__(256) void k_update(const float* __restrict__ theta, const float* __restrict__ factors,
-                                                int64_t ld_f, int64_t n_base, const float* __restrict__ fit,
+template <int R, bool V4, bool NORMS, bool GEN>
+__global__ __launch_bounds__(256) void k_update(const float* __restrict__ theta, FacSrc src,
+                                                int64_t n_base, const float* __restrict__ fit,
                                                 const float* __restrict__ stats, int32_t pop, int32_t antithetic,
                                                 const eggroll_mat_t* __restrict__ mats,
                                                 const eggroll_tile_t* __restrict__ tiles, int r, float sqrt_r,
@@ -765,15 +817,15 @@ __global__ __launch_bounds__(256) void k_update(const float* __restrict__ theta,
         [&](auto KD, auto NUv) {
             constexpr int KK = decltype(KD)::value;
             if constexpr (KK == T_VEC4)
-                update_fast<T_VEC4, 1, 1, V4, NORMS>(theta, factors, ld_f, n_base, s_c, nf, mt, tl.index, sqrt_r, lr,
-                                                     out, part);
+                update_fast<T_VEC4, 1, 1, V4, NORMS, GEN>(theta, src, n_base, s_c, nf, mt, tl.index, sqrt_r, lr,
+                                                          out, part);
             else if constexpr (R > 0)
-                update_fast<KK, R, decltype(NUv)::value, V4, NORMS>(theta, factors, ld_f, n_base, s_c, nf, mt,
-                                                                    tl.index, sqrt_r, lr, out, part);
+                update_fast<KK, R, decltype(NUv)::value, V4, NORMS, GEN>(theta, src, n_base, s_c, nf, mt,
+                                                                         tl.index, sqrt_r, lr, out, part);
         },
         [&](auto VD) {
-            update_chunk<decltype(VD)::value, NORMS>(theta, factors, ld_f, n_base, s_c, nf, mt, tl.index, r, sqrt_r,
-                                                     lr, out, part);
+            update_chunk<decltype(VD)::value, NORMS, GEN>(theta, src, n_base, s_c, nf, mt, tl.index, r, sqrt_r,
+                                                          lr, out, part);
         });
     if constexpr (NORMS) {
 #pragma unroll
@@ -904,6 +956,26 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 static int launch_rank(int32_t rank) { return (rank == 1 || rank == 2 || rank == 4) ? rank : 0; }
 
+static int perturb_launch(const float* theta, FacSrc src, bool gen, const eggroll_mat_t* mats,
+                          const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank, int32_t pop,
+                          int32_t antithetic, int64_t member_lo, int64_t member_hi, float sigma, float* out,
+                          int64_t ld_out, void* stream) {
+    EGG_CHECK_ARG(member_hi - member_lo <= 65535, "perturb: at most 65535 members per call");
+    EGG_CHECK_ARG(n_tiles >= 1 && n_tiles < (1ll << 31), "perturb: bad n_tiles");
+    if (member_hi == member_lo || D == 0) return EGGROLL_OK;
+    const float sqrt_r = (float)sqrt((double)rank);
+    const bool v4 = (theta == nullptr || al16(theta)) && al16(out) && ld_out % 4 == 0;
+#define EGG_PTB_K(RV) (gen ? (v4 ? k_perturb<RV, true, true> : k_perturb<RV, false, true>) \
+                           : (v4 ? k_perturb<RV, true, false> : k_perturb<RV, false, false>))
+    auto* k = launch_rank(rank) == 1 ? EGG_PTB_K(1) : launch_rank(rank) == 2 ? EGG_PTB_K(2)
+            : launch_rank(rank) == 4 ? EGG_PTB_K(4) : EGG_PTB_K(0);
+#undef EGG_PTB_K
+    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles), dim3(256), 0, as_stream(stream), theta, src, mats, tiles,
+                       rank, sqrt_r, pop, antithetic, member_lo, (int)(member_hi - member_lo), sigma, out, ld_out);
+    EGG_CHECK_LAUNCH("perturb");
+    return EGGROLL_OK;
+}
+
 int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int64_t n_base,
                     const eggroll_mat_t* mats, const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank,
                     int32_t pop, int32_t antithetic, int64_t member_lo, int64_t member_hi, float sigma, float* out,
@@ -915,19 +987,20 @@ int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int6
     EGG_CHECK_ARG(al16(factors) && ld_f % 4 == 0, "perturb: factors must be 16-byte aligned with ld_f %% 4 == 0");
     const int64_t need_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
     EGG_CHECK_ARG(n_base >= need_base, "perturb: n_base %lld < %lld needed", (long long)n_base, (long long)need_base);
-    EGG_CHECK_ARG(member_hi - member_lo <= 65535, "perturb: at most 65535 members per call");
-    EGG_CHECK_ARG(n_tiles >= 1 && n_tiles < (1ll << 31), "perturb: bad n_tiles");
-    if (member_hi == member_lo || D == 0) return EGGROLL_OK;
-    const float sqrt_r = (float)sqrt((double)rank);
-    const bool v4 = (theta == nullptr || al16(theta)) && al16(out) && ld_out % 4 == 0;
-    auto* k = launch_rank(rank) == 1 ? (v4 ? k_perturb<1, true> : k_perturb<1, false>)
-            : launch_rank(rank) == 2 ? (v4 ? k_perturb<2, true> : k_perturb<2, false>)
-            : launch_rank(rank) == 4 ? (v4 ? k_perturb<4, true> : k_perturb<4, false>)
-                                     : (v4 ? k_perturb<0, true> : k_perturb<0, false>);
-    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles), dim3(256), 0, as_stream(stream), theta, factors, ld_f, mats, tiles,
-                       rank, sqrt_r, pop, antithetic, member_lo, (int)(member_hi - member_lo), sigma, out, ld_out);
-    EGG_CHECK_LAUNCH("perturb");
-    return EGGROLL_OK;
+    return perturb_launch(theta, FacSrc{factors, ld_f, 0u, 0u}, false, mats, tiles, n_tiles, D, rank, pop, antithetic,
+                          member_lo, member_hi, sigma, out, ld_out, stream);
+}
+
+int eggroll_perturb_seeded(uint64_t seed, const float* theta, const eggroll_mat_t* mats, const eggroll_tile_t* tiles,
+                           int64_t n_tiles, int64_t D, int32_t rank, int32_t pop, int32_t antithetic,
+                           int64_t member_lo, int64_t member_hi, float sigma, float* out, int64_t ld_out,
+                           void* stream) {
+    EGG_CHECK_ARG(rank >= 1, "perturb_seeded: rank must be >= 1");
+    EGG_CHECK_ARG(pop >= 1 && member_lo >= 0 && member_hi <= pop && member_lo <= member_hi,
+                  "perturb_seeded: members [%lld,%lld) outside pop %d", (long long)member_lo, (long long)member_hi, pop);
+    EGG_CHECK_ARG(mats && tiles && out && ld_out >= D, "perturb_seeded: bad pointers/sizes");
+    return perturb_launch(theta, FacSrc{nullptr, 0, (uint32_t)seed, (uint32_t)(seed >> 32)}, true, mats, tiles,
+                          n_tiles, D, rank, pop, antithetic, member_lo, member_hi, sigma, out, ld_out, stream);
 }
 
 int eggroll_fitness(const float* S, int32_t n, int32_t m, int32_t use_promptnorm, float promptnorm_eps, float* scores,
@@ -946,16 +1019,10 @@ int64_t eggroll_update_workspace_bytes(int64_t n_tiles) {
     return n_tiles * 4 * (int64_t)sizeof(double) + 64;
 }
 
-int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64_t n_base, const float* fitness,
-                   const float* stats, int32_t pop, int32_t antithetic, const eggroll_mat_t* mats,
-                   const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank, float lr,
-                   float max_step_norm, float theta_max_norm, void* workspace, float* theta_out, void* stream) {
-    EGG_CHECK_ARG(rank >= 1 && pop >= 1, "update: bad rank/pop");
-    EGG_CHECK_ARG(theta && factors && fitness && stats && mats && tiles && workspace && theta_out, "update: NULL pointer");
-    EGG_CHECK_ARG(theta != theta_out, "update: theta_out may not alias theta");
-    EGG_CHECK_ARG(al16(factors) && ld_f % 4 == 0, "update: factors must be 16-byte aligned with ld_f %% 4 == 0");
-    const int64_t need_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
-    EGG_CHECK_ARG(n_base == need_base, "update: n_base %lld != %lld", (long long)n_base, (long long)need_base);
+static int update_launch(const float* theta, FacSrc src, bool gen, int64_t n_base, const float* fitness,
+                         const float* stats, int32_t pop, int32_t antithetic, const eggroll_mat_t* mats,
+                         const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank, float lr,
+                         float max_step_norm, float theta_max_norm, void* workspace, float* theta_out, void* stream) {
     EGG_CHECK_ARG(n_base <= 16384, "update: n_base > 16384 unsupported");
     EGG_CHECK_ARG(n_tiles >= 1 && n_tiles < (1ll << 31), "update: bad n_tiles");
     EGG_CHECK_ARG(al16(workspace), "update: workspace must be 16-byte aligned");
@@ -967,13 +1034,13 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
     const bool v4 = al16(theta) && al16(theta_out);
     const bool caps = max_step_norm > 0.0f || theta_max_norm > 0.0f;
     const int lr_ = launch_rank(rank);
-#define EGG_UPD_K(RV, V4V, NV) k_update<RV, V4V, NV>
+#define EGG_UPD_K(RV, V4V, NV) (gen ? k_update<RV, V4V, NV, true> : k_update<RV, V4V, NV, false>)
 #define EGG_UPD_PICK(RV) (v4 ? (caps ? EGG_UPD_K(RV, true, true) : EGG_UPD_K(RV, true, false)) \
                              : (caps ? EGG_UPD_K(RV, false, true) : EGG_UPD_K(RV, false, false)))
     auto* k = lr_ == 1 ? EGG_UPD_PICK(1) : lr_ == 2 ? EGG_UPD_PICK(2) : lr_ == 4 ? EGG_UPD_PICK(4) : EGG_UPD_PICK(0);
 #undef EGG_UPD_PICK
 #undef EGG_UPD_K
-    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles), dim3(256), (size_t)n_base * sizeof(float), st, theta, factors, ld_f,
+    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles), dim3(256), (size_t)n_base * sizeof(float), st, theta, src,
                        n_base, fitness, stats, pop, antithetic, mats, tiles, rank, sqrt_r, lr, theta_out, partials);
     EGG_CHECK_LAUNCH("update");
     if (caps) {
@@ -986,6 +1053,33 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
         EGG_CHECK_LAUNCH("update_caps");
     }
     return EGGROLL_OK;
+}
+
+int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64_t n_base, const float* fitness,
+                   const float* stats, int32_t pop, int32_t antithetic, const eggroll_mat_t* mats,
+                   const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank, float lr,
+                   float max_step_norm, float theta_max_norm, void* workspace, float* theta_out, void* stream) {
+    EGG_CHECK_ARG(rank >= 1 && pop >= 1, "update: bad rank/pop");
+    EGG_CHECK_ARG(theta && factors && fitness && stats && mats && tiles && workspace && theta_out, "update: NULL pointer");
+    EGG_CHECK_ARG(theta != theta_out, "update: theta_out may not alias theta");
+    EGG_CHECK_ARG(al16(factors) && ld_f % 4 == 0, "update: factors must be 16-byte aligned with ld_f %% 4 == 0");
+    const int64_t need_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
+    EGG_CHECK_ARG(n_base == need_base, "update: n_base %lld != %lld", (long long)n_base, (long long)need_base);
+    return update_launch(theta, FacSrc{factors, ld_f, 0u, 0u}, false, n_base, fitness, stats, pop, antithetic, mats,
+                         tiles, n_tiles, D, rank, lr, max_step_norm, theta_max_norm, workspace, theta_out, stream);
+}
+
+int eggroll_update_seeded(uint64_t seed, const float* theta, const float* fitness, const float* stats, int32_t pop,
+                          int32_t antithetic, const eggroll_mat_t* mats, const eggroll_tile_t* tiles, int64_t n_tiles,
+                          int64_t D, int32_t rank, float lr, float max_step_norm, float theta_max_norm,
+                          void* workspace, float* theta_out, void* stream) {
+    EGG_CHECK_ARG(rank >= 1 && pop >= 1, "update_seeded: bad rank/pop");
+    EGG_CHECK_ARG(theta && fitness && stats && mats && tiles && workspace && theta_out, "update_seeded: NULL pointer");
+    EGG_CHECK_ARG(theta != theta_out, "update_seeded: theta_out may not alias theta");
+    const int64_t n_base = antithetic ? (pop / 2 + (pop % 2)) : pop;
+    return update_launch(theta, FacSrc{nullptr, 0, (uint32_t)seed, (uint32_t)(seed >> 32)}, true, n_base, fitness,
+                         stats, pop, antithetic, mats, tiles, n_tiles, D, rank, lr, max_step_norm, theta_max_norm,
+                         workspace, theta_out, stream);
 }
 
 int64_t eggroll_tile_table(const eggroll_mat_t* mats_host, int32_t n_mats, int32_t rank, eggroll_tile_t* tiles_host,

@@ -6,8 +6,12 @@ ES hot path.  Differences are deliberate and documented per function:
   * noise is counter-based (Philox keyed by an explicit seed) instead of torch's global RNG —
     bit-exact reproduction of torch.randn streams is impossible across RNGs (SURVEY §7);
     feeding reference factors through `eps_from_factors` reproduces the reference eps exactly;
-  * the engine path never materialises eps [pop, D]: it keeps factors and calls the fused
-    perturb / update kernels (`EggRollNoiser.perturb`, `EggRollNoiser.update_from_factors`).
+  * the engine path never materialises eps [pop, D] and, by default, never stores the factors
+    either: `EggRollNoiser.epoch_noise` returns a `SeededFactors` handle (the epoch seed), and the
+    perturb / update kernels regenerate every factor value where they consume it
+    (`EggRollNoiser.perturb`, `EggRollNoiser.update_from_factors`); a factor TENSOR (`sample_factors`,
+    or reference factors injected for parity tests) runs the same kernels on the stored values —
+    both give the same bits.
 """
 from __future__ import annotations
 
@@ -19,6 +23,22 @@ from torch import nn
 
 from . import kernels as K
 from .kernels import ThetaLayout, n_base_samples
+
+
+class SeededFactors:
+    """The factors of one epoch, held as the Philox key that generates them (no buffer): base sample j's
+    factor element g is Philox4x32-10(counter (g / 4, j, tag), key seed) -> Box-Muller, as the noise
+    kernel writes it (include/eggroll.h)."""
+
+    def __init__(self, seed: int, n_base: int):
+        self.seed, self.n_base = int(seed), int(n_base)
+
+    def materialise(self, layout: ThetaLayout, device) -> torch.Tensor:
+        """The stored form [n_base, factor_ld] (eggroll_noise_factors) — for tests and eps materialisation."""
+        return K.noise_factors(self.seed, self.n_base, layout, device)
+
+
+Factors = Union[torch.Tensor, SeededFactors]
 
 
 class EggRollNoiser:
@@ -46,17 +66,31 @@ class EggRollNoiser:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         return K.noise_factors(seed, self.n_base(pop_size), self.layout, device)
 
-    def perturb(self, theta: torch.Tensor, factors: torch.Tensor, pop_size: int, member_lo: int, member_hi: int,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def epoch_noise(self, pop_size: int, seed: Optional[int] = None) -> SeededFactors:
+        """The epoch's factors as a seed handle (the engine path: regenerated inside perturb / update).
+        seed=None draws one from torch's global generator, as sample_factors does."""
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        return SeededFactors(seed, self.n_base(pop_size))
+
+    def perturb(self, theta: Optional[torch.Tensor], factors: Factors, pop_size: int, member_lo: int, member_hi: int,
+                out: Optional[torch.Tensor] = None, device=None) -> torch.Tensor:
         """theta_k = theta + sigma * eps_k for members [lo, hi)  (unifed_es.py:160)."""
+        if isinstance(factors, SeededFactors):
+            dev = theta.device if theta is not None else (out.device if out is not None else device)
+            return K.perturb_seeded(theta, factors.seed, self.layout, pop_size, self.use_antithetic, member_lo,
+                                    member_hi, self.sigma, dev, out=out)
         return K.perturb(theta, factors, self.layout, pop_size, self.use_antithetic, member_lo, member_hi,
                          self.sigma, out=out)
 
-    def eps_from_factors(self, factors: torch.Tensor, pop_size: int) -> torch.Tensor:
+    def eps_from_factors(self, factors: Factors, pop_size: int, device=None) -> torch.Tensor:
         """Materialised eps [pop, D] in the reference layout (utills.py:70-106)."""
+        if isinstance(factors, SeededFactors):
+            return K.perturb_seeded(None, factors.seed, self.layout, pop_size, self.use_antithetic, 0, pop_size, 1.0,
+                                    device)
         return K.perturb(None, factors, self.layout, pop_size, self.use_antithetic, 0, pop_size, 1.0)
 
-    def update_from_factors(self, theta: torch.Tensor, factors: torch.Tensor, fit: dict, pop_size: int,
+    def update_from_factors(self, theta: torch.Tensor, factors: Factors, fit: dict, pop_size: int,
                             max_step_norm: float = 0.0, theta_max_norm: float = 0.0,
                             out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """do_update + cap_step_norm + cap_theta_norm fused (utills.py:115-136, 333-349)."""
@@ -64,6 +98,9 @@ class EggRollNoiser:
         if ws is None:
             ws = self._ws[theta.device] = K.UpdateWorkspace(self.layout, theta.device)
         lr = float(self.lr_scale * self.sigma)
+        if isinstance(factors, SeededFactors):
+            return K.update_seeded(theta, factors.seed, fit, self.layout, pop_size, self.use_antithetic, lr,
+                                   max_step_norm, theta_max_norm, out=out, workspace=ws)
         return K.update(theta, factors, fit, self.layout, pop_size, self.use_antithetic, lr, max_step_norm,
                         theta_max_norm, out=out, workspace=ws)
 

@@ -3,7 +3,8 @@ member-sharded over ranks.
 
 Per epoch, on every rank (seed = epoch, unifed_es.py:766):
   1. sampling info (bit-exact prompt ids, es_backend.py:234-263)
-  2. noise factors for ALL base samples (Philox, regenerated — never communicated)   kernel (1)
+  2. noise factors for ALL base samples (Philox, regenerated inside perturb / update — never stored or
+     communicated)                                                                     kernel (1)
   3. theta_k = theta + sigma*eps_k for the rank's members [lo, hi)                    perturb
   4. one batched Sana one-step forward + VAE decode for all local members             kernel (2) inside
   5. batched rewards -> S_local [n_local, m] (mean over repeats, unifed_es.py:208-215)
@@ -139,6 +140,7 @@ class ESConfig:
     max_step_norm: float = 0.0
     max_log_batches: int = 1
     verify_replicas: bool = False   # debug: theta checksum all-reduce after every update (N > 1)
+    regenerate_noise: bool = True   # factors regenerated in perturb / update from the epoch seed (False: stored)
 
 
 class ESEngine:
@@ -166,7 +168,10 @@ class ESEngine:
         info = self.backend.step_sampling_info(seed=seed)
         m, flat_ids = info["m"], info["flat_ids"]
         R = len(flat_ids) // max(1, m)
-        factors = nz.sample_factors(pop, self.device, seed=seed)                       # (1)
+        # (1): the epoch's factors as its seed, regenerated inside perturb / update (no factor buffer);
+        # regenerate_noise=False stores them with the noise kernel first (the same bits)
+        factors = (nz.epoch_noise(pop, seed=seed) if self.cfg.regenerate_noise
+                   else nz.sample_factors(pop, self.device, seed=seed))
         mark("noise")
         tp = nz.perturb(theta, factors, pop, self.lo, self.hi, out=self.theta_pop[:nl])  # theta_k
         mark("perturb")
@@ -200,7 +205,7 @@ class ESEngine:
         return S_local, raw_local, factors, info
 
     @torch.no_grad()
-    def finish(self, theta: torch.Tensor, S: torch.Tensor, raw: torch.Tensor, factors: torch.Tensor, info, seed: int,
+    def finish(self, theta: torch.Tensor, S: torch.Tensor, raw: torch.Tensor, factors, info, seed: int,
                mark=lambda name: None):
         """Steps 7-8 on the gathered S (identical on every rank)."""
         fit = K.fitness(S, self.cfg.promptnorm)                                            # (3)

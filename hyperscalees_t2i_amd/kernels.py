@@ -202,6 +202,27 @@ def perturb(theta: Optional[torch.Tensor], factors: torch.Tensor, layout: ThetaL
     return out
 
 
+def perturb_seeded(theta: Optional[torch.Tensor], seed: int, layout: ThetaLayout, pop: int, antithetic: bool,
+                   member_lo: int, member_hi: int, sigma: float, device, out: Optional[torch.Tensor] = None
+                   ) -> torch.Tensor:
+    """perturb() with the factors regenerated in the kernel from `seed` (eggroll_perturb_seeded): bit-identical
+    to perturb(theta, noise_factors(seed, n_base), ...) with no factor buffer."""
+    device = torch.device(device)
+    if theta is not None:
+        _dev(theta, "perturb_seeded(theta)", torch.float32)
+    n = member_hi - member_lo
+    if out is None:
+        out = torch.empty((n, _pad4(layout.D)), dtype=torch.float32, device=device)[:, :layout.D]
+    if out.dim() != 2 or out.stride(1) != 1 or out.shape[1] < layout.D:
+        raise _lib.EggrollError("perturb_seeded(out): expected a [n, >= D] fp32 device tensor with unit inner stride")
+    if out.device.type != "cuda" or out.dtype != torch.float32:
+        raise _lib.EggrollError("perturb_seeded(out): expected a ROCm fp32 tensor (no CPU fallback)")
+    _lib.call("eggroll_perturb_seeded", int(seed) & 0xFFFFFFFFFFFFFFFF, _p(theta), layout.mats_on(device).data_ptr(),
+              layout.tiles_on(device).data_ptr(), layout.n_tiles, layout.D, layout.rank, pop, int(bool(antithetic)),
+              member_lo, member_hi, float(sigma), out.data_ptr(), out.stride(0), _stream(device))
+    return out
+
+
 # ---------------------------------------------------------------------------------------
 # (3) fitness
 # ---------------------------------------------------------------------------------------
@@ -255,6 +276,24 @@ def update(theta: torch.Tensor, factors: torch.Tensor, fit: Dict[str, torch.Tens
               fit["fitness"].data_ptr(), fit["stats"].data_ptr(), pop, int(bool(antithetic)),
               layout.mats_on(dev).data_ptr(), layout.tiles_on(dev).data_ptr(), layout.n_tiles, layout.D, layout.rank,
               float(lr),
+              float(max_step_norm or 0.0), float(theta_max_norm or 0.0), workspace.buf.data_ptr(), out.data_ptr(),
+              _stream(dev))
+    return out
+
+
+def update_seeded(theta: torch.Tensor, seed: int, fit: Dict[str, torch.Tensor], layout: ThetaLayout, pop: int,
+                  antithetic: bool, lr: float, max_step_norm: float, theta_max_norm: float,
+                  out: Optional[torch.Tensor] = None, workspace: Optional[UpdateWorkspace] = None) -> torch.Tensor:
+    """update() with the factors regenerated in the kernel from `seed` (eggroll_update_seeded)."""
+    _dev(theta, "update_seeded(theta)", torch.float32)
+    dev = theta.device
+    if out is None:
+        out = torch.empty_like(theta)
+    if workspace is None:
+        workspace = UpdateWorkspace(layout, dev)
+    _lib.call("eggroll_update_seeded", int(seed) & 0xFFFFFFFFFFFFFFFF, theta.data_ptr(), fit["fitness"].data_ptr(),
+              fit["stats"].data_ptr(), pop, int(bool(antithetic)), layout.mats_on(dev).data_ptr(),
+              layout.tiles_on(dev).data_ptr(), layout.n_tiles, layout.D, layout.rank, float(lr),
               float(max_step_norm or 0.0), float(theta_max_norm or 0.0), workspace.buf.data_ptr(), out.data_ptr(),
               _stream(dev))
     return out

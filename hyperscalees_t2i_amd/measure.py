@@ -7,6 +7,11 @@ priced against its ALGORITHMIC bytes:
   perturb        4 * (n_local * D + D + n_used * F)    (theta_pop written, theta + the local members'
                                                        factor sets read)
   update         4 * (n_base * F + 2 * D)              (factors + theta read, theta' written)
+  perturb_seeded 4 * (n_local * D + D)                 (factors regenerated in the kernel: no factor bytes)
+  update_seeded  4 * (2 * D)                           (idem)
+The seeded kernels replace HBM bytes by Philox4x32-10 + Box-Muller work: `philox_quads` per launch
+(one quad = 4 normals; perturb regenerates each local member's long factors, update every base
+sample's) is reported next to the byte-based fraction.
 with F = layout.factor_len_packed, the useful factor values per base sample (the 16-byte alignment
 pads of the device layout, < 0.2 % at the Sana shapes, are not counted).
 The fitness kernel reads a [pop, m] score matrix: latency-bound, reported in microseconds.
@@ -92,6 +97,24 @@ def aux_kernel_rooflines(layout: ThetaLayout, pop: int, member_lo: int, member_h
     out["update_caps_pass"] = {"us": max(out["update"]["us"] - out["update_nocaps"]["us"], 0.0),
                                "note": "the caps pass: a fixed-order reduction of n_tiles x 32 B of norm partials "
                                        "plus one dependent launch; latency-bound (rescales only if a cap fires)"}
+    # the engine path: factors regenerated inside perturb / update (no noise launch, no factor bytes)
+    sf = K.perturb_seeded
+    sec = _time(lambda: sf(theta, 0, layout, pop, antithetic, member_lo, member_hi, sigma, device, out=tp), it)
+    out["perturb_seeded"] = _entry(sec, 4.0 * (nl * D + D))
+    out["perturb_seeded"]["philox_quads"] = nl * F / 4.0
+    sec = _time(lambda: K.update_seeded(theta, 0, fit, layout, pop, antithetic, lr, 0.0, 40.0, out=newt, workspace=ws),
+                it)
+    out["update_seeded"] = _entry(sec, 4.0 * 2 * D)
+    out["update_seeded"]["philox_quads"] = nb * F / 4.0
+    sec = _time(lambda: K.update_seeded(theta, 0, fit, layout, pop, antithetic, lr, 0.0, 0.0, out=newt, workspace=ws),
+                it)
+    out["update_seeded_nocaps"] = _entry(sec, 4.0 * 2 * D)
+    out["update_seeded_nocaps"]["philox_quads"] = nb * F / 4.0
+    out["es_epoch_us"] = {
+        "stored": out["noise_factors"]["us"] + out["perturb"]["us"] + out["update"]["us"],
+        "seeded": out["perturb_seeded"]["us"] + out["update_seeded"]["us"],
+        "note": "noise + perturb + update(+caps) with the factors stored in HBM vs regenerated inside perturb / "
+                "update (the engine default); fitness and the all-gather are the same in both"}
     # empirical write / copy floors on this box for the same byte counts (torch's fill and copy kernels):
     # the noise kernel writes nb * F floats and also runs Philox4x32-10 + Box-Muller per 4 of them, so it is
     # priced against both the HBM peak (frac) and the plain-store floor (frac_of_store_floor)

@@ -104,6 +104,16 @@ int eggroll_perturb(const float* theta, const float* factors, int64_t ld_f, int6
                     int32_t pop, int32_t antithetic, int64_t member_lo, int64_t member_hi,
                     float sigma, float* out, int64_t ld_out, void* stream);
 
+/* Perturb with the noise REGENERATED in the kernel (north_star kernel (1)): the same result as
+ * eggroll_noise_factors(seed, 0, n_base, ...) followed by eggroll_perturb on those factors, bit for
+ * bit, but every factor value is recomputed (Philox4x32-10 + Box-Muller of its counter) where it is
+ * consumed — no factor buffer is written or read.  Replaces torch.manual_seed(epoch) +
+ * EggRollNoiser.sample_eps + theta + sigma * eps[k] (unifed_es.py:120-160).                     */
+int eggroll_perturb_seeded(uint64_t seed, const float* theta, const eggroll_mat_t* mats,
+                           const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank,
+                           int32_t pop, int32_t antithetic, int64_t member_lo, int64_t member_hi,
+                           float sigma, float* out, int64_t ld_out, void* stream);
+
 /* (3) Fitness — replaces paper_prompt_normalized_scores (utills.py:310-330) or
  * S.mean(dim=1) (unifed_es.py:234), the finite mask (unifed_es.py:236-240,266),
  * standardize_fitness (utills.py:168-178) and the rank sort (unifed_es.py:244).
@@ -135,6 +145,15 @@ int eggroll_update(const float* theta, const float* factors, int64_t ld_f, int64
                    const eggroll_mat_t* mats, const eggroll_tile_t* tiles, int64_t n_tiles,
                    int64_t D, int32_t rank, float lr, float max_step_norm, float theta_max_norm,
                    void* workspace, float* theta_out, void* stream);
+
+/* Update with the noise regenerated in the kernel from `seed` (see eggroll_perturb_seeded): the
+ * same result as eggroll_update on eggroll_noise_factors(seed, 0, n_base) bit for bit, n_base
+ * derived from (pop, antithetic).  The factor read — 4 * n_base * factor_len bytes — is gone.      */
+int eggroll_update_seeded(uint64_t seed, const float* theta, const float* fitness, const float* stats,
+                          int32_t pop, int32_t antithetic, const eggroll_mat_t* mats,
+                          const eggroll_tile_t* tiles, int64_t n_tiles, int64_t D, int32_t rank, float lr,
+                          float max_step_norm, float theta_max_norm, void* workspace, float* theta_out,
+                          void* stream);
 
 
 /* eggroll_lora_linear_pop with one elementwise op fused into the GEMM epilogue, applied to the

@@ -100,6 +100,62 @@ def test_perturb_member_ranges_consistent(dev):
     assert np.array_equal(eps.cpu().numpy(), ref)
 
 
+# ---------------------------------------------------------------- regenerated (seeded) noise
+# eggroll_perturb_seeded / eggroll_update_seeded regenerate every factor value inside the kernel from the
+# epoch seed; they must equal the stored path (noise kernel -> perturb / update) bit for bit, on every tile
+# kind: fast WIDE / TALL at ranks 1 / 2 / 4 with NU 1 / 2 / 4, aligned 1-D params (VEC4), unaligned 1-D
+# params (generic VEC) and rank 3 (generic GEN: a factor element per Philox quad).
+SEEDED_SHAPES = [(2, 2240), (2240, 2), (1, 300), (300, 1), (4, 96), (96, 4), (16,), (7,), (3, 5), (5, 3), (2, 7)]
+
+
+@pytest.mark.parametrize("rank", [1, 2, 3, 4])
+@pytest.mark.parametrize("pop,anti", [(8, True), (7, True), (6, False)])
+def test_seeded_perturb_bitexact_vs_stored(dev, rank, pop, anti):
+    n = EggRollNoiser(SEEDED_SHAPES, sigma=0.01, lr_scale=0.1, rank=rank, use_antithetic=anti)
+    theta = torch.randn(n.num_params, device=dev)
+    for seed in (3, 2 ** 40 + 11):
+        fac = n.sample_factors(pop, dev, seed=seed)
+        sf = n.epoch_noise(pop, seed=seed)
+        assert torch.equal(sf.materialise(n.layout, dev), fac)
+        for lo, hi in ((0, pop), (1, pop - 1)):
+            assert torch.equal(n.perturb(theta, sf, pop, lo, hi), n.perturb(theta, fac, pop, lo, hi)), (seed, lo, hi)
+        assert torch.equal(n.eps_from_factors(sf, pop, device=dev), n.eps_from_factors(fac, pop))
+
+
+@pytest.mark.parametrize("rank", [1, 2, 3, 4])
+@pytest.mark.parametrize("pop,anti", [(8, True), (7, True), (6, False), (64, True)])
+@pytest.mark.parametrize("caps", [(0.0, 0.0), (2e-4, 0.5)])
+def test_seeded_update_bitexact_vs_stored(dev, rank, pop, anti, caps):
+    n = EggRollNoiser(SEEDED_SHAPES, sigma=0.01, lr_scale=0.1, rank=rank, use_antithetic=anti)
+    g = torch.Generator().manual_seed(pop + rank)
+    theta = (torch.randn(n.num_params, generator=g) * 0.02).to(dev)
+    S = (torch.randn(pop, 4, generator=g) + 20).to(dev)
+    fit = K.fitness(S, True)
+    fac = n.sample_factors(pop, dev, seed=5)
+    a = n.update_from_factors(theta, fac, fit, pop, max_step_norm=caps[0], theta_max_norm=caps[1])
+    b = n.update_from_factors(theta, n.epoch_noise(pop, seed=5), fit, pop, max_step_norm=caps[0],
+                              theta_max_norm=caps[1])
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("layout", ["sana_r1_pop64", "zimage_r4_pop128", "infinity_r1_pop32"])
+def test_seeded_full_size_layouts_bitexact(dev, layout):
+    """The BASELINE node-level configs' theta layouts (one GPU's member share): seeded == stored."""
+    from hyperscalees_t2i_amd.model_shapes import infinity_lora_shapes, zimage_turbo_lora_shapes
+    from hyperscalees_t2i_amd.sana import SanaArch, sana_lora_shapes
+    shapes, rank, pop, nl = {"sana_r1_pop64": (sana_lora_shapes(SanaArch()), 1, 64, 8),
+                             "zimage_r4_pop128": (zimage_turbo_lora_shapes(), 4, 128, 16),
+                             "infinity_r1_pop32": (infinity_lora_shapes(), 1, 32, 4)}[layout]
+    n = EggRollNoiser(shapes, sigma=0.01, lr_scale=0.1, rank=rank, use_antithetic=True)
+    theta = torch.randn(n.num_params, device=dev) * 0.01
+    fac = n.sample_factors(pop, dev, seed=9)
+    sf = n.epoch_noise(pop, seed=9)
+    assert torch.equal(n.perturb(theta, sf, pop, pop - nl, pop), n.perturb(theta, fac, pop, pop - nl, pop))
+    fit = K.fitness((torch.randn(pop, 4, generator=torch.Generator().manual_seed(2)) + 20).to(dev), True)
+    assert torch.equal(n.update_from_factors(theta, sf, fit, pop, theta_max_norm=40.0),
+                       n.update_from_factors(theta, fac, fit, pop, theta_max_norm=40.0))
+
+
 # ---------------------------------------------------------------------------------- fitness
 def test_fitness_bit_exact_vs_oracle_and_reference_ranks(dev, golden):
     g = _groups(golden("g2_fitness.npz"))
