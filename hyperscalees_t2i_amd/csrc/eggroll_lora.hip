@@ -3310,16 +3310,26 @@ int eggroll_lora_linear_pop_sel(const void* X, int64_t ldx, const void* W, int64
                           ldy, kernel == 12 ? 8 : kernel, stream);
 }
 
-int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
-                                    const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
-                                    float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
-                                    int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr,
-                                    const void* gate, int64_t gstride, int64_t rows_per_group, int32_t kernel,
-                                    void* stream) {
+// The epilogue GEMM with T = X A_k^T already computed (shared by linear_pop_epi and lora_gemm_epi).
+static int gemm_epi_impl(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                         const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                         int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy, int32_t epi,
+                         const void* res, int64_t ldr, const void* gate, int64_t gstride, int64_t rows_per_group,
+                         int32_t kernel, void* stream) {
+    const EpiArgs ea{(const unsigned short*)res, ldr, (const unsigned short*)gate, gstride, rows_per_group};
+    const int64_t rpm = r ? rows_per_member : (M > 0 ? M : 1);
+    if (kernel == 0) kernel = gemm8_auto(M, N, r, rpm, epi);
+    if (kernel == 10)
+        return launch_gemm8n(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rpm, M, N, K, Y, ldy, epi,
+                             ea, as_stream(stream));
+    return launch_gemm8_epi(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rpm, M, N, K, Y, ldy, epi,
+                            ea, as_stream(stream));
+}
+
+static int epi_args_ok(const void* X, int64_t ldx, const void* W, int64_t ldw, int32_t r, int64_t rows_per_member,
+                       int64_t M, int64_t N, int64_t K, const void* Y, int64_t ldy, int32_t epi, const void* res,
+                       int64_t ldr, const void* gate, int64_t gstride, int64_t rows_per_group, int32_t kernel) {
     EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 10, "lora_linear_pop_epi: kernel must be 0, 8 or 10");
-    if (epi == EPI_NONE)
-        return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
-                                           rows_per_member, M, N, K, Y, ldy, T_ws, kernel, stream);
     EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_MUL, "lora_linear_pop_epi: epi=%d unknown", epi);
     EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
     EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
@@ -3332,19 +3342,43 @@ int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, i
     if (M == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(X && W && (Y || epi == EPI_RES32 || epi == EPI_GATED32), "lora_linear_pop_epi: NULL pointer");
     EGG_CHECK_ARG(M * ldx * 2 < (1ll << 31) && N * ldw * 2 < (1ll << 31), "lora_linear_pop_epi: operand > 2 GiB");
+    return EGGROLL_OK;
+}
+
+int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                                    const float* theta_pop, int64_t ld_theta, int64_t offA, int64_t offB, int32_t r,
+                                    float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                                    int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr,
+                                    const void* gate, int64_t gstride, int64_t rows_per_group, int32_t kernel,
+                                    void* stream) {
+    if (epi == EPI_NONE) {
+        EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 10, "lora_linear_pop_epi: kernel must be 0, 8 or 10");
+        return eggroll_lora_linear_pop_sel(X, ldx, W, ldw, bias, theta_pop, ld_theta, offA, offB, r, scale,
+                                           rows_per_member, M, N, K, Y, ldy, T_ws, kernel, stream);
+    }
+    const int rc0 = epi_args_ok(X, ldx, W, ldw, r, rows_per_member, M, N, K, Y, ldy, epi, res, ldr, gate, gstride,
+                                rows_per_group, kernel);
+    if (rc0 || M == 0) return rc0;
     if (r > 0) {
         EGG_CHECK_ARG(theta_pop && T_ws, "lora_linear_pop_epi: theta_pop / T_ws NULL with r > 0");
         int rc = eggroll_lora_project(X, ldx, theta_pop, ld_theta, offA, r, rows_per_member, M, K, T_ws, stream);
         if (rc) return rc;
     }
-    const EpiArgs ea{(const unsigned short*)res, ldr, (const unsigned short*)gate, gstride, rows_per_group};
-    const int64_t rpm = r ? rows_per_member : (M > 0 ? M : 1);
-    if (kernel == 0) kernel = gemm8_auto(M, N, r, rpm, epi);
-    if (kernel == 10)
-        return launch_gemm8n(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rpm, M, N, K, Y, ldy, epi,
-                             ea, as_stream(stream));
-    return launch_gemm8_epi(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rpm, M, N, K, Y, ldy, epi,
-                            ea, as_stream(stream));
+    return gemm_epi_impl(X, ldx, W, ldw, bias, T_ws, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y,
+                         ldy, epi, res, ldr, gate, gstride, rows_per_group, kernel, stream);
+}
+
+int eggroll_lora_gemm_epi_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, const float* T,
+                              const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r, float scale,
+                              int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y, int64_t ldy,
+                              int32_t epi, const void* res, int64_t ldr, const void* gate, int64_t gstride,
+                              int64_t rows_per_group, int32_t kernel, void* stream) {
+    const int rc0 = epi_args_ok(X, ldx, W, ldw, r, rows_per_member, M, N, K, Y, ldy, epi, res, ldr, gate, gstride,
+                                rows_per_group, kernel);
+    if (rc0 || M == 0) return rc0;
+    EGG_CHECK_ARG(r == 0 || (T && theta_pop), "lora_gemm_epi: T / theta_pop NULL with r > 0");
+    return gemm_epi_impl(X, ldx, W, ldw, bias, T, theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, K, Y, ldy,
+                         epi, res, ldr, gate, gstride, rows_per_group, kernel, stream);
 }
 
 int eggroll_lora_linear_pop_epi(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,

@@ -384,6 +384,42 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
     return res if f32res else out
 
 
+def lora_gemm_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T: Optional[torch.Tensor],
+                  theta_pop: Optional[torch.Tensor], offB: int, r: int, scale: float, rows_per_member: int, epi: str,
+                  res: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None, rows_per_group: int = 1,
+                  out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
+    """lora_linear_pop_epi's GEMM with T = X A_k^T given (eggroll_lora_gemm_epi_sel): the same kernel and bits
+    as the second of lora_linear_pop_epi's two launches.  Same res / out / return conventions."""
+    _dev(x, "lora_gemm_epi(x)", torch.bfloat16)
+    _dev(W, "lora_gemm_epi(W)", torch.bfloat16)
+    M, Kd = x.shape
+    N = W.shape[0]
+    code = EPI[epi]
+    if code == 0:
+        raise ValueError("lora_gemm_epi: needs an epilogue op (use lora_gemm)")
+    f32res = code in (4, 5)
+    if res is not None:
+        _dev(res, "lora_gemm_epi(res)", torch.float32 if f32res else torch.bfloat16)
+        if res.shape[-1] != N or res.numel() != M * N:
+            raise ValueError(f"res {tuple(res.shape)} does not match [{M}, {N}]")
+    if f32res:
+        if res is None or (code == 5 and (gate is None or gate.dtype != torch.float32)):
+            raise ValueError(f"lora_gemm_epi({epi}): needs an fp32 res (and an fp32 gate)")
+        if out is not None:
+            _dev(out, "lora_gemm_epi(out)", torch.bfloat16)
+    elif out is None:
+        out = res if res is not None and code in (2, 3, 7) else torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    pg, gst = _row_ptr(gate, "lora_gemm_epi(gate)", N, allow_f32=code == 5) if gate is not None else (None, 0)
+    if r > 0:
+        _dev(theta_pop, "lora_gemm_epi(theta_pop)", torch.float32)
+        _dev(T, "lora_gemm_epi(T)", torch.float32)
+    _lib.call("eggroll_lora_gemm_epi_sel", x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), _p(bias),
+              _p(T) if r > 0 else None, _p(theta_pop) if r > 0 else None, theta_pop.stride(0) if r > 0 else 0, offB, r,
+              float(scale), rows_per_member, M, N, Kd, _p(out), N, code, _p(res), N if res is not None else 0, pg,
+              gst or N, int(rows_per_group), int(kernel), _stream(x.device))
+    return res if f32res else out
+
+
 def lora_workspace_numel(M: int, K: int, r: int, rows_per_member: int) -> int:
     """fp32 elements of the eggroll_lora_linear_pop workspace (T, or the fused path's A_k images)."""
     nbytes = int(_lib.load().eggroll_lora_workspace_bytes(M, K, r, rows_per_member))
@@ -414,13 +450,13 @@ def lora_gemm(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], T:
     return out
 
 
-def gemm_tile_for(M: int, N: int, r: int = 2, rows_per_member: int = 1 << 30) -> int:
-    """Kernel libeggroll's automatic choice uses for an M x N LoRA GEMM without an epilogue op (mirrors
-    lora_gemm_impl / gemm8_auto): 8 = the 8-phase 256x256 kernel, 10 = the 8-phase 256x320 kernel,
-    128 = the 128x128 one-barrier tile."""
-    if (M // 256) * ((N + 255) // 256) < 512:
+def gemm_tile_for(M: int, N: int, r: int = 2, rows_per_member: int = 1 << 30, epi: Optional[str] = None) -> int:
+    """Kernel libeggroll's automatic choice uses for an M x N LoRA GEMM (mirrors lora_gemm_impl / gemm_epi_impl
+    / gemm8_auto): 8 = the 8-phase 256x256 kernel, 10 = the 8-phase 256x320 kernel, 128 = the 128x128
+    one-barrier tile (no epilogue op only)."""
+    if epi is None and (M // 256) * ((N + 255) // 256) < 512:
         return 128
-    if not (r == 0 or (r <= 2 and rows_per_member >= 256)):
+    if not (r == 0 or (r <= 2 and rows_per_member >= 256)) or epi in ("res", "gated", "mul"):
         return 8
     tm = -(-M // 256)
     rounds8, rounds10 = -(-(tm * -(-N // 256)) // 256), -(-(tm * -(-N // 320)) // 256)

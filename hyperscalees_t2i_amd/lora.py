@@ -59,41 +59,68 @@ class PopulationContext:
 
 class GemmTimer:
     """Opt-in live timing of every population LoRA linear with HIP events recorded on the launching
-    stream (bench.py's roofline leg).  While active, each linear runs as its two kernels with an
-    event between them — k_lora_project (T = X A_k^T, HBM-bound) and the GEMM + fused LoRA epilogue
-    (MFMA-bound) — so each kernel's duration is its own (the figure rocprof reports per kernel).
-    Records (e0, e1, e2, M, N, K, r, rows_per_member)."""
+    stream (bench.py's roofline leg).  The product path is kept — fused epilogues (the fp32 residual
+    stream's res32 / gated32, bf16 res / gated, SiLU / GELU) and the shared projections included — but
+    each linear's projection (k_lora_project, HBM-bound) and its GEMM + LoRA / op epilogue (MFMA-bound)
+    are launched as their two kernels with an event between them (the linear_pop[_epi] C calls run the
+    same two launches back to back: eggroll_lora_gemm_epi_sel is the second on its own), so each kernel's
+    duration is its own — the figure rocprof reports per kernel.
+    records: (e0 | None, e1, e2, M, N, K, r, rows_per_member, epi) — e0..e1 the projection (None when the
+    shared projection made T), e1..e2 the GEMM; proj_records: (e0, e1, M, K, n_linears, r) of the
+    shared projections."""
 
     active = False
     records: List[tuple] = []
+    proj_records: List[tuple] = []
 
     @classmethod
     def reset(cls, active: bool):
-        cls.active, cls.records = active, []
+        cls.active, cls.records, cls.proj_records = active, [], []
+
+    @staticmethod
+    def epilogue_bytes(M: int, N: int, epi: Optional[str]) -> float:
+        """HBM bytes an epilogue op adds to the bf16 y write: fp32 stream read + write (+ its bf16 shadow)
+        for res32 / gated32, the bf16 residual / multiplicand read for res / gated / mul."""
+        if epi in ("res32", "gated32"):
+            return 10.0 * M * N
+        if epi in ("res", "gated", "mul"):
+            return 2.0 * M * N
+        return 0.0
 
     @classmethod
     def summary(cls) -> Dict[str, Dict[str, float]]:
-        """Per GEMM kernel variant (what rocprof names: k_lora_gemm8<r> = the 8-phase 256x256 tile,
-        k_lora_gemm8n<r> = the 8-phase 256x320 tile, k_lora_gemm<r,Tile<128>>) and "all": launches,
-        total/avg kernel time, algorithmic FLOP = 2MNK (base) + 2MNr (rank-r LoRA expansion in the
-        epilogue).  "k_lora_project<r>": the projection pre-pass, algorithmic bytes = X (2MK) + T (4Mr)
-        + the members' A rows (4 n_k r K)."""
+        """Per GEMM kernel variant as rocprof names them (k_lora_gemm8<r> / k_lora_gemm8n<r> = the 8-phase
+        256x256 / 256x320 tiles, k_lora_gemm<r,Tile<128>>; ",epi" = the fused op code of
+        kernels.EPI) and "all": launches, total / avg kernel time, algorithmic FLOP = 2MNK (base) + 2MNr
+        (rank-r LoRA expansion in the epilogue), the epilogue op's HBM bytes.  "k_lora_project<r>" /
+        "k_lora_project_multi": the projection pre-passes, algorithmic bytes = X (2MK) + T (4Mr per linear)
+        + the members' A rows (4 n_k r K per linear)."""
         torch.cuda.synchronize()
         out: Dict[str, Dict[str, float]] = {}
-        for e0, e1, e2, M, N, Kd, r, rpm in cls.records:
-            t = K.gemm_tile_for(M, N, r, rpm)
-            name = {8: f"k_lora_gemm8<{r}>", 10: f"k_lora_gemm8n<{r}>"}.get(t, f"k_lora_gemm<{r},Tile<{t}>>")
+        for e0, e1, e2, M, N, Kd, r, rpm, epi in cls.records:
+            t = K.gemm_tile_for(M, N, r, rpm, epi)
+            code = K.EPI[epi]
+            name = {8: f"k_lora_gemm8<{r},{code}>", 10: f"k_lora_gemm8n<{r},{code}>"}.get(t, f"k_lora_gemm<{r},Tile<{t}>>")
             ms = e1.elapsed_time(e2)
             fl = 2.0 * M * N * Kd + 2.0 * M * N * r
             for key in (name, "all"):
-                d = out.setdefault(key, {"launches": 0, "total_ms": 0.0, "flops": 0.0})
+                d = out.setdefault(key, {"launches": 0, "total_ms": 0.0, "flops": 0.0, "epi_bytes": 0.0})
                 d["launches"] += 1
                 d["total_ms"] += ms
                 d["flops"] += fl
-            d = out.setdefault(f"k_lora_project<{r}>", {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
+                d["epi_bytes"] += cls.epilogue_bytes(M, N, epi)
+                if key != "all":
+                    d["shape"] = f"{M}x{N}x{Kd}"
+            if e0 is not None:
+                d = out.setdefault(f"k_lora_project<{r}>", {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
+                d["launches"] += 1
+                d["total_ms"] += e0.elapsed_time(e1)
+                d["bytes"] += 2.0 * M * Kd + 4.0 * M * r + 4.0 * (-(-M // rpm)) * r * Kd
+        for e0, e1, M, Kd, nl, r in cls.proj_records:
+            d = out.setdefault("k_lora_project_multi", {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
             d["launches"] += 1
             d["total_ms"] += e0.elapsed_time(e1)
-            d["bytes"] += 2.0 * M * Kd + 4.0 * M * r + 4.0 * (-(-M // rpm)) * r * Kd
+            d["bytes"] += 2.0 * M * Kd + nl * 4.0 * M * r
         for d in out.values():
             d["avg_us"] = 1e3 * d["total_ms"] / d["launches"]
             if "flops" in d:
@@ -101,6 +128,12 @@ class GemmTimer:
             else:
                 d["GBps"] = d["bytes"] / (d["total_ms"] * 1e6) if d["total_ms"] > 0 else float("nan")
         return out
+
+    @classmethod
+    def events(cls, n: int):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+        ev[0].record()
+        return ev
 
 
 class _Weight(nn.Module):
@@ -163,13 +196,16 @@ class LoRALinear(nn.Module):
         if M * self.in_features * 2 >= GEMM_OPERAND_LIMIT:   # the GEMMs address X with 32-bit buffer offsets
             return self._forward_chunked(x2, shp, epi, res, gate, rows_per_group, T, shadow)
         if epi in ("silu", "gelu"):   # silu / gelu(tanh) of the bf16-rounded output, in the GEMM epilogue where it applies
-            if (FUSE_EPILOGUES and ctx is not None and ctx.theta_pop is not None and self.r <= 2 and not GemmTimer.active
+            if (FUSE_EPILOGUES and ctx is not None and ctx.theta_pop is not None and self.r <= 2
                     and M % ctx.n_members == 0 and (self.r == 0 or M // ctx.n_members >= 256)
                     and self.in_features % 64 == 0):
                 rpm = M // ctx.n_members
                 ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device) if self.r else None
-                y = K.lora_linear_pop_epi(x2, self.weight, self.bias, ctx.theta_pop if self.r else None,
-                                          self.theta_off_A, self.theta_off_B, self.r, self.scale, rpm, epi, T_ws=ws)
+                if GemmTimer.active and self.r:
+                    y = self._timed_epi(x2, ctx.theta_pop, ws, rpm, epi)
+                else:
+                    y = K.lora_linear_pop_epi(x2, self.weight, self.bias, ctx.theta_pop if self.r else None,
+                                              self.theta_off_A, self.theta_off_B, self.r, self.scale, rpm, epi, T_ws=ws)
             elif epi == "silu":
                 y = torch.nn.functional.silu(self.forward(x).view(M, self.out_features))
             else:
@@ -179,15 +215,18 @@ class LoRALinear(nn.Module):
             res2 = res.view(M, self.out_features)
             sh2 = shadow.view(M, self.out_features) if shadow is not None else None
             if (FUSE_EPILOGUES and self.r and ctx is not None and ctx.theta_pop is not None and self.r <= 2
-                    and not GemmTimer.active
                     and M % ctx.n_members == 0 and M // ctx.n_members >= 256 and self.in_features % 64 == 0):
                 rpm = M // ctx.n_members
                 ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device)
-                K.lora_linear_pop_epi(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
-                                      self.r, self.scale, rpm, epi, res=res2, gate=gate, rows_per_group=rows_per_group,
-                                      T_ws=ws, out=sh2)
+                if GemmTimer.active:
+                    self._timed_epi(x2, ctx.theta_pop, ws, rpm, epi, res=res2, gate=gate, rows_per_group=rows_per_group,
+                                    out=sh2)
+                else:
+                    K.lora_linear_pop_epi(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
+                                          self.r, self.scale, rpm, epi, res=res2, gate=gate,
+                                          rows_per_group=rows_per_group, T_ws=ws, out=sh2)
                 return res
-            if (FUSE_EPILOGUES and not self.r and not GemmTimer.active and M >= max(4096, self.lib_small_m + 1)
+            if (FUSE_EPILOGUES and not self.r and M >= max(4096, self.lib_small_m + 1)
                     and self.in_features % 64 == 0
                     and epi in ("res", "gated", "mul")):   # plain linear (no LoRA), epilogue fused (Infinity's proj / fc2)
                 K.lora_linear_pop_epi(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M, epi, res=res2, gate=gate,
@@ -211,8 +250,13 @@ class LoRALinear(nn.Module):
             rpm = M // ctx.n_members
             ws = ctx.workspace(K.lora_workspace_numel(M, self.in_features, self.r, rpm), x2.device)
             if T is not None:     # projection already done for the linears sharing this input
+                ev = GemmTimer.events(2) if GemmTimer.active else None
                 y = K.lora_gemm(x2, self.weight, self.bias, T, ctx.theta_pop, self.theta_off_B, self.r, self.scale,
                                 rpm)
+                if ev is not None:
+                    ev[1].record()
+                    GemmTimer.records.append((None, ev[0], ev[1], M, self.out_features, self.in_features, self.r, rpm,
+                                              None))
             elif GemmTimer.active:  # the same two kernels as lora_linear_pop's unfused path, timed apart
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 T = ws[: M * self.r].view(M, self.r)
@@ -222,7 +266,7 @@ class LoRALinear(nn.Module):
                 y = K.lora_gemm(x2, self.weight, self.bias, T, ctx.theta_pop, self.theta_off_B, self.r, self.scale,
                                 rpm)
                 ev[2].record()
-                GemmTimer.records.append((*ev, M, self.out_features, self.in_features, self.r, rpm))
+                GemmTimer.records.append((*ev, M, self.out_features, self.in_features, self.r, rpm, None))
             else:  # projection T = X A_k^T + GEMM + LoRA epilogue (one fused kernel when eligible)
                 y = K.lora_linear_pop(x2, self.weight, self.bias, ctx.theta_pop, self.theta_off_A, self.theta_off_B,
                                       self.r, self.scale, rpm, T_ws=ws)
@@ -241,6 +285,20 @@ class LoRALinear(nn.Module):
             y = K.lora_linear_pop(x2, self.weight, self.bias, None, 0, 0, 0, 0.0, M)
         return y.view(*shp[:-1], self.out_features)
 
+
+    def _timed_epi(self, x2, theta_pop, ws, rpm, epi, res=None, gate=None, rows_per_group=1, out=None):
+        """lora_linear_pop_epi as its two launches with HIP events around each (GemmTimer): the projection,
+        then the epilogue GEMM on that T — the same kernels and bits as the fused call."""
+        M = x2.shape[0]
+        T = ws[: M * self.r].view(M, self.r)
+        ev = GemmTimer.events(3)
+        K.lora_project(x2, theta_pop, self.theta_off_A, self.r, rpm, out=T)
+        ev[1].record()
+        y = K.lora_gemm_epi(x2, self.weight, self.bias, T, theta_pop, self.theta_off_B, self.r, self.scale, rpm, epi,
+                            res=res, gate=gate, rows_per_group=rows_per_group, out=out)
+        ev[2].record()
+        GemmTimer.records.append((*ev, M, self.out_features, self.in_features, self.r, rpm, epi))
+        return y
 
     def _forward_chunked(self, x2, shp, epi, res, gate, rows_per_group, T, shadow):
         """forward() over row chunks whose X stays under 2 GiB: whole members per chunk on the population
@@ -332,7 +390,7 @@ def shared_projection(mods: Sequence[LoRALinear], x: torch.Tensor) -> List[Optio
     (single-member mode, LoRA off, GemmTimer's per-kernel timing, unsupported shapes)."""
     none = [None] * len(mods)
     ctx = mods[0].ctx if mods else None
-    if (not SHARED_PROJECTION or GemmTimer.active or ctx is None or ctx.theta_pop is None or len(mods) < 2
+    if (not SHARED_PROJECTION or ctx is None or ctx.theta_pop is None or len(mods) < 2
             or any(m.ctx is not ctx for m in mods)):
         return none
     r, Kd = mods[0].r, mods[0].in_features
@@ -346,7 +404,11 @@ def shared_projection(mods: Sequence[LoRALinear], x: torch.Tensor) -> List[Optio
     if M % ctx.n_members:
         raise RuntimeError(f"{M} rows do not split over {ctx.n_members} members")
     ws = ctx.multi_workspace(len(mods) * M * r, x2.device).view(len(mods), M, r)
+    ev = GemmTimer.events(2) if GemmTimer.active else None
     K.lora_project_multi(x2, ctx.theta_pop, [m.theta_off_A for m in mods], r, M // ctx.n_members, out=ws)
+    if ev is not None:
+        ev[1].record()
+        GemmTimer.proj_records.append((ev[0], ev[1], M, Kd, len(mods), r))
     return [ws[i] for i in range(len(mods))]
 
 

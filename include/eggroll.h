@@ -181,6 +181,14 @@ int eggroll_lora_linear_pop_epi_sel(const void* X, int64_t ldx, const void* W, i
                                     int64_t ldy, float* T_ws, int32_t epi, const void* res, int64_t ldr,
                                     const void* gate, int64_t gstride, int64_t rows_per_group, int32_t kernel,
                                     void* stream);
+/* The epilogue GEMM alone, with T = X A_k^T already computed (fp32 [M, r], e.g. by
+ * eggroll_lora_project / eggroll_lora_project_multi): the second of linear_pop_epi's two launches,
+ * bit-identical to it (bench.py times the two apart on the product path).                        */
+int eggroll_lora_gemm_epi_sel(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias,
+                              const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB, int32_t r,
+                              float scale, int64_t rows_per_member, int64_t M, int64_t N, int64_t K, void* Y,
+                              int64_t ldy, int32_t epi, const void* res, int64_t ldr, const void* gate,
+                              int64_t gstride, int64_t rows_per_group, int32_t kernel, void* stream);
 /* (2) Population-batched perturbed LoRA linear — replaces per-member
  * `unflatten_to_params` + PEFT lora.Linear.forward (peft: y = base(x) + B(A x) * alpha/r),
  * members evaluated sequentially in the reference (unifed_es.py:159-163).

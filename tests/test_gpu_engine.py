@@ -238,6 +238,37 @@ def test_fused_epilogues_population_forward(dev):
     assert float((fused - plain).norm() / plain.norm()) < 3e-2   # measured 1.1 % (bf16 through 2 blocks + DC-AE)
 
 
+def test_gemm_timer_keeps_the_product_path_bits(dev):
+    """bench.py's roofline epochs time every LoRA linear's projection and GEMM apart (GemmTimer): the
+    images must be bit-identical to the untimed product path (same kernels, fused epilogues and shared
+    projections kept), and every LoRA GEMM launch is recorded."""
+    from hyperscalees_t2i_amd.lora import GemmTimer
+    arch = SanaArch(num_attention_heads=14, attention_head_dim=32, num_layers=2, num_cross_attention_heads=4,
+                    cross_attention_head_dim=112, caption_channels=2304)
+    cfg = SanaConfig(synthetic_weights=True, width_latent=16, height_latent=16, batches_per_gen=2, arch=arch,
+                     vae_widths=(16, 32, 32, 64, 64, 64), vae_layers=(1, 1, 1, 1, 1, 1))
+    be = SanaBackend(str(dev), cfg)
+    be.init_and_attach_lora()
+    params, shapes = be.collect_lora_params()
+    theta0 = flatten_params(params).to(dev)
+    noiser = EggRollNoiser(shapes, sigma=0.05, lr_scale=0.1, rank=1, use_antithetic=True)
+    tp = noiser.perturb(theta0, noiser.epoch_noise(4, seed=2), 4, 0, 4)
+    flat = be.step_sampling_info(3)["flat_ids"]
+    plain = be.generate_population(flat, 3, 4.5, tp)
+    GemmTimer.reset(True)
+    try:
+        timed = be.generate_population(flat, 3, 4.5, tp)
+        summ = GemmTimer.summary()
+    finally:
+        GemmTimer.reset(False)
+    assert torch.equal(plain, timed)
+    n_lora = sum(1 for m in be.es_model.transformer.modules() if getattr(m, "r", 0))
+    # six LoRA'd linears run fp32 torch GEMMs by design (LoRALinear.forward_fp32: the time / guidance embedders'
+    # linear_1 / linear_2, time_embed.linear, proj_out — DESIGN §3.2); every other one is a recorded launch
+    assert summ["all"]["launches"] == n_lora - 6 and summ["all"]["tflops"] > 0
+    assert any(k.endswith(",4>") or k.endswith(",5>") for k in summ)   # the fp32-stream epilogue variants
+
+
 def test_cross_attention_kernel_in_population_forward(dev):
     """Sana attn2 on eggroll_cross_attention (head dim 112, caption rows through enc_index, mask as
     an additive bias) vs the SDPA path on gathered k / v, inside the population forward."""

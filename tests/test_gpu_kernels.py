@@ -1135,6 +1135,32 @@ def test_lora_epilogue_fp32_stream_bitexact(dev, epi, r, M, N, Kd, rpm, kernel):
     assert torch.equal(got, ref) and torch.equal(sh, ref_sh)
 
 
+@pytest.mark.parametrize("epi", ["silu", "gelu", "res", "gated", "mul", "res32", "gated32"])
+def test_lora_gemm_epi_with_given_T_bitexact(dev, epi):
+    """eggroll_lora_gemm_epi_sel (T precomputed by eggroll_lora_project) == eggroll_lora_linear_pop_epi (which
+    runs the same projection + GEMM itself), bit for bit — the pair GemmTimer times apart on the product path."""
+    M, N, Kd, r, rpm = 4 * 1024, 640, 512, 2, 1024
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn((M, Kd), generator=g, device=dev).to(torch.bfloat16)
+    W = (torch.randn((N, Kd), generator=g, device=dev) / Kd ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=dev).to(torch.bfloat16)
+    tp = torch.randn((M // rpm, Kd * r + N * r + 8), generator=g, device=dev) * 0.05
+    f32 = epi in ("res32", "gated32")
+    res = torch.randn((M, N), generator=g, device=dev)
+    res = res if f32 else res.to(torch.bfloat16)
+    gate = torch.randn((M // 512, N), generator=g, device=dev)
+    gate = gate if f32 else gate.to(torch.bfloat16)
+    kw = dict(gate=gate if "gated" in epi else None, rows_per_group=512)
+    a_res, b_res = (res.clone(), res.clone()) if epi not in ("silu", "gelu") else (None, None)
+    a_sh, b_sh = (torch.empty((M, N), dtype=torch.bfloat16, device=dev) for _ in range(2)) if f32 else (None, None)
+    a = K.lora_linear_pop_epi(x, W, bias, tp, 0, Kd * r, r, 2.0, rpm, epi, res=a_res, out=a_sh, **kw)
+    T = K.lora_project(x, tp, 0, r, rpm)
+    b = K.lora_gemm_epi(x, W, bias, T, tp, Kd * r, r, 2.0, rpm, epi, res=b_res, out=b_sh, **kw)
+    assert torch.equal(a, b)
+    if f32:
+        assert torch.equal(a_sh, b_sh)
+
+
 @pytest.mark.parametrize("B,N,H,L,U,hd", [(4, 64, 2, 37, 2, 112), (3, 100, 3, 300, 3, 112), (6, 17, 1, 320, 2, 112),
                                            (16, 1024, 20, 300, 4, 112),
                                            # Infinity text cross-attention: head dim 128, k / v interleaved in
