@@ -244,14 +244,34 @@ def marker():
     K.philox_words(0xBEEF, 0, 1, torch.device("cuda", torch.cuda.current_device()))
 
 
-def load_pmc_traffic():
-    f = ROOT / "profiles" / "pmc_lora_gemm.json"
+def load_pmc(name: str = "pmc_lora_gemm.json"):
+    f = ROOT / "profiles" / name
     if f.exists():
         try:
             return json.loads(f.read_text())
         except Exception:
             return None
     return None
+
+
+def load_pmc_traffic():
+    return load_pmc("pmc_lora_gemm.json")
+
+
+def mfma_busy_summary():
+    """Counter-measured MFMA-busy fraction of the LoRA GEMM variants (profiles/pmc_lora_gemm_mfma.json, written by
+    tools/gemm_mfma_summary.py from a separate rocprofv3 --pmc pass: the profiler cannot run inside this process)."""
+    d = load_pmc("pmc_lora_gemm_mfma.json")
+    if not d:
+        return None
+    return {"shape": d.get("shape"), "method": d.get("method"),
+            "source": "profiles/pmc_lora_gemm_mfma.json",
+            "kernels": {k: {kk: v[kk] for kk in ("mfma_busy_frac", "mfma_busy_frac_at_2.4GHz", "clock_GHz",
+                                                 "duration_us_median") if kk in v}
+                        for k, v in d.get("kernels", {}).items()},
+            "note": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 128 SIMDs per XCD): the share of SIMD-cycles "
+                    "with an MFMA executing at the clock the chip held; _at_2.4GHz prices the same MFMA cycles "
+                    "against the peak clock (the vendor 2.5 PF figure's)"}
 
 
 def main():
@@ -364,6 +384,10 @@ def main():
                 "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / BF16_DENSE_PEAK_TFLOPS,
                 "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                "traffic_measured_on": ("one epoch's LoRA-GEMM launch mix x2 (tools/lora_epoch_driver.py: every Sana "
+                                        "LoRA'd linear's shape, no epilogue op); profiles/pmc_lora_gemm.json")
+                                       if pmc else None,
+                "mfma_busy": mfma_busy_summary() if args.workload == "sana" and not args.small else None,
                 "launches": dom["launches"], "avg_launch_us": dom["avg_us"],
                 "flops_per_launch": dom["flops"] / max(dom["launches"], 1),
                 "window": {"epochs": n_roof, "ms_per_step": roof_ms_per_step,
