@@ -412,6 +412,10 @@ class ZImageConfig:
     lora_dropout: float = 0.0
     lora_target_modules: List[str] = field(default_factory=lambda: ["to_q", "to_k", "to_v", "linear", "w1", "w2", "w3"])
     use_vae_decoder_lora: bool = False
+    vae_lora_r: int = 2                      # unifed_es.py:488-492 defaults
+    vae_lora_alpha: int = 8
+    vae_lora_dropout: float = 0.0
+    vae_lora_target_modules: List[str] = field(default_factory=lambda: ["to_q", "to_k", "to_v", "to_out.0"])
     dtype: str = "bfloat16"
     # build-specific
     arch: Any = None                         # None: the Z-Image-Turbo config (zimage.ZIMAGE_TURBO)
@@ -456,7 +460,7 @@ class ZImageBackend(ESBackend):
                 raise FileNotFoundError(f"encoded_prompt_path not found and auto_encode unsupported: {enc}")
             self.prompt_data = torch.load(enc, map_location="cpu", weights_only=True)
         else:
-            a = self.cfg.arch
+            a = self.es_model.arch if self.es_model is not None else self.cfg.arch
             self.prompt_data = synthetic_zimage_prompt_data(self.cfg.synthetic_prompts, self.cfg.synthetic_prompt_lens,
                                                             a.cap_feat_dim if a is not None else 2560)
         self.base_prompt_embeds = self.prompt_data["prompt_embeds"]
@@ -466,13 +470,12 @@ class ZImageBackend(ESBackend):
     def init_and_attach_lora(self):
         from .zimage import ZIMAGE_TURBO
         from .zimage_pipeline import ZImageTurboES
+        from .lora import bind_theta_layout
         c = self.cfg
-        if c.use_vae_decoder_lora:
-            raise NotImplementedError("VAE-decoder LoRA (es_backend.py:586-595) is not built")
-        self._load_or_encode_prompts()
         self.es_model = ZImageTurboES(c.model_name, device=self.device, num_inference_steps=c.num_inference_steps,
                                       arch=c.arch or ZIMAGE_TURBO, vae_widths=c.vae_widths, vae_chunk=c.vae_chunk,
                                       weight_seed=c.weight_seed, synthetic_weights=c.synthetic_weights)
+        self._load_or_encode_prompts()
         n = attach_lora(self.es_model.transformer, c.lora_r, c.lora_alpha, c.lora_target_modules)
         if n == 0:
             raise RuntimeError("no LoRA target module matched")
@@ -480,20 +483,43 @@ class ZImageBackend(ESBackend):
         for m in lora_modules(self.es_model.transformer):
             m.reset_lora(g, b_std=c.lora_b_std)
         self.es_model.transformer.eval()
+        if c.use_vae_decoder_lora:
+            # es_backend.py:598-608: PEFT on the VAE decoder's mid-block attention linears; theta = the
+            # transformer's trainable params then the decoder's (collect_lora_params, es_backend.py:613-618)
+            vae = self.es_model.vae
+            if attach_lora(vae, c.vae_lora_r, c.vae_lora_alpha, c.vae_lora_target_modules) == 0:
+                raise RuntimeError("no VAE-decoder LoRA target module matched")
+            d_tr = sum(p.numel() for p in self.es_model.transformer.parameters() if p.requires_grad)
+            bind_theta_layout(vae, base=d_tr)
+            for m in lora_modules(vae):
+                m.reset_lora(g, b_std=c.lora_b_std)
 
     def collect_lora_params(self):
-        return get_trainable_params_and_shapes(self.es_model.transformer)
+        tr_params, tr_shapes = get_trainable_params_and_shapes(self.es_model.transformer)
+        if not self.cfg.use_vae_decoder_lora:
+            return tr_params, tr_shapes
+        vae_params, vae_shapes = get_trainable_params_and_shapes(self.es_model.vae)
+        return tr_params + vae_params, tr_shapes + vae_shapes
+
+    def _adapter_cfg(self, r, alpha, dropout, targets):
+        return {"peft_type": "LORA", "r": r, "lora_alpha": alpha, "lora_dropout": dropout,
+                "target_modules": list(targets), "base_model_name_or_path": self.cfg.model_name, "bias": "none",
+                "task_type": None}
 
     def save_lora(self, save_dir: Path) -> None:
-        """es_backend.py:611-619: the transformer adapter under save_dir/transformer."""
+        """es_backend.py:611-619: the transformer adapter under save_dir/transformer (+ vae_decoder/)."""
         c = self.cfg
         _save_adapter(self.es_model.transformer, Path(save_dir) / "transformer",
-                      {"peft_type": "LORA", "r": c.lora_r, "lora_alpha": c.lora_alpha, "lora_dropout": c.lora_dropout,
-                       "target_modules": list(c.lora_target_modules), "base_model_name_or_path": c.model_name,
-                       "bias": "none", "task_type": None})
+                      self._adapter_cfg(c.lora_r, c.lora_alpha, c.lora_dropout, c.lora_target_modules))
+        if c.use_vae_decoder_lora:
+            _save_adapter(self.es_model.vae, Path(save_dir) / "vae_decoder",
+                          self._adapter_cfg(c.vae_lora_r, c.vae_lora_alpha, c.vae_lora_dropout,
+                                            c.vae_lora_target_modules))
 
     def load_lora(self, save_dir: Path) -> None:
         _load_adapter(self.es_model.transformer, Path(save_dir) / "transformer")
+        if self.cfg.use_vae_decoder_lora:
+            _load_adapter(self.es_model.vae, Path(save_dir) / "vae_decoder")
 
     def _total_prompts(self) -> int:
         pe = self.base_prompt_embeds

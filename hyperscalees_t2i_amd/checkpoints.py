@@ -336,3 +336,110 @@ def save_sana_diffusers(transformer, vae, out_dir: Path) -> None:
     write_state_dir(out / "transformer", state_from_build(transformer, sana_rules(transformer)),
                     sana_config_from_arch(transformer.config))
     write_state_dir(out / "vae", state_from_build(vae, dcae_rules(vae)), dcae_config_from_build(vae))
+
+
+# ---------------------------------------------------------------------------------------
+# Z-Image-Turbo (BASELINE configs[3]): diffusers ZImageTransformer2DModel + FLUX AutoencoderKL
+# ---------------------------------------------------------------------------------------
+# Reference: ZImagePipeline.from_pretrained(model_name) (models/zImageTurbo.py:97-125).  zimage.py keeps
+# diffusers' module names (all_x_embedder."2-1", all_final_layer."2-1", noise_refiner / context_refiner /
+# layers .attention.to_q|to_k|to_v|to_out.0 / norm_q|norm_k, .feed_forward.w1|w2|w3, attention_norm1|2,
+# ffn_norm1|2, adaLN_modulation.0, t_embedder.mlp.0|2, cap_embedder.0|1, x_pad_token, cap_pad_token), so the
+# transformer maps key for key; flux_vae.py lists the decoder as conv_in / mid.0-2 / up_blocks.i.resnets.j /
+# up_blocks.i.upsample / conv_norm_out / conv_out, mapped to diffusers' decoder.* names below.  Like the Sana
+# loader, the key names follow the published diffusers modules and are UNPINNED here (no diffusers, no weights).
+
+ZIMAGE_CLASS = "ZImageTransformer2DModel"
+AUTOENCODER_KL_CLASS = "AutoencoderKL"
+
+
+def zimage_rules(model: nn.Module) -> List[Rule]:
+    return [_same(n) for n in _frozen_params(model)]
+
+
+def flux_vae_rules(vae: nn.Module) -> List[Rule]:
+    rules: List[Rule] = []
+    for n in _frozen_params(vae):
+        head, _, rest = n.partition(".")
+        if head == "mid":
+            i, _, leaf = rest.partition(".")
+            dn = {"0": "decoder.mid_block.resnets.0.", "2": "decoder.mid_block.resnets.1.",
+                  "1": "decoder.mid_block.attentions.0."}[i] + leaf
+        elif head == "up_blocks" and ".upsample." in n:
+            i = rest.split(".")[0]
+            dn = f"decoder.up_blocks.{i}.upsamplers.0.conv.{n.rsplit('.', 1)[1]}"
+        else:
+            dn = f"decoder.{n}"
+        rules.append(_same(n, dn))
+    return rules
+
+
+def zimage_arch_from_config(cfg: dict):
+    """diffusers ZImageTransformer2DModel config.json -> ZImageArch; refuses what zimage.py does not build."""
+    from .zimage import ZImageArch
+    if cfg.get("_class_name", ZIMAGE_CLASS) != ZIMAGE_CLASS:
+        raise NotImplementedError(f"transformer class {cfg.get('_class_name')!r} (expected {ZIMAGE_CLASS})")
+    ps, fps = list(cfg.get("all_patch_size", [2])), list(cfg.get("all_f_patch_size", [1]))
+    if len(ps) != 1 or len(fps) != 1 or int(fps[0]) != 1:
+        raise NotImplementedError(f"transformer config: patch sizes {ps} / {fps} (this build: one patch size, f 1)")
+    heads = int(cfg.get("n_heads", 30))
+    if int(cfg.get("n_kv_heads", heads)) != heads or not bool(cfg.get("qk_norm", True)):
+        raise NotImplementedError("transformer config: grouped kv heads / no qk_norm are not implemented")
+    dim = int(cfg.get("dim", 3840))
+    return ZImageArch(in_channels=int(cfg.get("in_channels", 16)), patch=int(ps[0]), dim=dim,
+                      n_layers=int(cfg.get("n_layers", 30)), n_refiner_layers=int(cfg.get("n_refiner_layers", 2)),
+                      n_heads=heads, ffn=int(dim / 3 * 8), norm_eps=float(cfg.get("norm_eps", 1e-5)),
+                      cap_feat_dim=int(cfg.get("cap_feat_dim", 2560)), adaln_dim=min(dim, 256),
+                      t_scale=float(cfg.get("t_scale", 1000.0)), rope_theta=float(cfg.get("rope_theta", 256.0)),
+                      axes_dims=tuple(int(x) for x in cfg.get("axes_dims", (32, 48, 48))))
+
+
+def zimage_config_from_arch(a) -> dict:
+    return {"_class_name": ZIMAGE_CLASS, "all_patch_size": [a.patch], "all_f_patch_size": [1],
+            "in_channels": a.in_channels, "dim": a.dim, "n_layers": a.n_layers, "n_refiner_layers": a.n_refiner_layers,
+            "n_heads": a.n_heads, "n_kv_heads": a.n_heads, "norm_eps": a.norm_eps, "qk_norm": True,
+            "cap_feat_dim": a.cap_feat_dim, "rope_theta": a.rope_theta, "t_scale": a.t_scale,
+            "axes_dims": list(a.axes_dims), "axes_lens": [1024, 512, 512]}
+
+
+def flux_vae_kwargs(cfg: dict) -> dict:
+    """diffusers AutoencoderKL config.json -> FluxVAEDecoder kwargs (decoder side)."""
+    if cfg.get("_class_name", AUTOENCODER_KL_CLASS) != AUTOENCODER_KL_CLASS:
+        raise NotImplementedError(f"vae class {cfg.get('_class_name')!r} (expected {AUTOENCODER_KL_CLASS})")
+    if cfg.get("use_post_quant_conv", False) or int(cfg.get("norm_num_groups", 32)) != 32 or \
+            cfg.get("act_fn", "silu") != "silu" or not cfg.get("mid_block_add_attention", True) or \
+            int(cfg.get("out_channels", 3)) != 3:
+        raise NotImplementedError("vae config: this build implements the FLUX AutoencoderKL decoder only (no post-quant "
+                                  "conv, GroupNorm(32), SiLU, mid-block attention, 3 output channels)")
+    return dict(latent_channels=int(cfg.get("latent_channels", 16)),
+                widths=tuple(int(w) for w in cfg.get("block_out_channels", (128, 256, 512, 512))),
+                layers=int(cfg.get("layers_per_block", 2)),
+                scaling_factor=float(cfg.get("scaling_factor", 0.3611)),
+                shift_factor=float(cfg.get("shift_factor", 0.1159) or 0.0))
+
+
+def flux_vae_config_from_build(vae: nn.Module) -> dict:
+    widths = [int(vae.conv_norm_out.weight.shape[0])] + [int(b.resnets[-1].conv2.weight.shape[0])
+                                                          for b in reversed(list(vae.up_blocks))][1:]
+    return {"_class_name": AUTOENCODER_KL_CLASS, "in_channels": 3, "out_channels": 3,
+            "latent_channels": int(vae.conv_in.weight.shape[1]), "block_out_channels": widths,
+            "layers_per_block": len(vae.up_blocks[0].resnets) - 1, "norm_num_groups": 32, "act_fn": "silu",
+            "scaling_factor": vae.scaling_factor, "shift_factor": vae.shift_factor, "use_quant_conv": False,
+            "use_post_quant_conv": False, "mid_block_add_attention": True}
+
+
+def load_zimage_transformer(model, d: Path) -> None:
+    load_into(model, zimage_rules(model), read_state_dir(d), f"{d} (transformer)")
+
+
+def load_flux_vae_decoder(vae, d: Path) -> None:
+    load_into(vae, flux_vae_rules(vae), read_state_dir(d), f"{d} (vae)",
+              ignore_prefixes=("encoder.", "quant_conv."))
+
+
+def save_zimage_diffusers(transformer, vae, out_dir: Path) -> None:
+    """The build's frozen Z-Image weights as a diffusers directory (transformer/ + vae/ decoder keys)."""
+    out = Path(out_dir)
+    write_state_dir(out / "transformer", state_from_build(transformer, zimage_rules(transformer)),
+                    zimage_config_from_arch(transformer.config))
+    write_state_dir(out / "vae", state_from_build(vae, flux_vae_rules(vae)), flux_vae_config_from_build(vae))

@@ -20,6 +20,7 @@ from torch import nn
 
 from . import kernels as K
 from .dcae import conv_gemm_px, nchw, nhwc
+from .lora import LoRALinear
 
 
 def _p(*shape):
@@ -81,19 +82,25 @@ class ResnetBlock(nn.Module):
 
 
 class MidAttention(nn.Module):
-    """diffusers Attention(c, heads=1, dim_head=c, norm=GroupNorm(32), residual) over the H*W tokens."""
+    """diffusers Attention(c, heads=1, dim_head=c, norm=GroupNorm(32), residual) over the H*W tokens.
+    to_q / to_k / to_v / to_out.0 are linears with diffusers' names (the Z-Image VAE-decoder LoRA targets,
+    es_backend.py:598-608, unifed_es.py:492): with LoRA attached and a population context they run the
+    population LoRA GEMM (kernel (2)); without LoRA, F.linear (hipBLASLt), as before."""
 
     def __init__(self, c: int):
         super().__init__()
         self.group_norm = GroupNorm(c)
-        self.to_q, self.to_k, self.to_v, self.to_out = (Conv(c, c, 1) for _ in range(4))
+        self.to_q, self.to_k, self.to_v = (LoRALinear(c, c, bias=True, lora=False) for _ in range(3))
+        self.to_out = nn.ModuleList([LoRALinear(c, c, bias=True, lora=False)])
+        for m in (self.to_q, self.to_k, self.to_v, self.to_out[0]):
+            m.lib_small_m = 1 << 62   # no LoRA: the vendor GEMM (these ran as F.linear 1x1 convs)
 
     def forward(self, x):
         B, H, W, C = x.shape
-        n = self.group_norm(x, silu=False)
+        n = self.group_norm(x, silu=False).reshape(B, H * W, C)
         q, k, v = (m(n).view(B, 1, H * W, C) for m in (self.to_q, self.to_k, self.to_v))
-        o = F.scaled_dot_product_attention(q, k, v, scale=C ** -0.5).view(B, H, W, C)
-        return self.to_out(o).add_(x)
+        o = F.scaled_dot_product_attention(q, k, v, scale=C ** -0.5).view(B, H * W, C)
+        return self.to_out[0](o).view(B, H, W, C).add_(x)
 
 
 class FluxVAEDecoder(nn.Module):
@@ -123,7 +130,7 @@ class FluxVAEDecoder(nn.Module):
             if p.ndim >= 2:
                 fan_in = p[0].numel()
                 std = 1.0 / math.sqrt(fan_in)
-                if name.endswith("conv2.weight") or name.endswith("to_out.weight"):
+                if name.endswith("conv2.weight") or name.endswith("to_out.0.weight"):
                     std *= 0.5
                 p.copy_(torch.randn(p.shape, generator=g, device=p.device) * std)
             elif name.endswith("weight"):

@@ -416,10 +416,12 @@ def lora_modules(model: nn.Module) -> List[LoRALinear]:
     return [m for m in model.modules() if isinstance(m, LoRALinear) and m.r]
 
 
-def bind_theta_layout(model: nn.Module) -> Dict[str, int]:
+def bind_theta_layout(model: nn.Module, base: int = 0) -> Dict[str, int]:
     """Record each LoRA module's (lora_A, lora_B) offsets inside theta, following the trainable
-    parameter order of model.parameters() (utills.py:141-152).  Returns {param_name: offset}."""
-    offs, off = {}, 0
+    parameter order of model.parameters() (utills.py:141-152).  base: where this model's parameters
+    start inside theta (a second LoRA'd model after the first, e.g. Z-Image's VAE decoder after its
+    transformer, es_backend.py:613-618).  Returns {param_name: offset}."""
+    offs, off = {}, int(base)
     by_param = {}
     for name, p in model.named_parameters():
         if p.requires_grad:

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from .flux_vae import FluxVAEDecoder
-from .lora import PopulationContext, set_population
+from .lora import PopulationContext, lora_modules, set_population
 from .pipeline import to_pil
 from .zimage import ZIMAGE_TURBO, ZImageArch, ZImageTransformer2DModel
 
@@ -46,21 +46,37 @@ class ZImageTurboES:
                  DTYPE: torch.dtype = torch.bfloat16, num_inference_steps: int = 9, arch: ZImageArch = ZIMAGE_TURBO,
                  vae_widths: Sequence[int] = (128, 256, 512, 512), vae_chunk: int = 16, weight_seed: int = 0,
                  synthetic_weights: bool = False):
-        if not synthetic_weights:
-            # the Sana host loads local diffusers directories (checkpoints.py); no Z-Image loader is built
-            raise FileNotFoundError(f"{model_name}: no local Z-Image-Turbo checkpoint loader in this build; "
-                                    "pass synthetic_weights=True for the throughput configuration")
+        from pathlib import Path
+
+        from . import checkpoints as ck
         self.model_name, self.device, self.DTYPE = model_name, device, torch.bfloat16
         self.num_inference_steps = int(num_inference_steps)
-        self.arch = arch
-        self.transformer = ZImageTransformer2DModel(arch).to(device)
-        self.transformer.init_weights(weight_seed)
-        self.vae = FluxVAEDecoder(widths=vae_widths).to(device)
-        self.vae.init_weights(weight_seed + 2)
+        if synthetic_weights:
+            self.arch = arch
+            self.transformer = ZImageTransformer2DModel(arch).to(device)
+            self.transformer.init_weights(weight_seed)
+            self.vae = FluxVAEDecoder(widths=vae_widths).to(device)
+            self.vae.init_weights(weight_seed + 2)
+            self.weights_source = "synthetic"
+        else:
+            # ZImagePipeline.from_pretrained(model_name) (models/zImageTurbo.py:97-125): a LOCAL diffusers
+            # directory (transformer/ + vae/, checkpoints.py); no hub access offline
+            root = Path(model_name)
+            if not (root / "transformer").is_dir() or not (root / "vae").is_dir():
+                raise FileNotFoundError(f"{model_name}: not a local diffusers Z-Image directory (transformer/ + vae/); "
+                                        "pass synthetic_weights=True for the throughput configuration")
+            self.arch = ck.zimage_arch_from_config(ck.read_config(root / "transformer"))
+            self.transformer = ZImageTransformer2DModel(self.arch).to(device)
+            ck.load_zimage_transformer(self.transformer, root / "transformer")
+            vk = ck.flux_vae_kwargs(ck.read_config(root / "vae"))
+            vae_widths = vk["widths"]
+            self.vae = FluxVAEDecoder(**vk).to(device)
+            ck.load_flux_vae_decoder(self.vae, root / "vae")
+            self.weights_source = str(root)
         self.vae_chunk = vae_chunk
         self.vae_scale_factor = 2 ** (len(vae_widths) - 1)
         self.ctx = PopulationContext()
-        self.weights_source = "synthetic"
+        self.vae_ctx = PopulationContext()   # theta rows of the decoding members when the VAE decoder has LoRA
 
     # ---- helpers --------------------------------------------------------------------
     def _check_hw_divisible(self, height_px: int, width_px: int):
@@ -100,7 +116,31 @@ class ZImageTurboES:
             v = self.transformer(x, t, capr, cap_lens, prompt_index, n_rep=n_rep)
             x = x + (sig[i + 1] - sig[i]) * (-v)
         z = x / self.vae.scaling_factor + self.vae.shift_factor
-        return torch.cat([self.vae(z[s:s + self.vae_chunk]) for s in range(0, z.shape[0], self.vae_chunk)])
+        if self.vae_ctx.theta_pop is None:
+            return torch.cat([self.vae(z[s:s + self.vae_chunk]) for s in range(0, z.shape[0], self.vae_chunk)])
+        # VAE-decoder LoRA on a population: every decode chunk holds whole members or a slice of one member,
+        # and the decoder's LoRA'd linears see exactly those members' theta rows
+        tp, b = self.vae_ctx.theta_pop, z.shape[0] // n_rep
+        out = []
+        if b <= self.vae_chunk:
+            per = max(1, self.vae_chunk // b)
+            for k0 in range(0, n_rep, per):
+                k1 = min(n_rep, k0 + per)
+                out.append(self._decode_members(z[k0 * b:k1 * b], tp[k0:k1]))
+        else:
+            for k in range(n_rep):
+                for s in range(0, b, self.vae_chunk):
+                    out.append(self._decode_members(z[k * b + s:k * b + min(b, s + self.vae_chunk)], tp[k:k + 1]))
+        return torch.cat(out)
+
+    def _decode_members(self, z: torch.Tensor, theta_rows: torch.Tensor) -> torch.Tensor:
+        sub = PopulationContext()
+        sub.theta_pop, sub.n_members = theta_rows, theta_rows.shape[0]
+        set_population(self.vae, sub)
+        try:
+            return self.vae(z)
+        finally:
+            set_population(self.vae, None)
 
     # ---- reference API (single member: the transformer's own LoRA params) ------------
     @torch.no_grad()
@@ -141,6 +181,8 @@ class ZImageTurboES:
         n = theta_pop.shape[0]
         self.ctx.theta_pop, self.ctx.n_members = theta_pop, n
         set_population(self.transformer, self.ctx)
+        if any(True for _ in lora_modules(self.vae)):
+            self.vae_ctx.theta_pop, self.vae_ctx.n_members = theta_pop, n
         try:
             cap, lens = self._captions(prompt_embeds)
             b = prompt_index.numel()
@@ -149,3 +191,4 @@ class ZImageTurboES:
         finally:
             set_population(self.transformer, None)
             self.ctx.theta_pop = None
+            self.vae_ctx.theta_pop = None

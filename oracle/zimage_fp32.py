@@ -103,8 +103,9 @@ def transformer_fp32(tr, lat, t, cap_feats, cap_lens, enc_index, theta_k, record
     return tr.unpatchify(out, H, W)
 
 
-def vae_fp32(vae, z):
-    """flux_vae.FluxVAEDecoder in fp32 (NCHW, torch.group_norm)."""
+def vae_fp32(vae, z, theta_k=None):
+    """flux_vae.FluxVAEDecoder in fp32 (NCHW, torch.group_norm); theta_k: member k's theta when the decoder
+    carries the VAE LoRA (mid-block to_q / to_k / to_v / to_out.0, PEFT formula)."""
     def conv(m, x):
         return F.conv2d(x, _w(m.weight), _w(m.bias), padding=m.ks // 2)
 
@@ -118,10 +119,10 @@ def vae_fp32(vae, z):
 
     def attn(m, x):
         B, C, H, W = x.shape
-        n = gn(m.group_norm, x, silu=False)
-        q, k, v = (conv(mm, n).flatten(2).transpose(1, 2)[:, None] for mm in (m.to_q, m.to_k, m.to_v))
-        o = F.scaled_dot_product_attention(q, k, v, scale=C ** -0.5)[:, 0].transpose(1, 2).view(B, C, H, W)
-        return conv(m.to_out, o) + x
+        n = gn(m.group_norm, x, silu=False).flatten(2).transpose(1, 2)                  # [B, HW, C]
+        q, k, v = (LoraLinear32(mm, theta_k)(n)[:, None] for mm in (m.to_q, m.to_k, m.to_v))
+        o = F.scaled_dot_product_attention(q, k, v, scale=C ** -0.5)[:, 0]
+        return LoraLinear32(m.to_out[0], theta_k)(o).transpose(1, 2).reshape(B, C, H, W) + x
 
     x = conv(vae.conv_in, z.to(f32))
     x = attn(vae.mid[1], res(vae.mid[0], x))
@@ -134,7 +135,8 @@ def vae_fp32(vae, z):
     return conv(vae.conv_out, gn(vae.conv_norm_out, x))
 
 
-def generate_fp32(model, theta_k, embeds, prompt_index, seed, width_px, height_px, steps, record=None):
+def generate_fp32(model, theta_k, embeds, prompt_index, seed, width_px, height_px, steps, record=None,
+                  vae_lora: bool = False):
     """One member's images: the build's ZImageTurboES inputs (distinct prompt embeddings, image ->
     prompt index, per-image seeded latents, flow_sigmas) through the fp32 transformer and VAE."""
     from hyperscalees_t2i_amd.zimage_pipeline import flow_sigmas
@@ -149,4 +151,4 @@ def generate_fp32(model, theta_k, embeds, prompt_index, seed, width_px, height_p
         vel.append(v)
         x = x + (sig[i + 1] - sig[i]) * (-v)
     z = x / model.vae.scaling_factor + model.vae.shift_factor
-    return vel, vae_fp32(model.vae, z)
+    return vel, vae_fp32(model.vae, z, theta_k if vae_lora else None)

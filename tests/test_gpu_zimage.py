@@ -108,6 +108,94 @@ def test_engine_step_rank4_matches_oracle(setup, dev):
     assert np.isfinite(st["summary/mean_reward"])
 
 
+@pytest.fixture(scope="module")
+def setup_vae_lora(dev):
+    """use_vae_decoder_lora=True (es_backend.py:598-608): the decoder's mid-block to_q / to_k / to_v / to_out.0
+    carry LoRA too; theta = transformer LoRA then decoder LoRA."""
+    cfg = ZImageConfig(synthetic_weights=True, arch=TINY, vae_widths=(32, 32, 64, 64), width_px=PX, height_px=PX,
+                       num_inference_steps=3, batches_per_gen=2, synthetic_prompt_lens=(20, 70),
+                       use_vae_decoder_lora=True, vae_chunk=4)
+    be = ZImageBackend(str(dev), cfg)
+    be.init_and_attach_lora()
+    params, shapes = be.collect_lora_params()
+    return be, params, shapes
+
+
+def test_vae_decoder_lora_population_vs_single_member_and_fp32(setup_vae_lora, dev):
+    """Population decode (each chunk's members' theta rows on the decoder's LoRA'd linears; vae_chunk 4 < the
+    8 images per member, so members span several chunks) vs one member at a time with its own LoRA params,
+    and vs the fp32 restatement with the decoder LoRA from theta_k; the decoder LoRA really changes the
+    images (members differing only in their decoder LoRA decode differently)."""
+    from oracle import zimage_fp32 as Z
+    be, params, shapes = setup_vae_lora
+    theta0 = flatten_params(params).to(dev)
+    d_tr = sum(int(np.prod(s)) for s in shapes[:-8])
+    noiser = EggRollNoiser(shapes, sigma=5e-2, lr_scale=0.1, rank=4, use_antithetic=True)
+    pop = 2
+    tp = noiser.perturb(theta0, noiser.epoch_noise(pop, seed=7), pop, 0, pop)
+    info = be.step_sampling_info(2)
+    flat = info["flat_ids"]
+    B = len(flat)
+    imgs = be.generate_population(flat, 2, 0.0, tp).float()
+    uniq = list(dict.fromkeys(flat))
+    idx = torch.tensor([uniq.index(f) for f in flat], device=dev)
+    embeds = [be._dev_prompts[p] for p in uniq]
+    worst = 0.0
+    for k in range(pop):
+        unflatten_to_params(tp[k], params, shapes)
+        one, _ = be.es_model.generate_one_batch([be._dev_prompts[p] for p in flat], seed=2, width_px=PX, height_px=PX,
+                                                num_inference_steps=3, output_type="pt")
+        a = imgs[k * B:(k + 1) * B]
+        assert ((a - one.float()).norm() / one.float().norm()).item() < 3e-2
+        _, img32 = Z.generate_fp32(be.es_model, tp[k], embeds, idx, 2, PX, PX, 3, vae_lora=True)
+        worst = max(worst, ((a - img32).norm() / img32.norm()).item())
+    unflatten_to_params(theta0, params, shapes)
+    print("[zimage-vae-lora] image rel vs fp32", worst)
+    assert worst < 0.02, worst
+    # only the decoder LoRA differs between two members -> different images
+    tp2 = theta0[None].repeat(2, 1)
+    tp2[1, d_tr:] += 0.5 * torch.randn(tp2.shape[1] - d_tr, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
+    two = be.generate_population(flat, 2, 0.0, tp2).float()
+    assert (two[:B] - two[B:]).abs().max().item() > 1e-3
+
+
+def test_vae_decoder_lora_engine_step_matches_oracle(setup_vae_lora, dev):
+    be, params, shapes = setup_vae_lora
+    rewards = RewardModels.build(dev, tiny=True, synthetic=True)
+    theta = flatten_params(params).to(dev)
+    pop = 4
+    noiser = EggRollNoiser(shapes, sigma=1e-2, lr_scale=1e-1, rank=4, use_antithetic=True)
+    eng = ESEngine(be, rewards, noiser, ESConfig(pop_size=pop, egg_rank=4, promptnorm=True, theta_max_norm=40.0), dev)
+    new, st = eng.step(theta, seed=3, guidance_scale=0.0)
+    eps = noiser.eps_from_factors(noiser.sample_factors(pop, dev, seed=3), pop).cpu().numpy()
+    ref, info = O.ref_es_tail(st["_S"].numpy(), eps, theta.cpu().numpy(), promptnorm=True, lr_scale=1e-1,
+                              sigma=1e-2, max_step_norm=0.0, theta_max_norm=40.0)
+    np.testing.assert_allclose(new.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
+    assert not np.array_equal(new.cpu().numpy()[-8 * 64:], theta.cpu().numpy()[-8 * 64:])   # decoder LoRA updated
+
+
+def test_loaded_zimage_generates_identically(dev, tmp_path):
+    """A synthetic Z-Image exported as a diffusers directory (checkpoints.save_zimage_diffusers) and loaded
+    back through ZImageConfig(model_name=dir) gives a bit-identical population member-eval."""
+    from hyperscalees_t2i_amd import checkpoints as C
+    arch = ZImageArch(dim=384, n_layers=2, n_refiner_layers=1, n_heads=3, ffn=1024, cap_feat_dim=256, t_mid=1024)
+    # 128 px: 8 x 8 = 64 image tokens, a multiple of diffusers' fixed seq_multiple 32 (not in the config)
+    kw = dict(width_px=128, height_px=128, num_inference_steps=2, batches_per_gen=2, synthetic_prompt_lens=(20, 70))
+    a = ZImageBackend(str(dev), ZImageConfig(synthetic_weights=True, arch=arch, vae_widths=(32, 32, 64, 64), **kw))
+    a.init_and_attach_lora()
+    C.save_zimage_diffusers(a.es_model.transformer, a.es_model.vae, tmp_path)
+    b = ZImageBackend(str(dev), ZImageConfig(model_name=str(tmp_path), **kw))
+    b.init_and_attach_lora()
+    pa, sa = a.collect_lora_params()
+    pb, sb = b.collect_lora_params()
+    assert sa == sb
+    theta = flatten_params(pa).to(dev)
+    noiser = EggRollNoiser(sa, sigma=5e-2, lr_scale=0.1, rank=4, use_antithetic=True)
+    tp = noiser.perturb(theta, noiser.epoch_noise(2, seed=1), 2, 0, 2)
+    flat = a.step_sampling_info(1)["flat_ids"]
+    assert torch.equal(a.generate_population(flat, 1, 0.0, tp), b.generate_population(flat, 1, 0.0, tp))
+
+
 def test_lora_linear_row_chunks_match_one_launch(dev, monkeypatch):
     """X beyond the GEMMs' 2 GiB operand runs in whole-member row chunks (LoRALinear._forward_chunked):
     with the limit lowered, the chunked population forward equals the one-launch forward, for the plain,
