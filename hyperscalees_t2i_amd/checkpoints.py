@@ -443,3 +443,189 @@ def save_zimage_diffusers(transformer, vae, out_dir: Path) -> None:
     write_state_dir(out / "transformer", state_from_build(transformer, zimage_rules(transformer)),
                     zimage_config_from_arch(transformer.config))
     write_state_dir(out / "vae", state_from_build(vae, flux_vae_rules(vae)), flux_vae_config_from_build(vae))
+
+
+# ---------------------------------------------------------------------------------------
+# Infinity (BASELINE configs[4]): the Infinity repo's state dicts
+# ---------------------------------------------------------------------------------------
+# Reference: InfinityES._load_infinity (models/Infinity.py:183-235) builds `Infinity(...)` and loads
+# checkpoint_type "torch" (one .pth: torch.load + load_state_dict) or "torch_shard" (a directory with an
+# index, transformers.load_sharded_checkpoint(strict=False)); the BSQ-VAE comes from vae_path (a .pth).
+# infinity.py keeps the repo's module names where it can (block_chunks.i.module.j.{sa,ca,ffn,ca_norm,ada_gss},
+# shared_ada_lin.1, head_nm.ada_lin.1, head, word_embed, text_norm, text_proj_for_ca.0|2, cfg_uncond, pos_start)
+# and folds the repo's separate bias vectors into its linears' biases:
+#   sa.q_bias, sa.v_bias (+ the zero_k_bias buffer)        -> sa.mat_qkv.bias = [q_bias | 0 | v_bias]
+#   ca.v_bias (+ zero_k_bias)                              -> ca.mat_kv.bias  = [0 | v_bias]
+#   sa.scale_mul_1H11 [1, 1, H, 1] (flash) or [1, H, 1, 1] -> [1, H, 1, 1]
+#   lvl_embed.weight (nn.Embedding)                        -> lvl_embed
+#   text_proj_for_sos.ca.{mat_q [1, 1, C], mat_kv.weight, v_bias, proj.*} -> text_proj_for_sos.{query, mat_kv, proj}
+# The BSQ-VAE decoder follows the LDM / FLUX autoencoder naming (decoder.conv_in, decoder.mid.block_1 / attn_1 /
+# block_2, decoder.up.L.block.j.{norm1,conv1,norm2,conv2,nin_shortcut}, decoder.up.L.upsample.conv with L = 0
+# the full-resolution level, decoder.norm_out, decoder.conv_out; 1x1-conv q / k / v / proj_out).  The Infinity
+# repo is not vendored: these names are UNPINNED against real files; the loader is strict (the reference's
+# shard path is strict=False — here a missing or unused tensor raises rather than leaving random weights).
+
+INFINITY_SHARD_INDEX = ("pytorch_model.bin.index.json", "model.safetensors.index.json")
+# persistent buffers of the Infinity modules that carry no learned value in this build
+INFINITY_BUFFER_SUFFIXES = ("zero_k_bias", "lvl_1L", "attn_bias_for_masking")
+
+
+def _fold_bias(name: str, keys: List[str], layout: str, C: int) -> Rule:
+    """layout "q0v": [q | 0 | v] from (q_bias, v_bias); "0v": [0 | v] from (v_bias,)."""
+    if layout == "q0v":
+        return (name, keys, lambda ts: torch.cat([ts[0], torch.zeros_like(ts[0]), ts[1]]),
+                lambda t: [t[:C], t[2 * C:]])
+    return (name, keys, lambda ts: torch.cat([torch.zeros_like(ts[0]), ts[0]]), lambda t: [t[C:]])
+
+
+def infinity_rules(model: nn.Module) -> List[Rule]:
+    C = model.arch.C
+    H = model.arch.num_heads
+    rules: List[Rule] = []
+    for n in _frozen_params(model):
+        if n.endswith(".sa.mat_qkv.bias"):
+            p = n[: -len(".mat_qkv.bias")]
+            rules.append(_fold_bias(n, [f"{p}.q_bias", f"{p}.v_bias"], "q0v", C))
+        elif n.endswith(".ca.mat_kv.bias"):
+            p = n[: -len(".mat_kv.bias")]
+            rules.append(_fold_bias(n, [f"{p}.v_bias"], "0v", C))
+        elif n.endswith(".sa.scale_mul_1H11"):
+            rules.append((n, [n], lambda ts: ts[0].reshape(1, H, 1, 1), lambda t: [t.reshape(1, H, 1, 1)]))
+        elif n == "lvl_embed":
+            rules.append(_same(n, "lvl_embed.weight"))
+        elif n == "text_proj_for_sos.query":
+            rules.append((n, ["text_proj_for_sos.ca.mat_q"], lambda ts: ts[0].reshape(-1),
+                          lambda t: [t.reshape(1, 1, -1)]))
+        elif n == "text_proj_for_sos.mat_kv.bias":
+            rules.append(_fold_bias(n, ["text_proj_for_sos.ca.v_bias"], "0v", C))
+        elif n.startswith("text_proj_for_sos."):
+            rules.append(_same(n, "text_proj_for_sos.ca." + n[len("text_proj_for_sos."):]))
+        else:
+            rules.append(_same(n))
+    return rules
+
+
+def bsq_vae_rules(vae: nn.Module) -> List[Rule]:
+    """FluxVAEDecoder (up_blocks listed lowest resolution first) <- LDM decoder keys (up.L, L = 0 the full
+    resolution level)."""
+    n_up = len(vae.up_blocks)
+    rules: List[Rule] = []
+    for n in _frozen_params(vae):
+        parts = n.split(".")
+        if parts[0] == "mid":
+            sub = {"0": "block_1", "1": "attn_1", "2": "block_2"}[parts[1]]
+            leaf = ".".join(parts[2:])
+            if sub == "attn_1":
+                lin, _, wb = leaf.rpartition(".")
+                if lin in ("to_q", "to_k", "to_v", "to_out.0"):
+                    dk = f"decoder.mid.attn_1.{ {'to_q': 'q', 'to_k': 'k', 'to_v': 'v', 'to_out.0': 'proj_out'}[lin] }.{wb}"
+                    rules.append(_conv1x1(n, dk) if wb == "weight" else _same(n, dk))
+                    continue
+                leaf = leaf.replace("group_norm", "norm")
+            rules.append(_same(n, f"decoder.mid.{sub}.{leaf}"))
+        elif parts[0] == "up_blocks":
+            lvl = n_up - 1 - int(parts[1])
+            if parts[2] == "upsample":
+                rules.append(_same(n, f"decoder.up.{lvl}.upsample.conv.{parts[3]}"))
+            else:   # resnets.j.<m>.<w|b>
+                m = "nin_shortcut" if parts[4] == "conv_shortcut" else parts[4]
+                rules.append(_same(n, f"decoder.up.{lvl}.block.{parts[3]}.{m}.{parts[5]}"))
+        elif parts[0] == "conv_norm_out":
+            rules.append(_same(n, f"decoder.norm_out.{parts[1]}"))
+        else:
+            rules.append(_same(n, f"decoder.{n}"))
+    return rules
+
+
+def _torch_state(path: Path) -> Dict[str, torch.Tensor]:
+    """A torch-saved state dict, loaded with weights_only=True (no code from the file runs); a dict whose
+    tensors sit under one of the usual wrapper keys is unwrapped."""
+    sd = torch.load(str(path), map_location="cpu", weights_only=True)
+    for k in ("state_dict", "model", "vae", "module"):
+        if isinstance(sd, dict) and k in sd and isinstance(sd[k], dict) and not torch.is_tensor(sd[k]):
+            sd = sd[k]
+            break
+    if not isinstance(sd, dict) or not all(torch.is_tensor(v) for v in sd.values()):
+        raise ValueError(f"{path}: not a state dict of tensors")
+    return dict(sd)
+
+
+def read_infinity_state(model_path: Path, checkpoint_type: str) -> Dict[str, torch.Tensor]:
+    """checkpoint_type "torch": one .pth file; "torch_shard": a directory with pytorch_model.bin.index.json
+    (or model.safetensors.index.json) naming its shards."""
+    p = Path(model_path)
+    if checkpoint_type == "torch":
+        if not p.is_file():
+            raise FileNotFoundError(f"{p}: Infinity checkpoint file not found")
+        return _torch_state(p)
+    if checkpoint_type != "torch_shard":
+        raise ValueError(f"checkpoint_type must be 'torch' or 'torch_shard', got {checkpoint_type}")
+    idx = next((p / n for n in INFINITY_SHARD_INDEX if (p / n).is_file()), None) if p.is_dir() else None
+    if idx is None:
+        raise FileNotFoundError(f"{p}: no shard index ({' / '.join(INFINITY_SHARD_INDEX)})")
+    wmap = json.loads(idx.read_text())["weight_map"]
+    out: Dict[str, torch.Tensor] = {}
+    for shard in sorted(set(wmap.values())):
+        if shard.endswith(".safetensors"):
+            from safetensors.torch import load_file
+            out.update(load_file(str(p / shard)))
+        else:
+            out.update(_torch_state(p / shard))
+    missing = set(wmap) - set(out)
+    if missing:
+        raise ValueError(f"{p}: index names tensors absent from its shards: {sorted(missing)[:3]}")
+    return out
+
+
+def _strip_buffers(state: Dict[str, torch.Tensor], what: str) -> Dict[str, torch.Tensor]:
+    out = {}
+    for k, v in state.items():
+        if k.endswith(INFINITY_BUFFER_SUFFIXES):
+            if k.endswith("zero_k_bias") and bool(v.float().abs().max() > 0):
+                raise ValueError(f"{what}: {k} is not zero (the build folds a zero k bias)")
+            continue
+        out[k] = v
+    return out
+
+
+def load_infinity_transformer(model, model_path: Path, checkpoint_type: str) -> None:
+    what = f"{model_path} (Infinity)"
+    load_into(model, infinity_rules(model), _strip_buffers(read_infinity_state(model_path, checkpoint_type), what),
+              what, ignore_prefixes=("vae_local.",))
+
+
+def load_bsq_vae_decoder(vae, vae_path: Path) -> None:
+    p = Path(vae_path)
+    if not p.is_file():
+        raise FileNotFoundError(f"{p}: BSQ-VAE checkpoint not found")
+    load_into(vae, bsq_vae_rules(vae), _torch_state(p), f"{p} (vae)",
+              ignore_prefixes=("encoder.", "quantizer.", "quantize.", "quant_conv.", "post_quant_conv."))
+
+
+def save_infinity_checkpoint(model, vae, model_path: Path, vae_path: Path, shards: int = 0) -> None:
+    """The build's frozen Infinity weights in the repo's layout (zero_k_bias buffers included): one .pth
+    (shards 0) or a shard directory with pytorch_model.bin.index.json; the VAE decoder as a .pth."""
+    st = state_from_build(model, infinity_rules(model))
+    C = model.arch.C
+    for blk in [f"block_chunks.{i}.module.{j}" for i, ch in enumerate(model.block_chunks) for j in range(len(ch.module))]:
+        st[f"{blk}.sa.zero_k_bias"] = torch.zeros(C, dtype=torch.bfloat16)
+        st[f"{blk}.ca.zero_k_bias"] = torch.zeros(C, dtype=torch.bfloat16)
+    st["text_proj_for_sos.ca.zero_k_bias"] = torch.zeros(C, dtype=torch.bfloat16)
+    st = {k: v.detach().cpu().contiguous() for k, v in st.items()}
+    mp = Path(model_path)
+    if shards <= 0:
+        mp.parent.mkdir(parents=True, exist_ok=True)
+        torch.save(st, str(mp))
+    else:
+        mp.mkdir(parents=True, exist_ok=True)
+        keys = sorted(st)
+        wmap = {}
+        for s in range(shards):
+            part = {k: st[k] for k in keys[s::shards]}
+            fn = f"pytorch_model-{s + 1:05d}-of-{shards:05d}.bin"
+            torch.save(part, str(mp / fn))
+            wmap.update({k: fn for k in part})
+        (mp / INFINITY_SHARD_INDEX[0]).write_text(json.dumps({"metadata": {}, "weight_map": wmap}, indent=1))
+    vp = Path(vae_path)
+    vp.parent.mkdir(parents=True, exist_ok=True)
+    torch.save({k: v.detach().cpu().contiguous() for k, v in state_from_build(vae, bsq_vae_rules(vae)).items()}, str(vp))

@@ -87,23 +87,26 @@ class InfinityES:
                                                    int(text_channels))
         if arch is None and checkpoint_type not in ("torch", "torch_shard"):
             raise ValueError(f"checkpoint_type must be 'torch' or 'torch_shard', got {checkpoint_type}")
-        if not synthetic_weights:
-            # models/Infinity.py:183-235 load the Infinity repo's module from a .pth / shard directory; that
-            # repo is not vendored, so there is no module tree to load it into
-            raise FileNotFoundError(f"{model_path}: no Infinity checkpoint loader in this build (the Infinity repo is "
-                                    "not vendored); pass synthetic_weights=True for the throughput configuration")
         self.arch = a
         self.vae_type = int(vae_type)
         self.text_tokenizer = self.text_encoder = None
         self.infinity = InfinityTransformer(a).to(device)
-        self.infinity.init_weights(weight_seed)
-        self.transformer = self.infinity
         self.vae = infinity_vae(a).to(device)
-        self.vae.init_weights(weight_seed + 2)
+        if synthetic_weights:
+            self.infinity.init_weights(weight_seed)
+            self.vae.init_weights(weight_seed + 2)
+            self.weights_source = "synthetic"
+        else:
+            # models/Infinity.py:183-235: the Infinity repo's state dict (.pth, or a shard directory with its
+            # index) and the BSQ-VAE .pth, strict (checkpoints.load_infinity_transformer / load_bsq_vae_decoder)
+            from . import checkpoints as ck
+            ck.load_infinity_transformer(self.infinity, Path(model_path), checkpoint_type)
+            ck.load_bsq_vae_decoder(self.vae, Path(vae_path))
+            self.weights_source = str(model_path)
+        self.transformer = self.infinity
         self.vae_chunk = int(vae_chunk)
         self.kv_budget = float(kv_budget_gb) * 2 ** 30
         self.ctx = PopulationContext()
-        self.weights_source = "synthetic"
 
     # ---- prompt cache (models/Infinity.py:257-349) ---------------------------------------
     def encode_prompts(self, prompts_txt_path, encoded_save_path, batch_size: int = 8, complex_human_instruction=None,

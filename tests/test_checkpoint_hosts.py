@@ -147,3 +147,107 @@ def test_zimage_vae_decoder_lora_theta_layout():
     mods = lora_modules(be.es_model.vae)
     assert [m.theta_off_A for m in mods] == [d_tr + i * 4 * Cv for i in range(4)]
     assert [m.theta_off_B for m in mods] == [d_tr + i * 4 * Cv + 2 * Cv for i in range(4)]
+
+
+# ---------------------------------------------------------------------------------------------- Infinity
+from hyperscalees_t2i_amd.infinity import InfinityArch, InfinityTransformer, infinity_vae  # noqa: E402
+
+ITINY = InfinityArch(depth=2, embed_dim=256, num_heads=2, block_chunks=2, text_channels=256, codebook_dim=4,
+                     spatial_patchify=1, vae_widths=(32, 32, 64, 64))
+
+
+@pytest.fixture(scope="module")
+def isaved(tmp_path_factory):
+    d = tmp_path_factory.mktemp("infinity_local")
+    tr = InfinityTransformer(ITINY)
+    tr.init_weights(3)
+    with torch.no_grad():   # nonzero biases everywhere, so the q | 0 | v folding is exercised
+        for blk in tr.blocks():
+            blk.sa.mat_qkv.bias.normal_()
+            blk.sa.mat_qkv.bias[256:512].zero_()
+            blk.ca.mat_kv.bias.normal_()
+            blk.ca.mat_kv.bias[:256].zero_()
+        tr.text_proj_for_sos.mat_kv.bias.normal_()
+        tr.text_proj_for_sos.mat_kv.bias[:256].zero_()
+    vae = infinity_vae(ITINY)
+    vae.init_weights(4)
+    C.save_infinity_checkpoint(tr, vae, d / "infinity.pth", d / "vae.pth")
+    C.save_infinity_checkpoint(tr, vae, d / "shards", d / "vae2.pth", shards=3)
+    return d, tr, vae
+
+
+def test_infinity_repo_layout(isaved):
+    d, _, _ = isaved
+    st = torch.load(str(d / "infinity.pth"), weights_only=True)
+    Cd = ITINY.C
+    for k, sh in {"block_chunks.1.module.0.sa.mat_qkv.weight": (3 * Cd, Cd), "block_chunks.0.module.0.sa.q_bias": (Cd,),
+                  "block_chunks.0.module.0.sa.v_bias": (Cd,), "block_chunks.0.module.0.sa.zero_k_bias": (Cd,),
+                  "block_chunks.0.module.0.ca.v_bias": (Cd,), "block_chunks.0.module.0.ffn.fc1.weight": (1024, Cd),
+                  "block_chunks.0.module.0.ada_gss": (1, 1, 6, Cd), "lvl_embed.weight": (15, Cd),
+                  "text_proj_for_sos.ca.mat_q": (1, 1, Cd), "text_proj_for_sos.ca.mat_kv.weight": (2 * Cd, 256),
+                  "shared_ada_lin.1.weight": (6 * Cd, Cd), "head_nm.ada_lin.1.weight": (2 * Cd, Cd)}.items():
+        assert tuple(st[k].shape) == sh, k
+    assert "block_chunks.0.module.0.sa.mat_qkv.bias" not in st and "block_chunks.0.module.0.ca.mat_kv.bias" not in st
+    sv = torch.load(str(d / "vae.pth"), weights_only=True)
+    for k, sh in {"decoder.mid.attn_1.q.weight": (64, 64, 1, 1), "decoder.mid.attn_1.norm.weight": (64,),
+                  "decoder.up.0.block.0.conv1.weight": (32, 32, 3, 3), "decoder.up.3.upsample.conv.weight": (64, 64, 3, 3),
+                  "decoder.up.1.block.0.nin_shortcut.weight": (32, 64, 1, 1), "decoder.norm_out.bias": (32,)}.items():
+        assert tuple(sv[k].shape) == sh, k
+    assert not any(k.startswith("decoder.up.0.upsample") for k in sv)
+
+
+@pytest.mark.parametrize("kind", ["torch", "torch_shard"])
+def test_infinity_roundtrip_bitexact(isaved, kind):
+    d, tr, vae = isaved
+    tr2 = InfinityTransformer(ITINY)
+    C.load_infinity_transformer(tr2, d / ("infinity.pth" if kind == "torch" else "shards"), kind)
+    a, b = _frozen(tr), _frozen(tr2)
+    assert list(a) == list(b) and all(torch.equal(a[n], b[n]) for n in a)
+    vae2 = infinity_vae(ITINY)
+    C.load_bsq_vae_decoder(vae2, d / "vae.pth")
+    assert all(torch.equal(x, y) for x, y in zip(_frozen(vae).values(), _frozen(vae2).values()))
+
+
+def test_infinity_loader_is_strict(isaved, tmp_path):
+    d, _, _ = isaved
+    st = torch.load(str(d / "infinity.pth"), weights_only=True)
+    H = ITINY.num_heads
+    cases = ((lambda s: s.pop("block_chunks.1.module.0.ffn.fc2.bias"), ValueError, "lacks"),
+             (lambda s: s.__setitem__("block_chunks.0.module.0.extra", torch.zeros(1)), ValueError, "not used"),
+             (lambda s: s.__setitem__("head.weight", torch.zeros(3, 256)), ValueError, "gives"),
+             (lambda s: s.__setitem__("block_chunks.0.module.0.sa.zero_k_bias", torch.ones(256)), ValueError, "not zero"))
+    for mutate, exc, match in cases:
+        s = dict(st)
+        mutate(s)
+        torch.save(s, str(tmp_path / "m.pth"))
+        with pytest.raises(exc, match=match):
+            C.load_infinity_transformer(InfinityTransformer(ITINY), tmp_path / "m.pth", "torch")
+    # the flash-attention form of scale_mul_1H11 ([1, 1, H, 1]) and wrapped / buffer-carrying dicts load
+    s = dict(st)
+    for k in [k for k in s if k.endswith("scale_mul_1H11")]:
+        s[k] = s[k].reshape(1, 1, H, 1)
+    s["lvl_1L"] = torch.zeros(1, 10)
+    torch.save({"state_dict": s}, str(tmp_path / "w.pth"))
+    C.load_infinity_transformer(InfinityTransformer(ITINY), tmp_path / "w.pth", "torch")
+    with pytest.raises(FileNotFoundError):
+        C.load_infinity_transformer(InfinityTransformer(ITINY), tmp_path / "missing.pth", "torch")
+    with pytest.raises(FileNotFoundError):
+        C.load_infinity_transformer(InfinityTransformer(ITINY), tmp_path, "torch_shard")
+    with pytest.raises(ValueError):
+        C.read_infinity_state(tmp_path / "w.pth", "safetensors")
+
+
+def test_infinity_backend_loads_local_files(isaved, tmp_path):
+    from hyperscalees_t2i_amd.backend import InfinityBackend, InfinityConfig
+    d, tr, vae = isaved
+    bad = InfinityBackend("cpu", InfinityConfig(arch=ITINY, model_path=str(tmp_path / "none.pth"), checkpoint_type="torch",
+                                                vae_path=str(d / "vae.pth"), pn="0.06M", synthetic_prompt_lens=(5, 9)))
+    with pytest.raises(FileNotFoundError):
+        bad.init_and_attach_lora()
+    be = InfinityBackend("cpu", InfinityConfig(arch=ITINY, model_path=str(d / "shards"), checkpoint_type="torch_shard",
+                                               vae_path=str(d / "vae.pth"), pn="0.06M", synthetic_prompt_lens=(5, 9)))
+    be.init_and_attach_lora()
+    m = be.es_model
+    assert m.weights_source == str(d / "shards")
+    assert all(torch.equal(x, y) for x, y in zip(_frozen(tr).values(), _frozen(m.transformer).values()))
+    assert all(torch.equal(x, y) for x, y in zip(_frozen(vae).values(), _frozen(m.vae).values()))

@@ -183,3 +183,27 @@ def test_qk_norm_rope_kv_cache_append(dev):
     assert tol(x[:, :C], ref_q)
     assert tol(cache, ref_cache)
     assert torch.equal(cache[:, :, :row0], ref_cache[:, :, :row0]) and torch.equal(cache[1], ref_cache[1])
+
+
+def test_loaded_infinity_generates_identically(setup, dev, tmp_path):
+    """The synthetic model exported in the Infinity repo's layout (checkpoints.save_infinity_checkpoint: a shard
+    directory + the BSQ-VAE .pth) and loaded back through InfinityConfig(model_path=..., checkpoint_type=
+    "torch_shard", vae_path=...) gives bit-identical sampled bits and images for a population pass."""
+    from hyperscalees_t2i_amd import checkpoints as C
+    be, params, shapes = setup
+    C.save_infinity_checkpoint(be.es_model.transformer, be.es_model.vae, tmp_path / "shards", tmp_path / "vae.pth",
+                               shards=2)
+    cfg = InfinityConfig(arch=TINY, pn="0.06M", batches_per_gen=2, micro_batch=0, synthetic_prompt_lens=(5, 40),
+                         vae_chunk=8, model_path=str(tmp_path / "shards"), checkpoint_type="torch_shard",
+                         vae_path=str(tmp_path / "vae.pth"))
+    be2 = InfinityBackend(str(dev), cfg)
+    be2.init_and_attach_lora()
+    p2, s2 = be2.collect_lora_params()
+    assert [tuple(s) for s in s2] == [tuple(s) for s in shapes]
+    theta = flatten_params(params).to(dev)
+    noiser = EggRollNoiser(shapes, sigma=5e-2, lr_scale=0.1, rank=1, use_antithetic=True)
+    tp = noiser.perturb(theta, noiser.epoch_noise(2, seed=4), 2, 0, 2)
+    flat = be.step_sampling_info(1)["flat_ids"]
+    a = be.generate_population(flat, 1, be.cfg.guidance_scale, tp)
+    b = be2.generate_population(flat, 1, be2.cfg.guidance_scale, tp)
+    assert torch.equal(a, b)
