@@ -34,15 +34,13 @@ __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcp
 // previous kernel (8-channel threads, weights and every tap re-read from LDS, bf16->fp32 per use)
 // ran the Sana FFN shape at 1.4 TB/s, VALU-bound on conversions.
 // HBM traffic: input ~(TH+KS-1)/TH (halo rows, mostly L2 hits), output one write.
-#ifndef EGG_DW5_WIN
-#define EGG_DW5_WIN 0   // measured 11 % slower at 8x128x128x1536 (2 vs 3 waves per SIMD; profiles/r05e_dw5_register_window_ab.log)
-#endif
 constexpr int DW_CS = 32;  // channels per plane per block (64 B per pixel: adjacent blocks share lines)
 constexpr int DW_TW = 32;  // output columns per block
 constexpr int DW_TH = 8;   // output rows per block
 constexpr int DW_ORDER_AUTO = 0;  // block order of kernel 0 (eggroll_dwconv_nhwc_sel: 1 = order 0, 2 = order 1)
 
 typedef __attribute__((ext_vector_type(4))) unsigned short u16x4m;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2m;
 
 // PW: the DC-AE multi-scale branch's grouped 1x1 conv (groups of DW_CS = 32 channels, the block's
 // channel slice) fused behind the depthwise conv: the block's bf16-rounded conv tile [256 px][32 ch]
@@ -100,34 +98,66 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
     }
     const int b = bid;
     const int y0 = band * DW_TH, x0 = xt * DW_TW, c0 = cs * DW_CS;
-    const unsigned short* img = in + (int64_t)b * H * W * Cin;
-    // stage: 16-byte units [plane][ty][tx][4 chunks]; every load of the thread is issued before the
-    // first is consumed (a rolled load -> SiLU -> ds_write loop pays one memory latency per unit)
-    constexpr int UNITS = PLANES * TR * TC * 4;
-    constexpr int PER = (UNITS + 255) / 256;
-    u16x8m v[PER];
+    const char* img = reinterpret_cast<const char*>(in + (int64_t)b * H * W * Cin);
+    const uint32_t cin2 = (uint32_t)Cin * 2, rowb = (uint32_t)W * cin2;
+    // Stage the 16-byte units [plane][ty][tx][4 chunks] with buffer loads whose addresses cost no VALU
+    // work (the address arithmetic of the previous form was ~40% of the kernel's VALU issue, and the
+    // kernel is VALU-issue-bound: profiles/r09a_pmc_dwconv.json).  Main columns (tx in [HALO, HALO+32)):
+    // thread = (row parity rp, column mc, chunk ch), one image row pair per pass; the row's buffer
+    // descriptor (SGPRs: base = the row, size 0 when the row is outside the image) makes the zero padding
+    // rows free, and a column past W gets an out-of-range offset (the load returns zeros).  The 2*HALO
+    // halo columns: one unit per thread with its own index arithmetic.  Every load of the thread is issued
+    // before the first is consumed.
+    constexpr uint32_t OOR = 0x80000000u;  // out-of-range buffer offset (images are < 2 GiB: host check)
+    const int rp = __builtin_amdgcn_readfirstlane(tid >> 7);  // wave-uniform
+    const int mc = (tid >> 2) & 31, ch = tid & 3;
+    const uint32_t mvoff = x0 + mc < W ? (uint32_t)(x0 + mc) * cin2 + (uint32_t)(c0 * 2 + ch * 16) : OOR;
+    constexpr int MPASS = PLANES * TR / 2;  // TR is even for KS 3 and 5
+    static_assert(TR % 2 == 0, "row pairs");
+    u16x8m v[MPASS];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
+    for (int p = 0; p < MPASS; ++p) {
+        const int pl = (2 * p) / TR, ty = (2 * p) % TR + rp;
+        const int gy = y0 + ty - HALO;
+        const bool ok = gy >= 0 && gy < H;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(img + (int64_t)(ok ? gy : 0) * rowb + pl * Cout * 2), (short)0, ok ? (int)rowb : 0, 0x00020000);
+        v[p] = __builtin_bit_cast(u16x8m, __builtin_amdgcn_raw_buffer_load_b128(rs, mvoff, 0, 0));
+    }
+    constexpr int HC = 2 * HALO, HUNITS = PLANES * TR * HC * 4, HPER = (HUNITS + 255) / 256;
+    const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc((void*)img, (short)0, (int)(H * rowb),
+                                                                          0x00020000);
+    u16x8m hv[HPER];
+    uint32_t hlds[HPER];
+#pragma unroll
+    for (int k = 0; k < HPER; ++k) {
         const int u = tid + k * 256;
-        const int ch = u & 3;
-        int pix = u >> 2;
-        const int pl = pix / (TR * TC);
-        pix -= pl * (TR * TC);
-        const int ty = pix / TC, tx = pix - ty * TC;
+        const int hch = u & 3, hcol = (u >> 2) % HC, row = (u >> 2) / HC;
+        const int pl = row / TR, ty = row - pl * TR;
+        const int tx = hcol < HALO ? hcol : hcol + DW_TW;
         const int gy = y0 + ty - HALO, gx = x0 + tx - HALO;
-        v[k] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
-        if (u < UNITS && gy >= 0 && gy < H && gx >= 0 && gx < W)
-            v[k] = *reinterpret_cast<const u16x8m*>(img + ((int64_t)gy * W + gx) * Cin + pl * Cout + c0 + ch * 8);
+        const bool ok = u < HUNITS && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const uint32_t off = ok ? (uint32_t)(gy * W + gx) * cin2 + (uint32_t)((pl * Cout + c0) * 2 + hch * 16) : OOR;
+        hv[k] = __builtin_bit_cast(u16x8m, __builtin_amdgcn_raw_buffer_load_b128(rimg, off, 0, 0));
+        hlds[k] = u < HUNITS ? (uint32_t)(((pl * TR + ty) * TC + tx) * 64 + hch * 16) : 0xffffffffu;
+    }
+    auto pre = [](u16x8m& x) {
+        if (PRE_SILU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = f2b(silu(b2f(x[i])));
+        }
+    };
+    const uint32_t mlds = (uint32_t)((rp * TC + HALO + mc) * 64 + ch * 16);
+#pragma unroll
+    for (int p = 0; p < MPASS; ++p) {
+        pre(v[p]);
+        *reinterpret_cast<u16x8m*>(lds + mlds + (2 * p) * TC * 64) = v[p];
     }
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int u = tid + k * 256;
-        if (u < UNITS) {
-            if (PRE_SILU) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[k][i] = f2b(silu(b2f(v[k][i])));
-            }
-            *reinterpret_cast<u16x8m*>(lds + (size_t)u * 16) = v[k];
+    for (int k = 0; k < HPER; ++k) {
+        if (hlds[k] != 0xffffffffu) {
+            pre(hv[k]);
+            *reinterpret_cast<u16x8m*>(lds + hlds[k]) = hv[k];
         }
     }
     __syncthreads();
@@ -139,61 +169,35 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
 #pragma unroll
         for (int i = 0; i < 4; ++i) f[i] = b2f(v[i]);
     };
+    // output: one buffer descriptor per image (rows past H: offset out of range, store dropped)
+    const int64_t obase = (int64_t)b * H * W * ldo_;
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(out + obase), (short)0, (int)((int64_t)H * W * ldo_ * 2), 0x00020000);
     float res[DW_TH][4];  // value-plane results, gated by the second plane (GLU)
 #pragma unroll 1
     for (int pl = 0; pl < PLANES; ++pl) {
         float w[KS * KS][4], bs[4];
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(wt + pl * Cout), (short)0, (int)(KS * KS * cin2), 0x00020000);
 #pragma unroll
         for (int t = 0; t < KS * KS; ++t) {
-            const u16x4m wv = *reinterpret_cast<const u16x4m*>(wt + (int64_t)t * Cin + pl * Cout + cq);
+            const u16x4m wv = __builtin_bit_cast(u16x4m, __builtin_amdgcn_raw_buffer_load_b64(rw, (uint32_t)cq * 2,
+                                                                                            t * (int)cin2, 0));
 #pragma unroll
             for (int i = 0; i < 4; ++i) w[t][i] = b2f(wv[i]);
         }
+        if (bias) {
+            const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(bias + pl * Cout), (short)0,
+                                                                                (int)cin2, 0x00020000);
+            const u16x4m bv = __builtin_bit_cast(u16x4m, __builtin_amdgcn_raw_buffer_load_b64(rb, (uint32_t)cq * 2, 0, 0));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) bs[i] = bias ? b2f(bias[pl * Cout + cq + i]) : 0.0f;
-        // the KS x KS input window in registers, sliding down the band: one new input row (KS LDS reads)
-        // per output row instead of KS*KS.  KS = 5 with EGG_DW5_WIN = 0: every tap read from LDS (the
-        // round-3 form: fewer VGPRs, 3 waves per SIMD instead of 2; A/B knob)
-        constexpr bool WIN = KS == 3 || EGG_DW5_WIN;
-        float win[KS][KS][4];
-        if constexpr (WIN) {
+            for (int i = 0; i < 4; ++i) bs[i] = b2f(bv[i]);
+        } else {
 #pragma unroll
-            for (int r = 0; r < KS - 1; ++r)
-#pragma unroll
-                for (int dx = 0; dx < KS; ++dx) rd(pl, r, xs + dx, win[r][dx]);
+            for (int i = 0; i < 4; ++i) bs[i] = 0.0f;
         }
-        constexpr int ROW_UNROLL = KS == 3 ? DW_TH : 1;
-#pragma unroll ROW_UNROLL
-        for (int oy = 0; oy < DW_TH; ++oy) {
-            if constexpr (WIN) {
-#pragma unroll
-                for (int dx = 0; dx < KS; ++dx) rd(pl, oy + KS - 1, xs + dx, win[KS - 1][dx]);
-            }
-            float acc[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i] = bs[i];
-#pragma unroll
-            for (int dy = 0; dy < KS; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < KS; ++dx) {
-                    float tap[4];
-                    if constexpr (WIN) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) tap[i] = win[dy][dx][i];
-                    } else {
-                        rd(pl, oy + dy, xs + dx, tap);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[i] += tap[i] * w[dy * KS + dx][i];
-                }
-            if constexpr (WIN) {
-#pragma unroll
-                for (int r = 0; r < KS - 1; ++r)
-#pragma unroll
-                    for (int dx = 0; dx < KS; ++dx)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) win[r][dx][i] = win[r + 1][dx][i];
-            }
+        // one output row's result -> the PW tile in LDS, the GLU value plane, or the output
+        auto emit = [&](int oy, const float (&acc)[4]) {
             if constexpr (PW) {
                 // conv tile -> LDS [pixel oy*32+x][32 ch], 64-B rows with slot ^= 2*((pixel >> 2) & 1): the
                 // 16x16x32 fragment reads (16 consecutive pixels, 4 chunks) are then bank-conflict-free
@@ -206,15 +210,67 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
                 for (int i = 0; i < 4; ++i) res[oy][i] = acc[i];
             } else {
                 const int y = y0 + oy;
-                if (y < H && x < W) {
-                    u16x4m o;
+                u16x4m o;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) o[i] = f2b(GLU ? res[oy][i] * silu(acc[i]) : acc[i]);
-                    unsigned short* orow = out + (((int64_t)b * H + y) * W + x) * ldo_;
-                    *reinterpret_cast<u16x4m*>(orow + cq) = o;
-                    if (ldo_ > Cout && cs == cslices - 1 && Cout + q * 4 < ldo_)
-                        *reinterpret_cast<u16x4m*>(orow + Cout + q * 4) = u16x4m{0, 0, 0, 0};
-                }
+                for (int i = 0; i < 4; ++i) o[i] = f2b(GLU ? res[oy][i] * silu(acc[i]) : acc[i]);
+                const uint32_t px = (uint32_t)(y * W + x) * (uint32_t)ldo_ * 2;
+                const bool ok = y < H && x < W;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o), rout,
+                                                      ok ? px + (uint32_t)cq * 2 : OOR, 0, 0);
+                if (ldo_ > Cout && cs == cslices - 1 && Cout + q * 4 < ldo_)
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2m{0u, 0u}, rout,
+                                                          ok ? px + (uint32_t)(Cout + q * 4) * 2 : OOR, 0, 0);
+            }
+        };
+        if constexpr (KS == 3) {
+            // the 3x3 input window in registers, sliding down the band: one new input row (3 LDS reads,
+            // 12 conversions) per output row instead of 9
+            float win[KS][KS][4];
+#pragma unroll
+            for (int r = 0; r < KS - 1; ++r)
+#pragma unroll
+                for (int dx = 0; dx < KS; ++dx) rd(pl, r, xs + dx, win[r][dx]);
+#pragma unroll
+            for (int oy = 0; oy < DW_TH; ++oy) {
+#pragma unroll
+                for (int dx = 0; dx < KS; ++dx) rd(pl, oy + KS - 1, xs + dx, win[KS - 1][dx]);
+                float acc[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = bs[i];
+#pragma unroll
+                for (int dy = 0; dy < KS; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < KS; ++dx)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[i] += win[dy][dx][i] * w[dy * KS + dx][i];
+#pragma unroll
+                for (int r = 0; r < KS - 1; ++r)
+#pragma unroll
+                    for (int dx = 0; dx < KS; ++dx)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) win[r][dx][i] = win[r + 1][dx][i];
+                emit(oy, acc);
+            }
+        } else {
+            // KS = 5: every tap read from LDS and converted at its use.  A 5x5 fp32 register window
+            // measured 11 % slower (2 vs 3 waves per SIMD, profiles/r05e_dw5_register_window_ab.log), and
+            // row groups that convert each input row once for 2-4 output rows spill at 3 waves per SIMD
+            // next to the 25 taps' fp32 weights (r09 build, 172-500 B of scratch per lane).
+#pragma unroll 1
+            for (int oy = 0; oy < DW_TH; ++oy) {
+                float acc[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = bs[i];
+#pragma unroll
+                for (int dy = 0; dy < KS; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < KS; ++dx) {
+                        float tap[4];
+                        rd(pl, oy + dy, xs + dx, tap);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[i] += tap[i] * w[dy * KS + dx][i];
+                    }
+                emit(oy, acc);
             }
         }
     }
@@ -235,12 +291,11 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
             for (int j = 0; j < 2; ++j) {
                 // transposed product: lane holds pixel p, outputs 16j + 4 g4 .. +3
                 const la_f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bo[j], a, la_f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                if (y < H && xx < W) {
-                    u16x4m o;
+                u16x4m o;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) o[e] = f2b(d[e]);
-                    *reinterpret_cast<u16x4m*>(out + (((int64_t)b * H + y) * W + xx) * Cout + c0 + 16 * j + 4 * g4) = o;
-                }
+                for (int e = 0; e < 4; ++e) o[e] = f2b(d[e]);
+                const uint32_t off = y < H && xx < W ? ((uint32_t)(y * W + xx) * Cout + c0 + 16 * j + 4 * g4) * 2 : OOR;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o), rout, off, 0, 0);
             }
         }
     }
@@ -1586,7 +1641,7 @@ extern "C" int eggroll_dwconv_nhwc_ex(const void* in, const void* w_t, const voi
     EGG_CHECK_ARG(ks == 3 || ks == 5, "dwconv: ks=%d unsupported (3, 5)", ks);
     EGG_CHECK_ARG(((uintptr_t)in & 15) == 0 && ((uintptr_t)w_t & 15) == 0 && ((uintptr_t)out & 15) == 0,
                   "dwconv: pointers must be 16-byte aligned");
-    EGG_CHECK_ARG(H * W * C < (1ll << 31) && H * W * ldo < (1ll << 31), "dwconv: image too large");
+    EGG_CHECK_ARG(H * W * C < (1ll << 30) && H * W * ldo < (1ll << 30), "dwconv: image too large (< 2 GiB per image)");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(in && w_t && out, "dwconv: NULL pointer");
     const int64_t bands = (H + DW_TH - 1) / DW_TH, xtiles = (W + DW_TW - 1) / DW_TW, cslices = cout / DW_CS;
@@ -1627,7 +1682,7 @@ extern "C" int eggroll_dwconv_pw_nhwc_sel(const void* in, const void* w_t, const
     EGG_CHECK_ARG(((uintptr_t)in & 15) == 0 && ((uintptr_t)w_t & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
                       ((uintptr_t)pw & 15) == 0,
                   "dwconv_pw: pointers must be 16-byte aligned");
-    EGG_CHECK_ARG(H * W * C < (1ll << 31), "dwconv_pw: image too large");
+    EGG_CHECK_ARG(H * W * C < (1ll << 30), "dwconv_pw: image too large (< 2 GiB per image)");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(in && w_t && pw && out && out != in, "dwconv_pw: NULL or aliased pointer");
     const int64_t bands = (H + DW_TH - 1) / DW_TH, xtiles = (W + DW_TW - 1) / DW_TW, cslices = C / DW_CS;
