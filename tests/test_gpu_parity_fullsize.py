@@ -34,7 +34,7 @@ from oracle import member_eval_fp32 as R
 
 pytestmark = pytest.mark.gpu
 
-# ~1.5x the round-5 measurement on MI355X (profiles/r08a_fullsize_parity.txt; DESIGN.md §3.2 "full size")
+# ~1.5x the round-5 measurement on MI355X (profiles/r08c_fullsize_parity.txt; DESIGN.md §3.2 "full size")
 BOUNDS = {"lora_rel": 6.5e-3,     # every LoRA'd linear output, ||y - y32|| / ||y32|| (measured 0.43 %)
           "eps_rel": 4.5e-3,      # transformer output (0.29 %)
           "image_rel": 0.055,     # decoded image (3.7 %: the bf16 1024-px DC-AE stages)
