@@ -960,10 +960,25 @@ constexpr int HD_PSTR = HD_C * 2;        // LDS bytes per staged pixel: 16-B chu
                                          // 53 KB per block -> 3 blocks per CU instead of 2)
 __device__ __forceinline__ int hd_slot(int pix, int c) { return pix * HD_PSTR + ((c ^ (pix & 15)) << 4); }
 
+// Sum over a 16-lane row, the xor butterfly 8, 4, 2, 1 on DPP (no LDS round trips): row_ror:8 is xor 8;
+// after it every value is symmetric under xor 8, so row_ror:4 reads the xor-4 partner; quad_perm does
+// xor 2 and xor 1.  Same additions in the same order as __shfl_xor(·, 8 / 4 / 2 / 1): the same bits in
+// every lane.
+template <int CTRL>
+__device__ __forceinline__ float hd_dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float hd_sum16(float v) {
+    v += hd_dpp<0x128>(v);  // row_ror:8
+    v += hd_dpp<0x124>(v);  // row_ror:4
+    v += hd_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += hd_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    return v;
+}
 typedef __attribute__((ext_vector_type(8))) __bf16 hd_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float hd_f32x4;
 
-__global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restrict__ x, int H, int W, float eps,
+__global__ __launch_bounds__(256, 3) void k_dcae_head(const unsigned short* __restrict__ x, int H, int W, float eps,
                                                    const unsigned short* __restrict__ nw,
                                                    const unsigned short* __restrict__ nb,
                                                    const unsigned short* __restrict__ wc,   // [3][3][3][C]
@@ -985,88 +1000,134 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
     const int b = bid / bgroups;
     const int band_lo = bg * tpb, band_hi = min(bands, band_lo + tpb);
     const int x0 = xt * HD_TW;
-    const unsigned short* img = x + (int64_t)b * H * W * HD_C;
+    const char* img = reinterpret_cast<const char*>(x + (int64_t)b * H * W * HD_C);
+    const uint32_t rowb = (uint32_t)W * HD_PSTR;
     // conv weights -> LDS (6.75 KiB), once per block
     for (int u = tid; u < 3 * 9 * HD_C / 8; u += 256)
         *reinterpret_cast<u16x8m*>(wl + u * 8) = *reinterpret_cast<const u16x8m*>(wc + u * 8);
-    // halo tile unit u = (pixel u / 16, 16-B chunk u % 16); a pixel's 16 chunks are 16 consecutive
-    // lanes, so its sum of squares is a 16-lane shuffle reduction
-    constexpr int UNITS = HD_TR * HD_TC * 16;
-    constexpr int PER = (UNITS + 255) / 256;
-    u16x8m v[PER];
-    auto in_b = [&](int k, int y0) {
-        const int u = tid + k * 256;
-        const int pix = u >> 4;
-        const int ty = pix / HD_TC, tx = pix - ty * HD_TC;
-        const int gy = y0 + ty - 1, gx = x0 + tx - 1;
-        return u < UNITS && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    // Halo tile staging with buffer descriptors (round 5; the per-unit pixel division and 64-bit address
+    // arithmetic of the previous form made this kernel VALU-issue-bound, profiles/r09d_epoch_census.txt).
+    // Thread = (main column mc, 16-B chunk ch): the 16 main columns (tx 1..16) of every halo row, one row
+    // descriptor per row (size 0 outside the image: zero rows), a column past W an out-of-range offset;
+    // the 2 halo columns (tx 0, 17) x 10 rows x 16 chunks = 320 units take one or two indexed loads.  A
+    // pixel's 16 chunks stay 16 consecutive lanes (its sum of squares is a 16-lane shuffle reduction).
+    constexpr uint32_t OOR = 0x80000000u;
+    const int ch = tid & 15, mc = tid >> 4;
+    const bool mcol_ok = x0 + mc < W;
+    const uint32_t mvoff = mcol_ok ? (uint32_t)(x0 + mc) * HD_PSTR + ch * 16 : OOR;
+    constexpr int HU = HD_TR * 2 * 16, HPER = (HU + 255) / 256;   // 320 halo-column units
+    u16x8m v[HD_TR], hv[HPER];
+    bool hok[HPER];
+    const __amdgpu_buffer_rsrc_t rimg = __builtin_amdgcn_make_buffer_rsrc((void*)img, (short)0, (int)(H * rowb),
+                                                                          0x00020000);
+    // halo-column unit k of rows rlo..HD_TR-1: row rlo + (hp >> 1), column 0 or 17
+    auto hunit = [&](int k, int rlo, int& ty, int& tx) {
+        const int u = tid + k * 256, hp = u >> 4;
+        ty = rlo + (hp >> 1);
+        tx = (hp & 1) ? HD_TC - 1 : 0;
+        return u < (HD_TR - rlo) * 32;
     };
-    auto load = [&](int y0) {
+    // rows rlo..HD_TR-1 of the halo tile whose first row is image row y0 - 1 (rlo = 0: a block's first
+    // band; 2: a later band, whose rows 0, 1 are the previous band's rows 8, 9, already in LDS)
+    auto load = [&](int y0, int rlo) {
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int u = tid + k * 256;
-            const int pix = u >> 4, ch = u & 15;
-            const int ty = pix / HD_TC, tx = pix - ty * HD_TC;
+        for (int r = 0; r < HD_TR; ++r) {
+            if (r < rlo) continue;
+            const int gy = y0 + r - 1;
+            const bool ok = gy >= 0 && gy < H;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(img + (int64_t)(ok ? gy : 0) * rowb), (short)0, ok ? (int)rowb : 0, 0x00020000);
+            v[r] = __builtin_bit_cast(u16x8m, __builtin_amdgcn_raw_buffer_load_b128(rs, mvoff, 0, 0));
+        }
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            int ty, tx;
+            const bool in = hunit(k, rlo, ty, tx);
             const int gy = y0 + ty - 1, gx = x0 + tx - 1;
-            v[k] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
-            if (in_b(k, y0)) v[k] = *reinterpret_cast<const u16x8m*>(img + ((int64_t)gy * W + gx) * HD_C + ch * 8);
+            hok[k] = in && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const uint32_t off = hok[k] ? (uint32_t)(gy * W + gx) * HD_PSTR + ch * 16 : OOR;
+            hv[k] = __builtin_bit_cast(u16x8m, __builtin_amdgcn_raw_buffer_load_b128(rimg, off, 0, 0));
         }
     };
     float wv[8], bv[8];
     {
-        const int ch = tid & 15;  // every unit of this thread has the same chunk (256 % 16 == 0)
         const u16x8m qw = *reinterpret_cast<const u16x8m*>(nw + ch * 8);
         const u16x8m qb = *reinterpret_cast<const u16x8m*>(nb + ch * 8);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { wv[i] = b2f(qw[i]); bv[i] = b2f(qb[i]); }
     }
+    // RMS-normalise one 16-B unit (8 channels of one pixel), affine, ReLU, bf16; zero where the halo pixel
+    // is outside the image.  (f * rstd) * w + b per value as before: the packed pairs round each product
+    // and sum exactly like the scalar ops, so the tile is bitwise unchanged.
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    auto norm = [&](const u16x8m& q, bool ok) {
+        float f[8], ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { f[i] = b2f(q[i]); ss += f[i] * f[i]; }
+        ss = hd_sum16(ss);
+        const float rstd = __builtin_amdgcn_rsqf(ss / HD_C + eps);  // >= eps: never denormal
+        u16x8m o8 = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ok) {
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                f2 t = f2{f[i], f[i + 1]} * f2{rstd, rstd};
+                t = t * f2{wv[i], wv[i + 1]};
+                t = t + f2{bv[i], bv[i + 1]};
+                o8[i] = f2b(t.x > 0.f ? t.x : 0.f);
+                o8[i + 1] = f2b(t.y > 0.f ? t.y : 0.f);
+            }
+        }
+        return o8;
+    };
     const int n = lane & 15, g = lane >> 4;
     const float bias = (n < 3 && cb) ? b2f(cb[n]) : 0.f;
-    load(band_lo * HD_TH);
+    // B operand column n = output channel n; columns 3..15 are computed and never stored, so their lanes
+    // read a real channel's weights (no zero row, no branch: 52.9 KB of LDS, 3 blocks per CU)
+    const int wrow = (n % 3) * 9 * HD_C + g * 8;
+    // Rolling rows: tile row r of the j-th band a block walks sits in LDS row slot (8j + r) mod 10, so the
+    // two rows a band shares with the next (its rows 8, 9 = the next band's rows 0, 1) are loaded and
+    // normalised once (10 -> 8 rows per band after the first).
+    auto slot = [](int j8, int r) { const int q = j8 + r; return q >= HD_TR ? q - HD_TR : q; };
+    load(band_lo * HD_TH, 0);
+    int j8 = 0;  // 8j mod 10
 #pragma unroll 1
     for (int band = band_lo; band < band_hi; ++band) {
         const int y0 = band * HD_TH;
+        const int rlo = band > band_lo ? 2 : 0;
         if (band > band_lo) __syncthreads();  // every wave's conv reads of the previous band are done
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int u = tid + k * 256;
-            float f[8], ss = 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { f[i] = b2f(v[k][i]); ss += f[i] * f[i]; }
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);  // within the pixel's 16 lanes
-            const float rstd = rsqrtf(ss / HD_C + eps);
-            u16x8m o8 = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (in_b(k, y0)) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    float t = f[i] * rstd;
-                    t *= wv[i];
-                    t += bv[i];
-                    o8[i] = f2b(t > 0.f ? t : 0.f);
-                }
-            }
-            if (u < UNITS) *reinterpret_cast<u16x8m*>(tile + hd_slot(u >> 4, u & 15)) = o8;
+        for (int r = 0; r < HD_TR; ++r) {
+            if (r < rlo) continue;
+            const int gy = y0 + r - 1;
+            const u16x8m o8 = norm(v[r], mcol_ok && gy >= 0 && gy < H);
+            *reinterpret_cast<u16x8m*>(tile + hd_slot(slot(j8, r) * HD_TC + 1 + mc, ch)) = o8;
         }
-        if (band + 1 < band_hi) load(y0 + HD_TH);
+#pragma unroll
+        for (int k = 0; k < HPER; ++k) {
+            int ty, tx;
+            const bool in = hunit(k, rlo, ty, tx);
+            const u16x8m o8 = norm(hv[k], hok[k]);
+            if (in) *reinterpret_cast<u16x8m*>(tile + hd_slot(slot(j8, ty) * HD_TC + tx, ch)) = o8;
+        }
+        if (band + 1 < band_hi) load(y0 + HD_TH, 2);
+        // conv A-fragment addresses: hd_slot(pix, cq*4 + g) = hd_slot(pix, g) ^ (cq << 6) (the chunk's low
+        // two bits are g, cq only flips bits 2..3 of the slot): one base per (output row, tap), a XOR per k-step
+        uint32_t abase[2][9];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap)
+                abase[r][tap] = (uint32_t)hd_slot(slot(j8, wave * 2 + r + tap / 3) * HD_TC + n + tap % 3, g);
         __syncthreads();
         // conv: wave w computes output rows 2w, 2w+1 (one 16-pixel M-tile each)
         hd_f32x4 acc[2] = {hd_f32x4{0.f, 0.f, 0.f, 0.f}, hd_f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll 4
+#pragma unroll
         for (int s = 0; s < 36; ++s) {
-            const int tap = s >> 2, cq = s & 3, dy = tap / 3, dx = tap - 3 * (tap / 3);
-            hd_bf16x8 bf;
-            if (n < 3) {
-                bf = *reinterpret_cast<const hd_bf16x8*>(wl + (n * 9 + tap) * HD_C + cq * 32 + g * 8);
-            } else {
-                const u16x8m z = {0, 0, 0, 0, 0, 0, 0, 0};
-                bf = __builtin_bit_cast(hd_bf16x8, z);
-            }
+            const int tap = s >> 2, cq = s & 3;
+            const hd_bf16x8 bf = *reinterpret_cast<const hd_bf16x8*>(wl + wrow + tap * HD_C + cq * 32);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
-                const int oy = wave * 2 + r;
-                const hd_bf16x8 af =
-                    *reinterpret_cast<const hd_bf16x8*>(tile + hd_slot((oy + dy) * HD_TC + n + dx, cq * 4 + g));
+                const hd_bf16x8 af = *reinterpret_cast<const hd_bf16x8*>(tile + (abase[r][tap] ^ (uint32_t)(cq << 6)));
                 acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[r], 0, 0, 0);
             }
         }
@@ -1082,6 +1143,7 @@ __global__ __launch_bounds__(256) void k_dcae_head(const unsigned short* __restr
                 }
             }
         }
+        j8 = slot(j8, HD_TH);
     }
 }
 
