@@ -301,6 +301,36 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
     }
 }
 
+// Sum over SEG-lane segments (16 / 32 / 64) without LDS round trips, as the xor butterfly
+// __shfl_xor(·, SEG/2 ... 1) computes it — the same additions in the same order, so the same bits in every
+// lane: xor 32 / xor 16 by v_permlane32_swap / v_permlane16_swap (gfx950; called on one register twice,
+// the two results are each lane's own value and its partner's, and their sum is the butterfly step), xor 8
+// by DPP row_ror:8; after that every value is symmetric under xor 8, so row_ror:4 reads the xor-4 partner;
+// quad_perm does xor 2 and xor 1.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+template <int SEG>
+__device__ __forceinline__ float seg_sum(float v) {
+    static_assert(SEG == 16 || SEG == 32 || SEG == 64, "segment of 16, 32 or 64 lanes");
+    if constexpr (SEG == 64) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                         false, false);
+        v = __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+    }
+    if constexpr (SEG >= 32) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                         false, false);
+        v = __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+    }
+    v += dpp_f<0x128>(v);  // row_ror:8 = xor 8
+    v += dpp_f<0x124>(v);  // row_ror:4 = xor 4 here
+    v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1] = xor 2
+    v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2] = xor 1
+    return v;
+}
+
 // ------------------------------------------------------------------------------------
 // Fused row normalisation over the channel (last) dim of a [rows, C] bf16 tensor:
 //   y = norm(x)                      RMS (x / sqrt(mean x^2 + eps)) or LayerNorm (centred)
@@ -357,8 +387,7 @@ __global__ __launch_bounds__(256) void k_rownorm(const void* __restrict__ x, int
             for (int i = 0; i < 8; ++i) v[t][i] = 0.f;
         }
     }
-#pragma unroll
-    for (int o = SEG / 2; o > 0; o >>= 1) s1 += __shfl_xor(s1, o, 64);
+    s1 = seg_sum<SEG>(s1);
     const float mean = layer ? s1 / C : 0.f;
     float s2 = 0.f;
 #pragma unroll
@@ -368,8 +397,7 @@ __global__ __launch_bounds__(256) void k_rownorm(const void* __restrict__ x, int
 #pragma unroll
             for (int i = 0; i < 8; ++i) { const float d = v[t][i] - mean; s2 += d * d; }
     }
-#pragma unroll
-    for (int o = SEG / 2; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    s2 = seg_sum<SEG>(s2);
     const float rstd = rsqrtf(s2 / C + eps);
     if (!live) return;
     const int64_t g = row / rows_per_group;
@@ -471,8 +499,7 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(float* __restrict__ h, 
             for (int i = 0; i < 8; ++i) s1 += v[t][i];
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s1 += __shfl_xor(s1, o, 64);
+    s1 = seg_sum<64>(s1);
     const float mean = s1 / C;
     float s2 = 0.f;
 #pragma unroll
@@ -481,8 +508,7 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(float* __restrict__ h, 
 #pragma unroll
             for (int i = 0; i < 8; ++i) { const float d = v[t][i] - mean; s2 += d * d; }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    s2 = seg_sum<64>(s2);
     const float rstd = rsqrtf(s2 / C + eps);
 #pragma unroll
     for (int t = 0; t < NCH; ++t) {
@@ -960,21 +986,6 @@ constexpr int HD_PSTR = HD_C * 2;        // LDS bytes per staged pixel: 16-B chu
                                          // 53 KB per block -> 3 blocks per CU instead of 2)
 __device__ __forceinline__ int hd_slot(int pix, int c) { return pix * HD_PSTR + ((c ^ (pix & 15)) << 4); }
 
-// Sum over a 16-lane row, the xor butterfly 8, 4, 2, 1 on DPP (no LDS round trips): row_ror:8 is xor 8;
-// after it every value is symmetric under xor 8, so row_ror:4 reads the xor-4 partner; quad_perm does
-// xor 2 and xor 1.  Same additions in the same order as __shfl_xor(·, 8 / 4 / 2 / 1): the same bits in
-// every lane.
-template <int CTRL>
-__device__ __forceinline__ float hd_dpp(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float hd_sum16(float v) {
-    v += hd_dpp<0x128>(v);  // row_ror:8
-    v += hd_dpp<0x124>(v);  // row_ror:4
-    v += hd_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-    v += hd_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-    return v;
-}
 typedef __attribute__((ext_vector_type(8))) __bf16 hd_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float hd_f32x4;
 
@@ -1064,7 +1075,7 @@ __global__ __launch_bounds__(256, 3) void k_dcae_head(const unsigned short* __re
         float f[8], ss = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) { f[i] = b2f(q[i]); ss += f[i] * f[i]; }
-        ss = hd_sum16(ss);
+        ss = seg_sum<16>(ss);
         const float rstd = __builtin_amdgcn_rsqf(ss / HD_C + eps);  // >= eps: never denormal
         u16x8m o8 = {0, 0, 0, 0, 0, 0, 0, 0};
         if (ok) {
@@ -1527,8 +1538,7 @@ __global__ __launch_bounds__(256) void k_qk_norm_rope(unsigned short* __restrict
         f[i] = b2f(v[i]);
         ss += f[i] * f[i];
     }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);   // within the 16-lane segment
+    ss = seg_sum<16>(ss);   // within the 16-lane segment
     const float r = rsqrtf(ss / 128.f + eps);
     if (!live) return;
     const u16x8m wv = *reinterpret_cast<const u16x8m*>(w + l * 8);

@@ -1,0 +1,76 @@
+"""A/B of two or more builds of libeggroll through the package's own op wrappers (kernels.py): the
+global library handle is swapped between bound builds, each op's outputs are compared bitwise with the
+first build's, then timed interleaved (median of rounds, HIP events on the launch stream).  Ops: the
+epoch's row norms (Sana AdaLN on the fp32 stream with fp32 modulation, C = 2240; bf16 rows, C = 2240;
+DC-AE RMSNorm + bias + fp32 residual, C = 512 and 1024), resid_layernorm (CLIP towers), the Z-Image q/k
+norm + RoPE and the DC-AE decoder head.
+usage: python tools/ops_lib_ab.py <libA.so> <libB.so> [...]"""
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from hyperscalees_t2i_amd import _lib  # noqa: E402
+from hyperscalees_t2i_amd import kernels as K  # noqa: E402
+from es_lib_ab import bind, timed  # noqa: E402
+
+
+def cases(dev, g):
+    r = lambda *s, dt=torch.bfloat16, sc=1.0: (torch.randn(*s, device=dev, generator=g) * sc).to(dt)  # noqa: E731
+    out = {}
+    # Sana AdaLN: fp32 stream x [131072, 2240], fp32 (1 + scale) / shift per image (1024 rows each)
+    x32 = r(131072, 2240, dt=torch.float32)
+    ms, mh = r(128, 2240, dt=torch.float32, sc=0.1), r(128, 2240, dt=torch.float32, sc=0.1)
+    out["adaln f32 131072x2240"] = lambda: K.rownorm(x32, 1e-6, layer=True, mscale=ms, mshift=mh, rows_per_group=1024)
+    xb = r(131072, 2240)
+    wb = r(2240, sc=0.5)
+    out["rms bf16 131072x2240 +w"] = lambda: K.rownorm(xb, 1e-6, w=wb)
+    for C, rows in ((512, 8 * 256 * 256), (1024, 8 * 128 * 128)):
+        xc, wc, bc = r(rows, C), r(C, sc=0.5), r(C, sc=0.1)
+        res0 = r(rows, C, dt=torch.float32)
+        res = res0.clone()
+
+        def f(xc=xc, wc=wc, bc=bc, res=res, res0=res0):
+            res.copy_(res0)
+            return K.rownorm(xc, 1e-5, w=wc, b=bc, res=res)
+        out[f"dcae rms+res32 {rows}x{C}"] = f
+    h0 = r(16 * 257, 1280, dt=torch.float32)
+    h = h0.clone()
+    y, w2, b2 = r(16 * 257, 1280), r(1280, sc=0.5), r(1280, sc=0.1)
+
+    def rl():
+        h.copy_(h0)
+        return torch.cat([K.resid_layernorm_(h, y, w2, b2, 1e-5).float().flatten(), h.flatten()])
+    out["resid_layernorm 4112x1280"] = rl
+    return out
+
+
+def main(paths, rounds=7):
+    libs = [bind(p) for p in paths]
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    res = {}
+    for name, fn in cases(dev, g).items():
+        outs = []
+        for lib in libs:
+            _lib._lib = lib
+            outs.append(fn().clone())
+        torch.cuda.synchronize()
+        same = [torch.equal(outs[0], o) for o in outs[1:]]
+        us = [[] for _ in libs]
+        for _ in range(rounds):
+            for i, lib in enumerate(libs):
+                _lib._lib = lib
+                us[i].append(timed(fn))
+        res[name] = {"bitwise_equal_to_A": same, **{Path(p).name: round(statistics.median(u), 1)
+                                                     for p, u in zip(paths, us)}}
+        print(json.dumps({name: res[name]}), flush=True)
+        assert all(same), name
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
