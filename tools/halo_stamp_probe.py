@@ -11,7 +11,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-OUT = ROOT / "tools" / "_stamps" / "libeggroll_stamps.so"
+OUT = ROOT / "tools" / "_ab" / "libeggroll_stamps.so"   # travels to the GPU box (git-ignored)
 
 
 def build():
@@ -63,8 +63,12 @@ def main():
                 out = {"tile0_prologue": med(s[:, 1] - s[:, 0]), "tile0_main": med(s[:, 2] - s[:, 1]),
                        "tile0_epilogue": med(s[:, 3] - s[:, 2]), "later_tile_avg": med((s[:, 5] - s[:, 3]) / 3),
                        "workgroup": med(s[:, 5] - s[:, 0])}
+            wall = float(s[:, 7].max() - s[:, 6].min()) * 10e-9
             out.update({"kernel": kern, "shape": f"8x{hw}x{hw}x{C}", "clock_GHz": round(clk / 1e9, 3),
-                        "wall_us": round(float(s[:, 7].max() - s[:, 6].min()) * 10e-3, 1)})
+                        "wall_us": round(wall * 1e6, 1),
+                        # cycles per workgroup a CU delivers (wall x clock x 256 CUs / workgroups): vs the
+                        # median workgroup duration, the time lost between workgroups
+                        "cu_cycles_per_workgroup": int(wall * clk * 256 / nblk)})
             print(json.dumps(out), flush=True)
         del x, y
 
