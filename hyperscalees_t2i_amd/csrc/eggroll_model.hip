@@ -896,14 +896,33 @@ __device__ __forceinline__ void la_split8(const float (&f)[8], la_bf16x8& hi, la
     }
 }
 
+// Round 5: the denominator row ksum is written into A rows 0, 4, 8 and 12 (each lane group g then holds
+// den of its own token r16 as C[4g][r16] — the shuffle that broadcast row 0 is gone), a wave covers
+// LAO_TPW tiles of 16 tokens (the kv hi/lo split amortised over twice the tokens, twice the q loads in
+// flight), and q / out go through buffer descriptors (one per image, head offset in the base: 32-bit
+// offsets, tokens past N out of range).  Same MFMAs, same operands: the same bits.
+constexpr int LAO_TPW = 8;                     // 16-token tiles per wave
+constexpr int LAO_T = 4 * LAO_TPW * 16;        // tokens per block
 __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict__ q, int64_t ld, int64_t hstride,
-                                                int heads, int N, int nchunk, int relu, const float* __restrict__ kvsum,
+                                                int heads, int N, int nblk_tok, int relu, const float* __restrict__ kvsum,
                                                 unsigned short* __restrict__ out, int64_t ldo) {
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = lb / nchunk, c = lb - bh * nchunk;
+    const int bh = lb / nblk_tok, c = lb - bh * nblk_tok;
     const int b = bh / heads, h = bh - b * heads;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r16 = lane & 15, g = lane >> 4;
+    const int n0 = c * LAO_T + wave * (LAO_T / 4);
+    // q tiles first (the longest latency), then kv from L2
+    constexpr uint32_t OOR = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(q + (int64_t)b * N * ld + (int64_t)h * hstride), (short)0, (int)((int64_t)N * ld * 2), 0x00020000);
+    u16x8m qr[LAO_TPW];
+#pragma unroll
+    for (int tt = 0; tt < LAO_TPW; ++tt) {
+        const int tok = n0 + tt * 16 + r16;
+        const uint32_t off = tok < N ? ((uint32_t)tok * (uint32_t)ld + 8 * g) * 2 : OOR;
+        qr[tt] = __builtin_bit_cast(u16x8m, __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, 0));
+    }
     const float* kvh = kvsum + (int64_t)bh * LA_PART;
     la_bf16x8 akv[2][2], aden[2];  // [feature block][hi, lo]
 #pragma unroll
@@ -915,7 +934,7 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
     }
     {
         float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (r16 == 0) {  // A row 0 = ksum, rows 1..15 = 0
+        if ((r16 & 3) == 0) {  // A rows 0, 4, 8, 12 = ksum, the rest 0
             const float4 x0 = *reinterpret_cast<const float4*>(kvh + LA_D * LA_D + 8 * g);
             const float4 x1 = *reinterpret_cast<const float4*>(kvh + LA_D * LA_D + 8 * g + 4);
             f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w;
@@ -923,16 +942,10 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
         }
         la_split8(f, aden[0], aden[1]);
     }
-    const int n0 = c * LA_T + wave * (LA_T / 4);
-    u16x8m qr[LA_T / 64];  // this wave's 4 tiles of 16 tokens: all loads in flight first
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(out + (int64_t)b * N * ldo + h * LA_D), (short)0, (int)((int64_t)N * ldo * 2), 0x00020000);
 #pragma unroll
-    for (int tt = 0; tt < LA_T / 64; ++tt) {
-        const int tok = n0 + tt * 16 + r16;
-        qr[tt] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
-        if (tok < N) qr[tt] = *reinterpret_cast<const u16x8m*>(q + ((int64_t)b * N + tok) * ld + (int64_t)h * hstride + 8 * g);
-    }
-#pragma unroll
-    for (int tt = 0; tt < LA_T / 64; ++tt) {
+    for (int tt = 0; tt < LAO_TPW; ++tt) {
         const int tok = n0 + tt * 16 + r16;
         u16x8m qv = qr[tt];
         if (relu) {
@@ -947,19 +960,16 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
         a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[1][1], bq, a1, 0, 0, 0);
         ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[0], bq, ad, 0, 0, 0);
         ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[1], bq, ad, 0, 0, 0);
-        const float den = __shfl(ad[0], r16, 64);  // denominator of token r16 sits in lane r16 (row 0)
-        const float inv = 1.0f / (den + 1e-15f);
-        if (tok < N) {
-            unsigned short* o = out + ((int64_t)b * N + tok) * ldo + h * LA_D + 4 * g;
-            u16x4m o0, o1;
+        const float inv = 1.0f / (ad[0] + 1e-15f);  // C[4g][r16] = den of token r16 in every lane group
+        const uint32_t off = tok < N ? ((uint32_t)tok * (uint32_t)ldo + 4 * g) * 2 : OOR;
+        u16x4m o0, o1;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                o0[e] = f2b(a0[e] * inv);
-                o1[e] = f2b(a1[e] * inv);
-            }
-            *reinterpret_cast<u16x4m*>(o) = o0;
-            *reinterpret_cast<u16x4m*>(o + 16) = o1;
+        for (int e = 0; e < 4; ++e) {
+            o0[e] = f2b(a0[e] * inv);
+            o1[e] = f2b(a1[e] * inv);
         }
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o0), ro, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o1), ro, off + 32, 0, 0);
     }
 }
 
@@ -1867,6 +1877,7 @@ extern "C" int eggroll_linear_attention(const void* q, const void* k, const void
                   ((uintptr_t)out & 15) == 0, "linear_attention: pointers must be 16-byte aligned");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(q && k && v && out && workspace, "linear_attention: NULL pointer");
+    EGG_CHECK_ARG(N * ld < (1ll << 30) && N * ldo < (1ll << 30), "linear_attention: image too large (< 2 GiB per image)");
     const int64_t nchunk = (N + LA_T - 1) / LA_T;
     const int64_t blocks = B * heads * nchunk;
     EGG_CHECK_ARG(blocks < (1ll << 31), "linear_attention: grid too large");
@@ -1883,8 +1894,9 @@ extern "C" int eggroll_linear_attention(const void* q, const void* k, const void
         hipLaunchKernelGGL(k_la_reduce, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const float*)workspace,
                            (int)nchunk, kvsum);
     EGG_CHECK_LAUNCH("linear_attention_reduce");
-    hipLaunchKernelGGL(k_la_out, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)q, ld, hstride,
-                       (int)heads, (int)N, (int)nchunk, relu_qk, (const float*)kvsum, (unsigned short*)out, ldo);
+    const int64_t oblk = (N + LAO_T - 1) / LAO_T;
+    hipLaunchKernelGGL(k_la_out, dim3((unsigned)(B * heads * oblk)), dim3(256), 0, st, (const unsigned short*)q, ld,
+                       hstride, (int)heads, (int)N, (int)oblk, relu_qk, (const float*)kvsum, (unsigned short*)out, ldo);
     EGG_CHECK_LAUNCH("linear_attention_out");
     return EGGROLL_OK;
 }

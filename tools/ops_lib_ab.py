@@ -37,6 +37,14 @@ def cases(dev, g):
             res.copy_(res0)
             return K.rownorm(xc, 1e-5, w=wc, b=bc, res=res)
         out[f"dcae rms+res32 {rows}x{C}"] = f
+    # linear attention: Sana attn1 (separate q / k / v [B*N, 2240], 70 heads) and DC-AE planar [Q|K|V]
+    qs, ks, vs = r(128 * 1024, 2240), r(128 * 1024, 2240), r(128 * 1024, 2240)
+    out["linear_attention sana 128x1024 h70"] = lambda: K.linear_attention(qs, ks, vs, 128, 1024, 70, 32, False)
+    for Bd, N, hd in ((8, 16384, 16), (8, 4096, 32), (8, 1024, 32)):
+        flat = r(Bd * N, 3 * hd * 32)
+        inner = hd * 32
+        out[f"linear_attention dcae {Bd}x{N} h{hd}"] = (lambda flat=flat, inner=inner, Bd=Bd, N=N, hd=hd:
+            K.linear_attention(flat, flat[:, inner:], flat[:, 2 * inner:], Bd, N, hd, 32, True))
     h0 = r(16 * 257, 1280, dt=torch.float32)
     h = h0.clone()
     y, w2, b2 = r(16 * 257, 1280), r(1280, sc=0.5), r(1280, sc=0.1)
@@ -48,12 +56,14 @@ def cases(dev, g):
     return out
 
 
-def main(paths, rounds=7):
+def main(paths, rounds=7, only=None):
     libs = [bind(p) for p in paths]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     res = {}
     for name, fn in cases(dev, g).items():
+        if only and only not in name:
+            continue
         outs = []
         for lib in libs:
             _lib._lib = lib
@@ -73,4 +83,5 @@ def main(paths, rounds=7):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    only = next((a[7:] for a in sys.argv[1:] if a.startswith("--only=")), None)
+    main([a for a in sys.argv[1:] if not a.startswith("--only=")], only=only)
