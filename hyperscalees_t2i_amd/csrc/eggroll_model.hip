@@ -1465,6 +1465,191 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     }
 }
 
+// Round 5: 32 queries per wave block (QF = 2 query fragments share every k / v fragment read from LDS:
+// half the LDS bytes per query, the bound of the 16-query form), with the softmax taken online over two
+// key halves so that only half the scores are live in registers (S for 2 x LM/2 keys: the QF = 2
+// two-pass form needed 160 score registers and fell to 1 wave per SIMD).  After the first half
+// (max m0, P0 = exp(S0 - m0), O = V0^T P0), the second rescales O and the running row sums by
+// exp(m0 - m1) before adding its own keys — exact softmax up to fp32 rounding.
+template <int HD, int NWAVE, int LM>
+__global__ __launch_bounds__(64 * NWAVE) void k_cross_attn_h2(const unsigned short* __restrict__ q, int64_t ldq,
+                                                       const unsigned short* __restrict__ k,
+                                                       const unsigned short* __restrict__ v, int64_t ldkv,
+                                                       const unsigned short* __restrict__ bias,
+                                                       const int* __restrict__ enc_index, int heads, int N, int L,
+                                                       int U, float scale, unsigned short* __restrict__ o, int64_t ldo) {
+    constexpr int QF = 2;
+    constexpr int RS = HD + 8, KSN = (HD + 31) / 32, DF = HD / 16;
+    constexpr int FH = LM / 32;  // key fragments (of 16) per half
+    static_assert(HD % 16 == 0 && HD <= 128 && LM % 64 == 0, "head dim / key capacity");
+    __shared__ __attribute__((aligned(16))) unsigned short sk[LM * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short sv[LM * RS];
+    __shared__ float sb[LM];
+    constexpr int NT = 64 * NWAVE;
+    const int bh = xcd_remap(blockIdx.x, gridDim.x);
+    const int b = bh / heads, h = bh - b * heads;
+    const int u_in = enc_index ? enc_index[b] : b;
+    const bool u_bad = u_in < 0 || u_in >= U;  // out-of-range caption row: NaN output, no out-of-bounds read
+    const int u = u_bad ? 0 : u_in;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+    constexpr int CH = HD / 8;
+    for (int c = tid; c < LM * CH; c += NT) {
+        const int r = c / CH, cc = c - r * CH;
+        u16x8m kv = u16x8m{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
+        if (r < L) {
+            const int64_t off = ((int64_t)u * L + r) * ldkv + (int64_t)h * HD + cc * 8;
+            kv = *reinterpret_cast<const u16x8m*>(k + off);
+            vv = *reinterpret_cast<const u16x8m*>(v + off);
+        }
+        *reinterpret_cast<u16x8m*>(sk + r * RS + cc * 8) = kv;
+        *reinterpret_cast<u16x8m*>(sv + r * RS + cc * 8) = vv;
+    }
+    for (int r = tid; r < LM; r += NT)
+        sb[r] = u_bad ? __builtin_nanf("") : r < L ? (bias ? b2f(bias[(int64_t)u * L + r]) : 0.0f) : -INFINITY;
+    __syncthreads();
+    const int nkf = (L + 15) / 16, nkb = (L + 31) / 32;
+    const int nqb = (N + 16 * QF - 1) / (16 * QF);
+    auto load_q = [&](int qb_, la_bf16x8 (&dst)[QF][KSN]) {
+#pragma unroll
+        for (int x = 0; x < QF; ++x) {
+            const int qrow = qb_ * 16 * QF + 16 * x + r16;
+#pragma unroll
+            for (int ks = 0; ks < KSN; ++ks) {
+                const int d0 = 32 * ks + 8 * g;
+                u16x8m t = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+                if (d0 < HD && qrow < N)
+                    t = *reinterpret_cast<const u16x8m*>(q + ((int64_t)b * N + qrow) * ldq + (int64_t)h * HD + d0);
+                dst[x][ks] = __builtin_bit_cast(la_bf16x8, t);
+            }
+        }
+    };
+    // the next block's q fragments are loaded right after this block's first-half S^T MFMAs are issued
+    // (their latency runs under the softmax and PV: EGG_XA_PREFETCH)
+    la_bf16x8 bq[QF][KSN], bqn[QF][KSN];
+    if (w < nqb) load_q(w, bqn);
+#pragma unroll 1
+    for (int qb = w; qb < nqb; qb += NWAVE) {
+#pragma unroll
+        for (int x = 0; x < QF; ++x)
+#pragma unroll
+            for (int ks = 0; ks < KSN; ++ks) bq[x][ks] = bqn[x][ks];
+        float mx[QF], sum[QF];
+        la_f32x4 oc[QF][DF];
+#pragma unroll
+        for (int x = 0; x < QF; ++x) {
+            mx[x] = -INFINITY;
+            sum[x] = 0.0f;
+#pragma unroll
+            for (int d = 0; d < DF; ++d) oc[x][d] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int f0 = half * FH;
+            if (f0 >= nkf) break;  // uniform: L <= LM / 2 keys
+            la_f32x4 sf[QF][FH];
+            float lm[QF];
+#pragma unroll
+            for (int x = 0; x < QF; ++x) lm[x] = -INFINITY;
+#pragma unroll
+            for (int f = 0; f < FH; ++f) {
+#pragma unroll
+                for (int x = 0; x < QF; ++x) sf[x][f] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+                if (f0 + f < nkf) {
+#pragma unroll
+                    for (int ks = 0; ks < KSN; ++ks) {
+                        const int d0 = 32 * ks + 8 * g;
+                        la_bf16x8 a;
+                        if (d0 < HD) a = *reinterpret_cast<const la_bf16x8*>(sk + (16 * (f0 + f) + r16) * RS + d0);
+                        else a = la_bf16x8{};
+#pragma unroll
+                        for (int x = 0; x < QF; ++x) sf[x][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[x][ks], sf[x][f], 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float bb = sb[16 * (f0 + f) + 4 * g + e];
+#pragma unroll
+                        for (int x = 0; x < QF; ++x) {
+                            const float sv_ = sf[x][f][e] * scale + bb;
+                            sf[x][f][e] = sv_;
+                            lm[x] = fmaxf(lm[x], sv_);
+                        }
+                    }
+                }
+            }
+            if (half == 0 && qb + NWAVE < nqb) load_q(qb + NWAVE, bqn);
+            float alpha[QF];
+#pragma unroll
+            for (int x = 0; x < QF; ++x) {
+                lm[x] = fmaxf(lm[x], __shfl_xor(lm[x], 16));
+                lm[x] = fmaxf(lm[x], __shfl_xor(lm[x], 32));
+                const float mn = fmaxf(mx[x], lm[x]);
+                alpha[x] = half == 0 ? 0.0f : __expf(mx[x] - mn);
+                mx[x] = mn;
+            }
+            if (half > 0) {
+#pragma unroll
+                for (int x = 0; x < QF; ++x) {
+                    sum[x] *= alpha[x];
+#pragma unroll
+                    for (int d = 0; d < DF; ++d)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) oc[x][d][e] *= alpha[x];
+                }
+            }
+#pragma unroll
+            for (int f = 0; f < FH; ++f) {
+                if (f0 + f < nkf) {
+#pragma unroll
+                    for (int x = 0; x < QF; ++x)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float pe = __expf(sf[x][f][e] - mx[x]);
+                            sf[x][f][e] = pe;
+                            sum[x] += pe;
+                        }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < FH / 2; ++j) {
+                const int jj = half * (FH / 2) + j;
+                if (jj < nkb) {
+                    la_bf16x8 bp[QF];
+#pragma unroll
+                    for (int x = 0; x < QF; ++x)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            bp[x][e] = (__bf16)sf[x][2 * j][e];
+                            bp[x][4 + e] = (__bf16)sf[x][2 * j + 1][e];
+                        }
+#pragma unroll
+                    for (int d = 0; d < DF; ++d) {
+                        const la_bf16x8 av = xa_tr8_perm<RS>(sv + (32 * jj) * RS + 16 * d, lane);
+#pragma unroll
+                        for (int x = 0; x < QF; ++x) oc[x][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bp[x], oc[x][d], 0, 0, 0);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < QF; ++x) {
+            sum[x] += __shfl_xor(sum[x], 16);
+            sum[x] += __shfl_xor(sum[x], 32);
+            const int qrow = qb * 16 * QF + 16 * x + r16;
+            if (qrow < N) {
+                const float inv = 1.0f / sum[x];
+                unsigned short* dst = o + ((int64_t)b * N + qrow) * ldo + (int64_t)h * HD + 4 * g;
+#pragma unroll
+                for (int d = 0; d < DF; ++d) {
+                    u16x4m t;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) t[e] = f2b(oc[x][d][e] * inv);
+                    *reinterpret_cast<u16x4m*>(dst + 16 * d) = t;
+                }
+            }
+        }
+    }
+}
+
 template <int SEG, int NCH>
 static void launch_rownorm(const void* x, int xf32, int64_t rows, int C, float eps, int layer, const void* w,
                            const void* b, const void* ms, const void* mh, int64_t mstride, int mf32, int64_t rpg,
@@ -2375,8 +2560,16 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
     // 8 waves x 16-query blocks (164 VGPRs, 2 waves per SIMD): measured 0.80 ms at the Sana attn2 shape
     // (B 128, N 1024, 20 heads, L 300) vs 0.94 for 4 waves x 32 queries and 1.27 for 4 x 16 (SDPA on
     // the gathered k / v with the mask: 1.53 ms)
+#ifndef EGG_XA_H2
+#define EGG_XA_H2 1   // 32-query blocks with the two-half online softmax (k_cross_attn_h2); 0 = k_cross_attn
+#endif
+#if EGG_XA_H2
+#define EGG_XA_KERNEL(HD_, LM_) (k_cross_attn_h2<HD_, 8, LM_>)
+#else
+#define EGG_XA_KERNEL(HD_, LM_) (k_cross_attn<HD_, 8, 1, LM_>)
+#endif
 #define EGG_XA(HD_, LM_)                                                                                         \
-    hipLaunchKernelGGL((k_cross_attn<HD_, 8, 1, LM_>), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream), \
+    hipLaunchKernelGGL(EGG_XA_KERNEL(HD_, LM_), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream),     \
                        (const unsigned short*)q, ldq, (const unsigned short*)k, (const unsigned short*)v, ldkv,    \
                        (const unsigned short*)bias, enc_index, (int)heads, (int)N, (int)L, (int)U, scale, (unsigned short*)o, \
                        ldo)
@@ -2385,6 +2578,7 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
     else if (head_dim == 80) EGG_XA(80, XA_LMAX);
     else EGG_XA(64, XA_LMAX);
 #undef EGG_XA
+#undef EGG_XA_KERNEL
     EGG_CHECK_LAUNCH("cross_attention");
     return EGGROLL_OK;
 }
