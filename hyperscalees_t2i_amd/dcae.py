@@ -145,10 +145,11 @@ class GLUMBConvC(nn.Module):
         (shadow = its bf16 copy)."""
         B, H, W, C = x.shape
         if C <= 512:
-            # 1x1 conv + SiLU on the 8-phase GEMM (SiLU in its epilogue; same values as the unfused
-            # path).  At 1024 channels hipBLASLt's GEMM is faster than the saved SiLU pass.
+            # 1x1 conv on the 8-phase GEMM, SiLU in the depthwise conv's staging (lora.SILU_IN_GEMM: in the
+            # GEMM epilogue instead, the same bits; 3.5 % slower at 512 channels since round 5,
+            # profiles/r09q_silu_placement.log).  At 1024 channels hipBLASLt's GEMM is faster.
             x2 = x.reshape(-1, C)
-            if lora.FUSE_EPILOGUES:
+            if lora.FUSE_EPILOGUES and lora.SILU_IN_GEMM:
                 h = K.lora_linear_pop_epi(x2, self.w_inv, self.b_inv, None, 0, 0, 0, 0.0, B * H * W, "silu")
                 g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=False, glu=True)
             else:

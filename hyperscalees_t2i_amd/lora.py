@@ -33,6 +33,9 @@ from . import kernels as K
 # (tests/test_gpu_engine.py::test_fused_epilogues_bit_identical); False keeps every GEMM output
 # materialised (per-linear captures in the fp32 drift test).
 FUSE_EPILOGUES = True
+# GLUMBConv's SiLU in the inverted conv's GEMM epilogue (True) or in the depthwise conv's staging (False,
+# the default since round 5: the same bits, 1.2-3.5 % faster per GLUMBConv, profiles/r09q_silu_placement.log)
+SILU_IN_GEMM = False
 
 
 # bytes of one GEMM operand the kernels can address (32-bit buffer offsets); larger X runs in row chunks

@@ -231,10 +231,12 @@ class GLUMBConv(nn.Module):
         """res / gate (optional): the block's gated residual x += gate_mlp * ff(x) fused into the
         point conv's GEMM epilogue ("gated32" on the fp32 stream, "gated" on bf16); returns res."""
         B, N, D = x.shape
-        # 1x1 conv + SiLU on the 8-phase GEMM (SiLU of the bf16-rounded output in its epilogue), then
-        # dw3x3 -> GLU fused; the same values as F.linear -> dwconv(pre_silu=True)
+        # 1x1 conv on the 8-phase GEMM, then SiLU -> dw3x3 -> GLU in the depthwise conv (SiLU applied once
+        # per staged element); lora.SILU_IN_GEMM moves the SiLU into the GEMM epilogue instead — the same
+        # bits (silu of the bf16-rounded output), measured 1.2 % slower per FFN since round 5's cheaper
+        # depthwise staging (tools/silu_split_probe.py, profiles/r09q_silu_placement.log)
         kp = -(-self.hidden // 64) * 64     # 5600 -> 5632: the GEMM's k-step is 64
-        if lora.FUSE_EPILOGUES:
+        if lora.FUSE_EPILOGUES and lora.SILU_IN_GEMM:
             h = K.lora_linear_pop_epi(x.reshape(B * N, D), self.w_inv, self.b_inv, None, 0, 0, 0, 0.0, B * N, "silu")
             g = K.dwconv_nhwc(h.view(B, H, W, -1), self.w_dw, self.b_dw, 3, pre_silu=False, glu=True, ldo=kp)
         else:

@@ -1369,3 +1369,23 @@ def test_group_norm_nhwc_vs_torch(dev, B, H, W, C, G, silu):
     got = Kk.group_norm_nhwc(x, G, w, b, 1e-6, silu=silu).float()
     err = (got - ref).abs()
     assert (err <= ref.abs() * 2 ** -7 + 2e-3).all(), float(err.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M_img,H,W,C,H2,ldo", [(2, 8, 8, 64, 512, 0), (2, 4, 8, 128, 384, 224)])
+def test_glumbconv_silu_placement_bitexact(dev, M_img, H, W, C, H2, ldo):
+    """GLUMBConv's SiLU in the inverted conv's GEMM epilogue (lora.SILU_IN_GEMM) and in the depthwise
+    conv's staging (the default since round 5) compute silu of the same bf16-rounded GEMM output with
+    the same device silu: the depthwise conv outputs are bitwise equal."""
+    g = torch.Generator(device=dev).manual_seed(5)
+    M = M_img * H * W
+    x = (torch.randn(M, C, device=dev, generator=g) * 0.5).bfloat16()
+    wi = (torch.randn(H2, C, device=dev, generator=g) * C ** -0.5).bfloat16()
+    bi = (torch.randn(H2, device=dev, generator=g) * 0.1).bfloat16()
+    wd = (torch.randn(9, H2, device=dev, generator=g) * 0.2).bfloat16()
+    bd = (torch.randn(H2, device=dev, generator=g) * 0.1).bfloat16()
+    h_epi = K.lora_linear_pop_epi(x, wi, bi, None, 0, 0, 0, 0.0, M, "silu")
+    a = K.dwconv_nhwc(h_epi.view(M_img, H, W, H2), wd, bd, 3, pre_silu=False, glu=True, ldo=ldo)
+    h = K.lora_linear_pop(x, wi, bi, None, 0, 0, 0, 0.0, M)
+    b = K.dwconv_nhwc(h.view(M_img, H, W, H2), wd, bd, 3, pre_silu=True, glu=True, ldo=ldo)
+    assert torch.equal(a, b)
