@@ -41,11 +41,12 @@ BOUNDS = {"lora_rel": 6.5e-3,     # every LoRA'd linear output, ||y - y32|| / ||
           "reward_abs": 5e-3,     # per-image combined reward (0.0032)
           "S_abs": 3e-3}          # S[k, j] (0.0018; member spread of S 0.029)
 # pooled over SEEDS x 28 member pairs: measured tau 1.0 (round 5, 4 seeds, profiles/r08c_fullsize_parity.txt)
-# and 0.982 after the cross-attention's online softmax (one discordant pair of 112, a worst-member swap;
-# profiles/r09s_pytest_gpu.log, r09t_fullsize_rank_fidelity.log: the swapped pair is 1.45x the epoch's score error apart), max |dS| 0.0017-0.0020 against a member spread of 0.013.  A bf16 build
-# cannot order two members whose fp32 fitness scores differ by less than its own score error, so every
-# discordant pair and every best / worst miss must be such a near-tie: its fp32 score gap at most
-# NEAR_TIE x the epoch's largest |score - score32| (the member-level error of the same epoch).
+# and 0.982 after the cross-attention's online softmax: one discordant pair of 112, a worst-member swap
+# whose fp32 scores are 1.45x the epoch's score error apart (profiles/r09t_fullsize_rank_fidelity.log);
+# max |dS| 0.0017-0.0020 against a member spread of 0.013.  A bf16 build cannot order two members whose
+# fp32 fitness scores differ by less than its own score error, so every discordant pair and every best /
+# worst miss must be such a near-tie: its fp32 score gap at most NEAR_TIE x the epoch's largest
+# |score - score32| (the member-level error of the same epoch).
 RANK_BOUNDS = {"S_abs": 3e-3, "pooled_tau": 0.95, "near_tie": 2.0}
 SEEDS = (5, 6, 7, 8)
 DECODE_CHUNK = 4
