@@ -100,6 +100,10 @@ class InfinityES:
             # models/Infinity.py:183-235: the Infinity repo's state dict (.pth, or a shard directory with its
             # index) and the BSQ-VAE .pth, strict (checkpoints.load_infinity_transformer / load_bsq_vae_decoder)
             from . import checkpoints as ck
+            for nm, pth in (("model_path", model_path), ("vae_path", vae_path)):
+                if not Path(pth).exists():
+                    raise FileNotFoundError(f"{nm} {pth}: no local Infinity checkpoint there (a .pth or a shard "
+                                            "directory); pass synthetic_weights=True for the throughput configuration")
             ck.load_infinity_transformer(self.infinity, Path(model_path), checkpoint_type)
             ck.load_bsq_vae_decoder(self.vae, Path(vae_path))
             self.weights_source = str(model_path)
