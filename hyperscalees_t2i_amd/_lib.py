@@ -70,6 +70,7 @@ SIGNATURES = {
     "eggroll_conv3x3_rmsnorm_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, C.c_float, vp, vp, vp, vp,
                                                vp]),
     "eggroll_conv_nhwc_sel": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, i32, i32, vp, i32, vp]),
+    "eggroll_conv2x2_subpixel_nhwc": (C.c_int, [vp, vp, vp, vp, i32, i64, i64, i64, i64, i64, vp, vp, vp]),
     "eggroll_conv3x3_rmsnorm_nhwc_sel": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i64, i32, C.c_float, vp, vp, vp,
                                                    vp, i32, vp]),
     "eggroll_dcae_head": (C.c_int, [vp, i64, i64, i64, i64, f32, vp, vp, vp, vp, vp, vp]),

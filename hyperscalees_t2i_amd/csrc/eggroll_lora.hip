@@ -2392,6 +2392,120 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
     }
 }
 
+// DC-AE up-block epilogue (eggroll_conv2x2_subpixel_nhwc): the phase conv's C tile goes straight to the
+// up-sampled output instead of a y4 [B, H+1, W+1, 4*Cout] intermediate read back by
+// k_subpixel_shortcut4.  Row = phase-conv position (b, h', w') of the (H+1) x (W+1) grid, column =
+// (phase k = 2i + j, output channel): out[b, 2h + i, 2w + j, c] = bf16(y) + bias[c] + src[b, h, w,
+// (4c + k) / REP] with (h, w) = (h' - i, w' - j) (positions with h or w outside the input are dropped),
+// y rounded to bf16 first and the two adds in that order — the arithmetic of k_subpixel_shortcut4, so the
+// output is bitwise the two-kernel path's.  SP 1: bf16 src and out; SP 2: fp32 src (the DC-AE fp32
+// residual stream) and fp32 out, plus its bf16 shadow when given.
+struct SubpixArgs {
+    const unsigned short* bias;  // [Cout] or null
+    const void* src;             // shortcut source [B, H, W, Cin]
+    void* out;                   // [B, 2H, 2W, Cout]
+    unsigned short* shadow;      // SP 2: optional bf16 copy of out
+    int H, W, Cin, Cout;
+};
+
+// KP: the wave's phase (wave-uniform, dispatched by the caller) — a compile-time shortcut channel index
+template <int SP, int REP, int KP>
+__device__ __forceinline__ void store_tile_subpix(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int rbase,
+                                                  int col0, int Mp, const SubpixArgs& sp) {
+    constexpr int ROWB = 128, SLOTS = 8;
+    constexpr int XW = 32 / REP;                     // shortcut channels spanned by 8 outputs
+    constexpr int WD = SP == 2 ? XW : XW / 2;        // their dwords (raw, converted at use)
+    constexpr int RBAT = WD >= 16 ? 64 / WD : 8;     // rows whose shortcut loads are in flight together (<= 64 VGPRs)
+    char* ctile = smem + wave * (128 * ROWB);
+    {
+        const int r_l = lane & 15, c_l = (lane >> 4) * 4;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int rr = i * 16 + r_l;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int cc = j * 16 + c_l;
+                const int slot = (cc >> 3) ^ (rr & (SLOTS - 1));
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = f32_to_bf16(acc[i][j][e]);
+                *reinterpret_cast<u16x4*>(ctile + rr * ROWB + slot * 16 + (cc & 7) * 2) = o;
+            }
+        }
+    }
+    // the wave's 64 columns lie in one phase (Cout % 64 == 0, host-checked)
+    constexpr int k = KP, pi = KP >> 1, pj = KP & 1;
+    const int c0 = col0 - k * sp.Cout + (lane & 7) * 8;
+    float bv[8];
+    if (sp.bias) {
+        const u16x8 q = *reinterpret_cast<const u16x8*>(sp.bias + c0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = bf16_to_f32(q[e]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+    }
+    const int H = sp.H, W = sp.W, Ho = H + 1, Wo = W + 1;
+    int p = rbase + (lane >> 3);
+    int bb = p / (Ho * Wo), hp = (p - bb * Ho * Wo) / Wo, wp = p - bb * Ho * Wo - hp * Wo;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
+#pragma unroll
+    for (int it0 = 0; it0 < 16; it0 += RBAT) {
+        uint32_t raw[RBAT][WD];
+        int64_t opix[RBAT];
+        bool ok[RBAT];
+#pragma unroll
+        for (int u = 0; u < RBAT; ++u) {
+            const int h = hp - pi, w = wp - pj;
+            ok[u] = p < Mp && h >= 0 && h < H && w >= 0 && w < W;
+            const int64_t lp = ok[u] ? ((int64_t)bb * H + h) * W + w : 0;
+            opix[u] = ((int64_t)bb * 2 * H + 2 * h + pi) * (2 * W) + 2 * w + pj;
+            // window of channels (4c + k) / REP, c = c0 .. c0+7: XW channels from 4 c0 / REP
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(
+                reinterpret_cast<const char*>(sp.src) + (lp * sp.Cin + 4 * c0 / REP) * (SP == 2 ? 4 : 2));
+#pragma unroll
+            for (int t = 0; t < WD / 4; ++t) {
+                typedef __attribute__((ext_vector_type(4))) unsigned int sp_u32x4;
+                const sp_u32x4 q = *reinterpret_cast<const sp_u32x4*>(src + 4 * t);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) raw[u][4 * t + e] = q[e];
+            }
+            p += 8;
+            wp += 8;
+            while (wp >= Wo) {
+                wp -= Wo;
+                if (++hp == Ho) { hp = 0; ++bb; }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RBAT; ++u) {
+            const int it = it0 + u, rr = it * 8 + (lane >> 3), sl = lane & 7;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(ctile + rr * ROWB + ((sl ^ (rr & (SLOTS - 1))) << 4));
+            if (!ok[u]) continue;
+            float f[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int ch = (4 * q + k) / REP;  // compile-time: q unrolled, k = KP
+                const float xsv = SP == 2 ? __uint_as_float(raw[u][ch])
+                                          : bf16_to_f32((unsigned short)(raw[u][ch >> 1] >> (16 * (ch & 1))));
+                f[q] = bf16_to_f32(v[q]) + bv[q] + xsv;
+            }
+            const int64_t oo = opix[u] * sp.Cout + c0;
+            if constexpr (SP == 2) {
+                float* o32 = reinterpret_cast<float*>(sp.out) + oo;
+                *reinterpret_cast<f32x4*>(o32) = f32x4{f[0], f[1], f[2], f[3]};
+                *reinterpret_cast<f32x4*>(o32 + 4) = f32x4{f[4], f[5], f[6], f[7]};
+            }
+            if (SP == 1 || sp.shadow) {
+                u16x8 o;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) o[q] = f32_to_bf16(f[q]);
+                *reinterpret_cast<u16x8*>((SP == 2 ? sp.shadow : reinterpret_cast<unsigned short*>(sp.out)) + oo) = o;
+            }
+        }
+    }
+}
+
 template <int WMW, bool NORM>
 constexpr int conv_smem_bytes() {
     using G = G8<WMW>;
@@ -2399,7 +2513,7 @@ constexpr int conv_smem_bytes() {
     return G::LDS > need ? G::LDS : need;
 }
 
-template <int PX, int ACT, bool NORM = false, int KS = 3, int WMW = 2>
+template <int PX, int ACT, bool NORM = false, int KS = 3, int WMW = 2, int SP = 0, int REP = 2>
 __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* __restrict__ X,
                                                           const unsigned short* __restrict__ Wt,
                                                           const unsigned short* __restrict__ bias, int H, int W,
@@ -2407,7 +2521,9 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
                                                           unsigned short* __restrict__ Y, float eps = 0.0f,
                                                           const unsigned short* __restrict__ nw = nullptr,
                                                           const unsigned short* __restrict__ nb = nullptr,
-                                                          const unsigned short* __restrict__ res = nullptr) {
+                                                          const unsigned short* __restrict__ res = nullptr,
+                                                          SubpixArgs spa = SubpixArgs{}) {
+    static_assert(SP == 0 || (KS == 2 && PX == 1 && ACT == 0 && !NORM), "sub-pixel epilogue: the up-block phase conv");
     using G = G8<WMW>;
     constexpr int TW = PX + KS - 1;
     __shared__ __attribute__((aligned(16))) char smem[conv_smem_bytes<WMW, NORM>()];
@@ -2509,7 +2625,14 @@ __global__ __launch_bounds__(512, 1) void k_conv3x3_gemm8(const unsigned short* 
     EGG_STAMP(3);
     if (bias)
         lora_mfma_addend<0>(acc, lane, m0, n0, wm * 128, wn * 64, bias, nullptr, nullptr, 0, 0, 0.0f, 1 << 30, Mp, N);
-    if constexpr (NORM) {
+    if constexpr (SP != 0) {
+        EGG_STAMP(4);
+        const int kp = __builtin_amdgcn_readfirstlane((n0 + wn * 64) / spa.Cout);
+        if (kp == 0) store_tile_subpix<SP, REP, 0>(acc, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, Mp, spa);
+        else if (kp == 1) store_tile_subpix<SP, REP, 1>(acc, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, Mp, spa);
+        else if (kp == 2) store_tile_subpix<SP, REP, 2>(acc, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, Mp, spa);
+        else store_tile_subpix<SP, REP, 3>(acc, smem, wave, lane, m0 + wm * 128, n0 + wn * 64, Mp, spa);
+    } else if constexpr (NORM) {
         conv_rmsnorm_epilogue<PX, WMW>(
             acc, reinterpret_cast<float*>(smem + G::CSTAGE), wm, wn, lane,
             [&](int rr) -> int64_t { return m0 + rr < Mp ? m0 + rr : Mp - 1; }, eps, nw, nb, res);
@@ -3520,6 +3643,53 @@ int eggroll_conv_nhwc_sel(const void* x, const void* w_packed, const void* bias,
     else EGG_CONV(2, 1, 3, 2);
 #undef EGG_CONV
     EGG_CHECK_LAUNCH("conv_nhwc");
+    return EGGROLL_OK;
+}
+
+int eggroll_conv2x2_subpixel_nhwc(const void* x, const void* w_packed, const void* bias, const void* src,
+                                  int32_t src_f32, int64_t B, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                  void* out, void* shadow, void* stream) {
+    EGG_CHECK_ARG(B > 0 && H > 0 && W > 0, "conv2x2_subpixel: bad B/H/W");
+    EGG_CHECK_ARG(Cin >= 64 && Cin <= 2048 && (Cin & (Cin - 1)) == 0,
+                  "conv2x2_subpixel: Cin=%lld must be a power of two in [64, 2048]", (long long)Cin);
+    EGG_CHECK_ARG(Cout >= 64 && Cout % 64 == 0 && 4 * Cout <= 8192 && (4 * Cout) % Cin == 0,
+                  "conv2x2_subpixel: Cout=%lld must be a multiple of 64 with 4*Cout a multiple of Cin", (long long)Cout);
+    const int64_t rep = 4 * Cout / Cin;
+    EGG_CHECK_ARG(rep == 1 || rep == 2 || rep == 4, "conv2x2_subpixel: 4*Cout/Cin = %lld unsupported (1, 2, 4)",
+                  (long long)rep);
+    EGG_CHECK_ARG(src_f32 == 0 || src_f32 == 1, "conv2x2_subpixel: src_f32 must be 0 or 1");
+    EGG_CHECK_ARG(src_f32 || !shadow, "conv2x2_subpixel: shadow needs the fp32 form");
+    const int64_t Mp = B * (H + 1) * (W + 1), N = 4 * Cout, K = 4 * Cin;
+    EGG_CHECK_ARG(Mp < (1ll << 31) && (256 * 2 + 2 * W + 8) * Cin * 2 < (1ll << 30) && N * K * 2 < (1ll << 31) &&
+                      B * 4 * H * W * Cout < (1ll << 31),
+                  "conv2x2_subpixel: sizes exceed the kernel's offsets");
+    EGG_CHECK_ARG(x && w_packed && src && out, "conv2x2_subpixel: NULL pointer");
+    EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                      ((uintptr_t)shadow & 15) == 0 && ((uintptr_t)bias & 15) == 0,
+                  "conv2x2_subpixel: pointers must be 16-byte aligned");
+    const int64_t tiles_m = (Mp + 255) / 256, tiles_n = N / 256 + (N % 256 != 0);
+    EGG_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "conv2x2_subpixel: grid too large");
+    int lcpt = 0;
+    while ((64ll << lcpt) < Cin) ++lcpt;
+    const SubpixArgs spa{(const unsigned short*)bias, src, out, (unsigned short*)shadow, (int)H, (int)W, (int)Cin,
+                         (int)Cout};
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)(tiles_m * tiles_n));
+#define EGG_SPX(SP_, REP_)                                                                                      \
+    hipLaunchKernelGGL((k_conv3x3_gemm8<1, 0, false, 2, 2, SP_, REP_>), grid, dim3(512), 0, st,                 \
+                       (const unsigned short*)x, (const unsigned short*)w_packed, nullptr, (int)H, (int)W, (int)Cin, \
+                       lcpt, (int)Mp, (int)N, (int)tiles_n, nullptr, 0.0f, nullptr, nullptr, nullptr, spa)
+    if (src_f32) {
+        if (rep == 1) EGG_SPX(2, 1);
+        else if (rep == 2) EGG_SPX(2, 2);
+        else EGG_SPX(2, 4);
+    } else {
+        if (rep == 1) EGG_SPX(1, 1);
+        else if (rep == 2) EGG_SPX(1, 2);
+        else EGG_SPX(1, 4);
+    }
+#undef EGG_SPX
+    EGG_CHECK_LAUNCH("conv2x2_subpixel_nhwc");
     return EGGROLL_OK;
 }
 

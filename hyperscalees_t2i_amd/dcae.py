@@ -263,6 +263,11 @@ def subpixel_phase_weights(w3: torch.Tensor) -> torch.Tensor:
     return torch.cat(out, dim=0)
 
 
+# Up-block phase conv with the sub-pixel interleave + shortcut in its epilogue (one launch, no y4
+# intermediate; eggroll_conv2x2_subpixel_nhwc, bitwise equal to the two-launch form, which False selects)
+FUSED_SUBPIXEL = True
+
+
 class UpBlock(nn.Module):
     """DCUpBlock2d(interpolate=True, shortcut=True): nearest x2 + 3x3 conv + pixel-shuffle shortcut.
     Executed as a pad-1 2x2 conv with 4*Cout sub-pixel phase outputs on the LOW-resolution input
@@ -287,6 +292,8 @@ class UpBlock(nn.Module):
         if self.w4 is None:
             self.refresh_phase_weights()
         x = x.contiguous()
+        if self.w4p is not None and FUSED_SUBPIXEL and self.w4.shape[0] % 256 == 0:
+            return K.conv2x2_subpixel(x, self.w4p, x, bias=self.conv.bias)   # one launch, the same bits
         # bias-free phase conv; the conv bias is added in fp32 by the interleave kernel
         if self.w4p is not None:
             y4 = K.conv_nhwc(x, self.w4p, None, 2)
@@ -299,6 +306,10 @@ class UpBlock(nn.Module):
         shortcut reads the fp32 stream and writes the new fp32 stream and its shadow in one pass."""
         if self.w4 is None:
             self.refresh_phase_weights()
+        B, H, W, _ = x32.shape
+        if self.w4p is not None and FUSED_SUBPIXEL and self.w4.shape[0] % 256 == 0:
+            s16 = torch.empty((B, 2 * H, 2 * W, self.w4.shape[0] // 4), dtype=torch.bfloat16, device=x32.device)
+            return K.conv2x2_subpixel(x16, self.w4p, x32, bias=self.conv.bias, shadow=s16), s16
         if self.w4p is not None:
             y4 = K.conv_nhwc(x16, self.w4p, None, 2)
         else:

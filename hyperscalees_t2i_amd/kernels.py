@@ -937,6 +937,42 @@ def conv_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tens
     return out
 
 
+def conv2x2_subpixel(x: torch.Tensor, w4_packed: torch.Tensor, src: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                     shadow: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """DC-AE up-block in one launch (eggroll_conv2x2_subpixel_nhwc): the bias-free ks-2 phase conv of x
+    [B,H,W,Cin] bf16 (w4_packed [4*Cout][2][2][Cin]) with the sub-pixel interleave, bias and pixel-shuffle
+    shortcut from src in its epilogue -> [B,2H,2W,Cout].  src bf16 (= x): bf16 out; src fp32 (the DC-AE
+    fp32 residual stream): fp32 out and, when given, its bf16 shadow.  Bitwise equal to conv_nhwc(ks 2)
+    followed by subpixel_shortcut / subpixel_shortcut_f32."""
+    _dev(x, "conv2x2_subpixel(x)", torch.bfloat16)
+    _dev(w4_packed, "conv2x2_subpixel(w)", torch.bfloat16)
+    f32 = src.dtype == torch.float32
+    _dev(src, "conv2x2_subpixel(src)", torch.float32 if f32 else torch.bfloat16)
+    x = x.contiguous()
+    B, H, W, Cin = x.shape
+    N = w4_packed.shape[0]
+    if w4_packed.shape[1] != 4 * Cin or N % 4 or tuple(src.shape) != (B, H, W, Cin):
+        raise ValueError(f"conv2x2_subpixel: weight {tuple(w4_packed.shape)} / src {tuple(src.shape)} vs x {tuple(x.shape)}")
+    Cout = N // 4
+    if bias is not None:
+        _dev(bias, "conv2x2_subpixel(bias)", torch.bfloat16)
+        if bias.numel() != Cout:
+            raise ValueError(f"conv2x2_subpixel: bias has {bias.numel()} entries, Cout = {Cout}")
+    if shadow is not None:
+        if not f32:
+            raise ValueError("conv2x2_subpixel: shadow needs an fp32 src")
+        _dev(shadow, "conv2x2_subpixel(shadow)", torch.bfloat16)
+    if out is None:
+        out = torch.empty((B, 2 * H, 2 * W, Cout), dtype=src.dtype, device=x.device)
+    _dev(out, "conv2x2_subpixel(out)", src.dtype)
+    e0 = OpTimer.begin()
+    _lib.call("eggroll_conv2x2_subpixel_nhwc", x.data_ptr(), w4_packed.data_ptr(), _p(bias), src.data_ptr(), int(f32),
+              B, H, W, Cin, Cout, out.data_ptr(), _p(shadow), _stream(x.device))
+    OpTimer.end(e0, "conv2x2", 2.0 * x.numel() + out.element_size() * out.numel() + src.element_size() * src.numel(),
+                f"{tuple(x.shape)}->{N} px1 +subpixel", flops=2.0 * B * (H + 1) * (W + 1) * N * 4 * Cin)
+    return out
+
+
 def conv3x3_nhwc(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], px: int,
                  act: Optional[str] = None, out: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
     """3x3 conv (stride 1, pad 1) of x [B,H,W,Cin] NHWC bf16 with a pack_conv3x3_weight operand;

@@ -375,6 +375,16 @@ int eggroll_conv3x3_nhwc(const void* x, const void* w_packed, const void* bias, 
  * phase conv of the DC-AE up-blocks (see eggroll_subpixel_shortcut).                          */
 int eggroll_conv_nhwc(const void* x, const void* w_packed, const void* bias, int64_t B, int64_t H, int64_t W,
                       int64_t Cin, int64_t N, int32_t ks, int32_t px, int32_t act, void* y, void* stream);
+/* DC-AE up-block in one launch (round 5): the ks = 2 phase conv above with the sub-pixel interleave,
+ * bias and pixel-shuffle shortcut in its epilogue (no [B, H+1, W+1, 4*Cout] intermediate):
+ *   out[b, 2h+i, 2w+j, c] = bf16(y4[b, h+i, w+j, (2i+j)*Cout + c]) + bias[c] + src[b, h, w, (4c + 2i+j) / REP]
+ * REP = 4*Cout/Cin in {1, 2, 4}; y4 the bias-free phase conv of x (w_packed as eggroll_conv_nhwc, ks 2).
+ * src_f32 0: src [B,H,W,Cin] bf16 (= x), out bf16; 1: src fp32 (the DC-AE fp32 residual stream), out fp32
+ * and shadow (optional) its bf16 copy.  Bitwise equal to eggroll_conv_nhwc + eggroll_subpixel_shortcut(_f32).
+ * Cout % 64 == 0; pointers 16-byte aligned.                                                     */
+int eggroll_conv2x2_subpixel_nhwc(const void* x, const void* w_packed, const void* bias, const void* src,
+                                  int32_t src_f32, int64_t B, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                  void* out, void* shadow, void* stream);
 /* Kernel choice per call: 0 auto, 1 the tap-staged implicit GEMM (any shape above), 2 the halo-
  * staged kernel (ks 3, px 1, H % 16 == 0, and W % 32 == 0 with N == 128 or W % 16 == 0 with
  * N % 256 == 0: the input halo of a 16-row tile is staged once per 32-channel slice instead of once

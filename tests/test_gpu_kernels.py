@@ -1389,3 +1389,33 @@ def test_glumbconv_silu_placement_bitexact(dev, M_img, H, W, C, H2, ldo):
     h = K.lora_linear_pop(x, wi, bi, None, 0, 0, 0, 0.0, M)
     b = K.dwconv_nhwc(h.view(M_img, H, W, H2), wd, bd, 3, pre_silu=True, glu=True, ldo=ldo)
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,B,H,W", [(256, 128, 2, 12, 20), (128, 128, 1, 9, 7), (64, 64, 2, 5, 6),
+                                            (128, 64, 1, 8, 8), (256, 64, 2, 7, 11), (512, 256, 1, 16, 16)])
+@pytest.mark.parametrize("f32", [False, True])
+def test_conv2x2_subpixel_fused_bitexact(dev, cin, cout, B, H, W, f32):
+    """The up-block phase conv with the interleave + bias + shortcut in its epilogue
+    (eggroll_conv2x2_subpixel_nhwc, REP = 4 Cout / Cin in {1, 2, 4}) == conv_nhwc(ks 2) followed by
+    subpixel_shortcut / subpixel_shortcut_f32, bitwise (bf16 stream, and the fp32 stream + shadow);
+    ragged positions (H, W not tile multiples) and the dropped border positions of the phase grid."""
+    from hyperscalees_t2i_amd.dcae import subpixel_phase_weights
+    g = torch.Generator(device=dev).manual_seed(cin + cout + H)
+    w3 = torch.randn(cout, cin, 3, 3, device=dev, generator=g) * (9 * cin) ** -0.5
+    w4 = subpixel_phase_weights(w3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wp = K.pack_conv3x3_weight(w4, 1)
+    bias = (torch.randn(cout, device=dev, generator=g) * 0.1).bfloat16()
+    x = torch.randn(B, H, W, cin, device=dev, generator=g).bfloat16()
+    y4 = K.conv_nhwc(x, wp, None, 2)
+    if f32:
+        x32 = x.float() + torch.randn(B, H, W, cin, device=dev, generator=g) * 1e-3
+        s_ref = torch.empty(B, 2 * H, 2 * W, cout, device=dev, dtype=torch.bfloat16)
+        ref = K.subpixel_shortcut_f32(y4, x32, bias=bias, shadow=s_ref)
+        s_got = torch.empty_like(s_ref)
+        got = K.conv2x2_subpixel(x, wp, x32, bias=bias, shadow=s_got)
+        assert torch.equal(got, ref) and torch.equal(s_got, s_ref)
+    else:
+        ref = K.subpixel_shortcut(y4, x, bias=bias)
+        got = K.conv2x2_subpixel(x, wp, x, bias=bias)
+        assert torch.equal(got, ref)
