@@ -22,7 +22,8 @@ def main(pa, pb, rounds=7):
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     g = torch.Generator(device=dev).manual_seed(1)
     out = {}
-    for B, H, W, C, ks, pre, glu, pw in ((128, 32, 32, 11200, 3, 0, 1, False), (8, 128, 128, 4096, 3, 0, 1, False),
+    for B, H, W, C, ks, pre, glu, pw in ((128, 32, 32, 11200, 3, 0, 1, False), (128, 32, 32, 11200, 3, 1, 1, False),
+                                         (8, 128, 128, 4096, 3, 0, 1, False), (8, 128, 128, 4096, 3, 1, 1, False),
                                          (8, 64, 64, 8192, 3, 1, 1, False), (8, 128, 128, 1536, 5, 0, 0, True)):
         x = torch.randn(B, H, W, C, device=dev, generator=g).bfloat16()
         w = (torch.randn(ks * ks, C, device=dev, generator=g) * 0.2).bfloat16()
