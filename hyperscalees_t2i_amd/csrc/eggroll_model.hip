@@ -2103,7 +2103,7 @@ extern "C" int eggroll_dcae_head(const void* x, int64_t B, int64_t H, int64_t W,
                                  void* y, void* stream) {
     EGG_CHECK_ARG(B >= 0 && H > 0 && W > 0, "dcae_head: bad sizes");
     EGG_CHECK_ARG(C == HD_C, "dcae_head: C=%lld unsupported (%d)", (long long)C, HD_C);
-    EGG_CHECK_ARG(H * W * C < (1ll << 31), "dcae_head: image too large");
+    EGG_CHECK_ARG(H * W * C < (1ll << 30), "dcae_head: image too large (< 2 GiB per image: 32-bit buffer offsets)");
     if (B == 0) return EGGROLL_OK;
     EGG_CHECK_ARG(x && norm_w && norm_b && conv_w && y, "dcae_head: NULL pointer");
     EGG_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)norm_w & 15) == 0 && ((uintptr_t)norm_b & 15) == 0 &&
