@@ -1163,6 +1163,9 @@ def test_lora_gemm_epi_with_given_T_bitexact(dev, epi):
 
 @pytest.mark.parametrize("B,N,H,L,U,hd", [(4, 64, 2, 37, 2, 112), (3, 100, 3, 300, 3, 112), (6, 17, 1, 320, 2, 112),
                                            (16, 1024, 20, 300, 4, 112),
+                                           # the online softmax's key-half boundary (160 of 320 keys; 128 of 256)
+                                           (2, 33, 2, 160, 2, 112), (2, 33, 2, 161, 2, 112), (2, 65, 2, 129, 2, 128),
+                                           (2, 257, 16, 257, 2, 80),
                                            # Infinity text cross-attention: head dim 128, k / v interleaved in
                                            # one [U*L, 2C] row (mat_kv), -inf masks, rows -> text rows
                                            (8, 36, 4, 77, 4, 128), (6, 145, 2, 256, 3, 128), (5, 1, 3, 20, 2, 128)])
