@@ -592,7 +592,7 @@ def test_rownorm_fp32_residual_stream(dev):
     assert torch.equal(o16, o32.to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 37, 21), (1, 64, 64)])
+@pytest.mark.parametrize("B,H,W", [(2, 37, 21), (1, 64, 64), (1, 136, 18), (3, 9, 100)])  # band walks of 17 / 2 bands
 def test_dcae_head_matches_unfused(dev, B, H, W):
     """k_dcae_head (RMSNorm*w+b -> ReLU -> 3x3 conv 128->3 +bias, MFMA) vs the unfused rownorm kernel +
     torch conv2d and vs an fp32 restatement; ragged tiles (37 x 21) exercise the zero halo."""
