@@ -255,7 +255,9 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
             // KS = 5: every tap read from LDS and converted at its use.  A 5x5 fp32 register window
             // measured 11 % slower (2 vs 3 waves per SIMD, profiles/r05e_dw5_register_window_ab.log), and
             // row groups that convert each input row once for 2-4 output rows spill at 3 waves per SIMD
-            // next to the 25 taps' fp32 weights (r09 build, 172-500 B of scratch per lane).
+            // next to the 25 taps' fp32 weights (r09 build, 172-500 B of scratch per lane).  Staging the
+            // tile as fp32 (one conversion per staged element, 71.7 KB LDS -> 2 blocks per CU) measured
+            // 0.90x (366 -> 408 us at 8 x 128^2 x 1536, profiles/r10a_dw5_fp32_tile_ab.log).
 #pragma unroll 1
             for (int oy = 0; oy < DW_TH; ++oy) {
                 float acc[4];
