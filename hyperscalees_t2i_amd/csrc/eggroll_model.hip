@@ -729,6 +729,9 @@ __global__ __launch_bounds__(256) void k_subpixel_shortcut4(const unsigned short
 constexpr int LA_D = 32;
 constexpr int LA_PART = LA_D * LA_D + LA_D;   // kv + ksum floats per partial
 constexpr int LA_T = 256;                     // tokens per chunk
+#ifndef EGG_LA_HEAD_PAIRS
+#define EGG_LA_HEAD_PAIRS 1
+#endif
 
 // Pass 1 per (image*head, chunk of LA_T tokens) on MFMA: k (ReLU'd) and v staged into LDS token-major
 // as bf16 (all 8 loads per thread in flight), then kv^T-free: C[i][j] = sum_n v[n][i] relu(k[n][j]) as
@@ -753,84 +756,107 @@ __device__ __forceinline__ la_bf16x8 la_tr8(const unsigned short* base, int lane
     return __builtin_bit_cast(la_bf16x8, f);
 }
 
+// HP = 2 (contiguous heads, hstride == 32, even head count): a block stages one token chunk of a head
+// PAIR, so every k / v load covers a whole 128-B line (a token's 64 B of two neighbouring heads) instead
+// of relying on the neighbouring head's block to read the other half through L2; each head's MFMAs,
+// per-wave token split and partial sums are those of HP = 1 (the same bits).
+template <int HP>
 __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict__ k, const unsigned short* __restrict__ v,
                                                int64_t ld, int64_t hstride, int heads, int N, int nchunk, int relu,
                                                float* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) unsigned short lds_kv[2 * LA_T * LA_RS];  // sk | sv, then red
-    unsigned short* sk = lds_kv;
-    unsigned short* sv = lds_kv + LA_T * LA_RS;
-    float(*red)[LA_PART] = reinterpret_cast<float(*)[LA_PART]>(lds_kv);  // after the MFMAs
-    static_assert(4 * LA_PART * 4 <= 2 * LA_T * LA_RS * 2, "reduction buffer fits in the staging LDS");
+    __shared__ __attribute__((aligned(16))) unsigned short lds_kv[HP * 2 * LA_T * LA_RS];  // [head] sk | sv, then red
+    float(*red)[LA_PART] = reinterpret_cast<float(*)[LA_PART]>(lds_kv);  // [head * 4 + wave], after the MFMAs
+    static_assert(HP * 4 * LA_PART * 4 <= HP * 2 * LA_T * LA_RS * 2, "reduction buffer fits in the staging LDS");
     const int lb = xcd_remap(blockIdx.x, gridDim.x);  // adjacent heads share 128-B lines: same L2
-    const int bh = lb / nchunk, c = lb - bh * nchunk;
-    const int b = bh / heads, h = bh - b * heads;
+    const int bhp = lb / nchunk, c = lb - bhp * nchunk;
+    const int hg = heads / HP, b = bhp / hg, h0 = (bhp - b * hg) * HP;
     const int n0 = c * LA_T;
     const int cnt = (N - n0) < LA_T ? (N - n0) : LA_T;
     const int tid = threadIdx.x;
-    u16x8m kr[4], vr[4];
+    constexpr int U = 4 * HP;  // 16-B units per token and tensor (HP heads x 64 B)
+    u16x8m kr[U], vr[U];
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {  // LA_T tokens x 4 16-B chunks per tensor = 4 units per thread
-        const int u = tid + it * 256, t = u >> 2, q4 = u & 3;
+    for (int it = 0; it < U; ++it) {  // LA_T tokens x U units per tensor
+        const int u = tid + it * 256, t = u / U, q8 = u % U;
         kr[it] = vr[it] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
         if (t < cnt) {
-            const int64_t off = ((int64_t)b * N + n0 + t) * ld + (int64_t)h * hstride + q4 * 8;
+            const int64_t off = ((int64_t)b * N + n0 + t) * ld + (int64_t)h0 * hstride + (q8 >> 2) * hstride + (q8 & 3) * 8;
             kr[it] = *reinterpret_cast<const u16x8m*>(k + off);
             vr[it] = *reinterpret_cast<const u16x8m*>(v + off);
         }
     }
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int u = tid + it * 256, t = u >> 2, q4 = u & 3;
+    for (int it = 0; it < U; ++it) {
+        const int u = tid + it * 256, t = u / U, q8 = u % U;
+        unsigned short* sk = lds_kv + (q8 >> 2) * (2 * LA_T * LA_RS);
+        unsigned short* sv = sk + LA_T * LA_RS;
         if (relu) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) kr[it][i] = (kr[it][i] & 0x8000) ? (unsigned short)0 : kr[it][i];  // bf16 ReLU (-0 -> +0)
         }
-        *reinterpret_cast<u16x8m*>(sk + t * LA_RS + q4 * 8) = kr[it];
-        *reinterpret_cast<u16x8m*>(sv + t * LA_RS + q4 * 8) = vr[it];
+        *reinterpret_cast<u16x8m*>(sk + t * LA_RS + (q8 & 3) * 8) = kr[it];
+        *reinterpret_cast<u16x8m*>(sv + t * LA_RS + (q8 & 3) * 8) = vr[it];
     }
     __syncthreads();
     const int lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
     la_bf16x8 ones;
 #pragma unroll
     for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(r16 == 0 ? 1.0f : 0.0f);  // A row 0 = ones -> ksum
-    la_f32x4 acc[2][2], ks[2];
+    la_f32x4 acc[HP][2][2], ks[HP][2];
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-        ks[x] = la_f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int y = 0; y < 2; ++y) acc[x][y] = la_f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {  // this wave's 64 tokens as 2 K-steps of 32
-        const int t0 = w * 64 + s * 32;
-        la_bf16x8 av[2], bk[2];
+    for (int hh = 0; hh < HP; ++hh)
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
-            av[x] = la_tr8(sv + t0 * LA_RS + 16 * x, lane);  // A[i = 16x + r16][n]
-            bk[x] = la_tr8(sk + t0 * LA_RS + 16 * x, lane);  // B[n][j = 16x + r16]
+            ks[hh][x] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[hh][x][y] = la_f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
-        for (int x = 0; x < 2; ++x) {
+    for (int hh = 0; hh < HP; ++hh) {
+        const unsigned short* sk = lds_kv + hh * (2 * LA_T * LA_RS);
+        const unsigned short* sv = sk + LA_T * LA_RS;
 #pragma unroll
-            for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[x], bk[y], acc[x][y], 0, 0, 0);
-            ks[x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bk[x], ks[x], 0, 0, 0);
+        for (int s = 0; s < 2; ++s) {  // this wave's 64 tokens as 2 K-steps of 32
+            const int t0 = w * 64 + s * 32;
+            la_bf16x8 av[2], bk[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                av[x] = la_tr8(sv + t0 * LA_RS + 16 * x, lane);  // A[i = 16x + r16][n]
+                bk[x] = la_tr8(sk + t0 * LA_RS + 16 * x, lane);  // B[n][j = 16x + r16]
+            }
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+                    acc[hh][x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[x], bk[y], acc[hh][x][y], 0, 0, 0);
+                ks[hh][x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bk[x], ks[hh][x], 0, 0, 0);
+            }
         }
     }
     __syncthreads();  // every wave is done reading sk / sv: reuse the staging LDS for the reduction
     // C layout: lane holds C[4g + e][r16]
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int hh = 0; hh < HP; ++hh) {
+        float* rw = red[hh * 4 + w];
 #pragma unroll
-        for (int y = 0; y < 2; ++y)
+        for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) red[w][(16 * x + 4 * g + e) * LA_D + 16 * y + r16] = acc[x][y][e];
-    if (g == 0) {
+            for (int y = 0; y < 2; ++y)
 #pragma unroll
-        for (int y = 0; y < 2; ++y) red[w][LA_D * LA_D + 16 * y + r16] = ks[y][0];
+                for (int e = 0; e < 4; ++e) rw[(16 * x + 4 * g + e) * LA_D + 16 * y + r16] = acc[hh][x][y][e];
+        if (g == 0) {
+#pragma unroll
+            for (int y = 0; y < 2; ++y) rw[LA_D * LA_D + 16 * y + r16] = ks[hh][y][0];
+        }
     }
     __syncthreads();
-    float* dst = part + (int64_t)lb * LA_PART;  // slot bh * nchunk + c: k_la_reduce sums chunks in order
-    for (int e = tid; e < LA_PART; e += 256) dst[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+#pragma unroll
+    for (int hh = 0; hh < HP; ++hh) {
+        // slot bh * nchunk + c (bh = b * heads + h): k_la_reduce sums chunks in order
+        float* dst = part + ((int64_t)b * heads + h0 + hh) * nchunk * LA_PART + (int64_t)c * LA_PART;
+        const float(*r4)[LA_PART] = red + hh * 4;
+        for (int e = tid; e < LA_PART; e += 256) dst[e] = ((r4[0][e] + r4[1][e]) + r4[2][e]) + r4[3][e];
+    }
 }
 
 // Fixed-order sum of the nchunk partials of one (image, head) -> kvsum[bh], once per head: the
@@ -900,41 +926,47 @@ __device__ __forceinline__ void la_split8(const float (&f)[8], la_bf16x8& hi, la
 
 // Round 5: the denominator row ksum is written into A rows 0, 4, 8 and 12 (each lane group g then holds
 // den of its own token r16 as C[4g][r16] — the shuffle that broadcast row 0 is gone), a wave covers
-// LAO_TPW tiles of 16 tokens (the kv hi/lo split amortised over twice the tokens, twice the q loads in
+// TPW tiles of 16 tokens (the kv hi/lo split amortised over twice the tokens, twice the q loads in
 // flight), and q / out go through buffer descriptors (one per image, head offset in the base: 32-bit
 // offsets, tokens past N out of range).  Same MFMAs, same operands: the same bits.
-constexpr int LAO_TPW = 8;                     // 16-token tiles per wave
-constexpr int LAO_T = 4 * LAO_TPW * 16;        // tokens per block
+// TPW: 16-token tiles per wave (8; 16 at the DC-AE's 128^2 maps: 166 -> 154 us, r10c); HP = 2: a head
+// pair per block as in k_la_kv (each q load / output row a whole 128-B line), per-head math unchanged.
+template <int HP, int TPW>
 __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict__ q, int64_t ld, int64_t hstride,
                                                 int heads, int N, int nblk_tok, int relu, const float* __restrict__ kvsum,
                                                 unsigned short* __restrict__ out, int64_t ldo) {
+    constexpr int T = 4 * TPW * 16;  // tokens per block
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = lb / nblk_tok, c = lb - bh * nblk_tok;
-    const int b = bh / heads, h = bh - b * heads;
+    const int bhp = lb / nblk_tok, c = lb - bhp * nblk_tok;
+    const int hg = heads / HP, b = bhp / hg, h0 = (bhp - b * hg) * HP;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r16 = lane & 15, g = lane >> 4;
-    const int n0 = c * LAO_T + wave * (LAO_T / 4);
+    const int n0 = c * T + wave * (T / 4);
     // q tiles first (the longest latency), then kv from L2
     constexpr uint32_t OOR = 0x80000000u;
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(q + (int64_t)b * N * ld + (int64_t)h * hstride), (short)0, (int)((int64_t)N * ld * 2), 0x00020000);
-    u16x8m qr[LAO_TPW];
+        (void*)(q + (int64_t)b * N * ld + (int64_t)h0 * hstride), (short)0, (int)((int64_t)N * ld * 2), 0x00020000);
+    u16x8m qr[TPW][HP];
 #pragma unroll
-    for (int tt = 0; tt < LAO_TPW; ++tt) {
+    for (int tt = 0; tt < TPW; ++tt) {
         const int tok = n0 + tt * 16 + r16;
-        const uint32_t off = tok < N ? ((uint32_t)tok * (uint32_t)ld + 8 * g) * 2 : OOR;
-        qr[tt] = __builtin_bit_cast(u16x8m, __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, 0));
-    }
-    const float* kvh = kvsum + (int64_t)bh * LA_PART;
-    la_bf16x8 akv[2][2], aden[2];  // [feature block][hi, lo]
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-        const float4 x0 = *reinterpret_cast<const float4*>(kvh + (16 * cb + r16) * LA_D + 8 * g);
-        const float4 x1 = *reinterpret_cast<const float4*>(kvh + (16 * cb + r16) * LA_D + 8 * g + 4);
-        const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        la_split8(f, akv[cb][0], akv[cb][1]);
+        for (int hh = 0; hh < HP; ++hh) {
+            const uint32_t off = tok < N ? ((uint32_t)tok * (uint32_t)ld + (uint32_t)(hh * hstride) + 8 * g) * 2 : OOR;
+            qr[tt][hh] = __builtin_bit_cast(u16x8m, __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, 0));
+        }
     }
-    {
+    la_bf16x8 akv[HP][2][2], aden[HP][2];  // [head][feature block][hi, lo]
+#pragma unroll
+    for (int hh = 0; hh < HP; ++hh) {
+        const float* kvh = kvsum + ((int64_t)b * heads + h0 + hh) * LA_PART;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+            const float4 x0 = *reinterpret_cast<const float4*>(kvh + (16 * cb + r16) * LA_D + 8 * g);
+            const float4 x1 = *reinterpret_cast<const float4*>(kvh + (16 * cb + r16) * LA_D + 8 * g + 4);
+            const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            la_split8(f, akv[hh][cb][0], akv[hh][cb][1]);
+        }
         float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if ((r16 & 3) == 0) {  // A rows 0, 4, 8, 12 = ksum, the rest 0
             const float4 x0 = *reinterpret_cast<const float4*>(kvh + LA_D * LA_D + 8 * g);
@@ -942,36 +974,39 @@ __global__ __launch_bounds__(256) void k_la_out(const unsigned short* __restrict
             f[0] = x0.x; f[1] = x0.y; f[2] = x0.z; f[3] = x0.w;
             f[4] = x1.x; f[5] = x1.y; f[6] = x1.z; f[7] = x1.w;
         }
-        la_split8(f, aden[0], aden[1]);
+        la_split8(f, aden[hh][0], aden[hh][1]);
     }
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(out + (int64_t)b * N * ldo + h * LA_D), (short)0, (int)((int64_t)N * ldo * 2), 0x00020000);
+        (void*)(out + (int64_t)b * N * ldo + h0 * LA_D), (short)0, (int)((int64_t)N * ldo * 2), 0x00020000);
 #pragma unroll
-    for (int tt = 0; tt < LAO_TPW; ++tt) {
+    for (int tt = 0; tt < TPW; ++tt) {
         const int tok = n0 + tt * 16 + r16;
-        u16x8m qv = qr[tt];
-        if (relu) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) qv[e] = (qv[e] & 0x8000) ? (unsigned short)0 : qv[e];  // bf16 ReLU
-        }
-        const la_bf16x8 bq = *reinterpret_cast<const la_bf16x8*>(&qv);
-        la_f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, ad = a0;
-        a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[0][0], bq, a0, 0, 0, 0);
-        a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[0][1], bq, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[1][0], bq, a1, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[1][1], bq, a1, 0, 0, 0);
-        ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[0], bq, ad, 0, 0, 0);
-        ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[1], bq, ad, 0, 0, 0);
-        const float inv = 1.0f / (ad[0] + 1e-15f);  // C[4g][r16] = den of token r16 in every lane group
-        const uint32_t off = tok < N ? ((uint32_t)tok * (uint32_t)ldo + 4 * g) * 2 : OOR;
-        u16x4m o0, o1;
+        for (int hh = 0; hh < HP; ++hh) {
+            u16x8m qv = qr[tt][hh];
+            if (relu) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            o0[e] = f2b(a0[e] * inv);
-            o1[e] = f2b(a1[e] * inv);
+                for (int e = 0; e < 8; ++e) qv[e] = (qv[e] & 0x8000) ? (unsigned short)0 : qv[e];  // bf16 ReLU
+            }
+            const la_bf16x8 bq = *reinterpret_cast<const la_bf16x8*>(&qv);
+            la_f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, ad = a0;
+            a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[hh][0][0], bq, a0, 0, 0, 0);
+            a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[hh][0][1], bq, a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[hh][1][0], bq, a1, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akv[hh][1][1], bq, a1, 0, 0, 0);
+            ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[hh][0], bq, ad, 0, 0, 0);
+            ad = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aden[hh][1], bq, ad, 0, 0, 0);
+            const float inv = 1.0f / (ad[0] + 1e-15f);  // C[4g][r16] = den of token r16 in every lane group
+            const uint32_t off = tok < N ? ((uint32_t)tok * (uint32_t)ldo + (uint32_t)(hh * LA_D) + 4 * g) * 2 : OOR;
+            u16x4m o0, o1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o0[e] = f2b(a0[e] * inv);
+                o1[e] = f2b(a1[e] * inv);
+            }
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o0), ro, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o1), ro, off + 32, 0, 0);
         }
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o0), ro, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2m, o1), ro, off + 32, 0, 0);
     }
 }
 
@@ -2069,9 +2104,20 @@ extern "C" int eggroll_linear_attention(const void* q, const void* k, const void
     const int64_t blocks = B * heads * nchunk;
     EGG_CHECK_ARG(blocks < (1ll << 31), "linear_attention: grid too large");
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_la_kv, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)k,
-                       (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
-                       (float*)workspace);
+    // head pairs per block when a head's 64 B and its neighbour's are one 128-B line (Sana's q / k / v,
+    // the DC-AE's planar [Q | K | V]) and the grid stays large: Sana attn1 637 -> 615 us, the DC-AE's 128^2
+    // maps 154 -> 152; at 8 x 64^2 / 32^2 x 32 heads (4096 / 1024 per-head blocks) the halved grid lost
+    // 1-4 % (profiles/r10d_linear_attention_head_pairs_ab.log).  The reference-layout interleaved q | k | v
+    // (hstride 96) stays per head.
+    const int hp = hstride == LA_D && heads % 2 == 0 && blocks >= 8192 && EGG_LA_HEAD_PAIRS ? 2 : 1;
+    if (hp == 2)
+        hipLaunchKernelGGL(k_la_kv<2>, dim3((unsigned)(blocks / 2)), dim3(256), 0, st, (const unsigned short*)k,
+                           (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
+                           (float*)workspace);
+    else
+        hipLaunchKernelGGL(k_la_kv<1>, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)k,
+                           (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
+                           (float*)workspace);
     EGG_CHECK_LAUNCH("linear_attention_kv");
     float* kvsum = (float*)workspace + blocks * LA_PART;
     if (nchunk >= LA_RED_WIDE)
@@ -2081,9 +2127,18 @@ extern "C" int eggroll_linear_attention(const void* q, const void* k, const void
         hipLaunchKernelGGL(k_la_reduce, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const float*)workspace,
                            (int)nchunk, kvsum);
     EGG_CHECK_LAUNCH("linear_attention_reduce");
-    const int64_t oblk = (N + LAO_T - 1) / LAO_T;
-    hipLaunchKernelGGL(k_la_out, dim3((unsigned)(B * heads * oblk)), dim3(256), 0, st, (const unsigned short*)q, ld,
-                       hstride, (int)heads, (int)N, (int)oblk, relu_qk, (const float*)kvsum, (unsigned short*)out, ldo);
+    const bool big = N >= 8192;  // 16 tiles per wave at the DC-AE's 128^2 maps
+    const int64_t tpb = 4 * 16 * (big ? 16 : 8);
+    const int64_t oblk = (N + tpb - 1) / tpb;
+    const dim3 og((unsigned)(B * (heads / hp) * oblk));
+#define EGG_LAO(HP_, TPW_)                                                                                          \
+    hipLaunchKernelGGL((k_la_out<HP_, TPW_>), og, dim3(256), 0, st, (const unsigned short*)q, ld, hstride, (int)heads, \
+                       (int)N, (int)oblk, relu_qk, (const float*)kvsum, (unsigned short*)out, ldo)
+    if (hp == 2 && big) EGG_LAO(2, 16);
+    else if (hp == 2) EGG_LAO(2, 8);
+    else if (big) EGG_LAO(1, 16);
+    else EGG_LAO(1, 8);
+#undef EGG_LAO
     EGG_CHECK_LAUNCH("linear_attention_out");
     return EGGROLL_OK;
 }

@@ -675,6 +675,29 @@ def test_linear_attention_interleaved_relu(dev):
     assert rel < 8e-3, rel
 
 
+@pytest.mark.parametrize("B,N,heads,relu", [(8, 16384, 16, True), (32, 1024, 64, False), (4, 16500, 32, True)])
+def test_linear_attention_head_pairs_bitexact(dev, B, N, heads, relu):
+    """Contiguous heads (hstride 32, even head count: Sana's q / k / v, the DC-AE's planar [Q|K|V]) run as
+    head-pair blocks once the per-head grid has >= 8192 blocks (all three shapes); each head's output must
+    equal a one-head call on that head's columns (per-head blocks) bit for bit, and the fp32 restatement
+    within bf16 rounding.  N >= 8192 takes the 16-tile-per-wave output pass; 16500 ends on partial token
+    chunks and a partial output block."""
+    g = torch.Generator().manual_seed(B * N + heads)
+    inner = heads * 32
+    flat = torch.randn(B * N, 3 * inner, generator=g).to(torch.bfloat16).to(dev)
+    if not relu:
+        flat = flat.abs()   # keep the denominator away from 0 (as Sana's post-ReLU keys)
+    q, k, v = flat, flat[:, inner:], flat[:, 2 * inner:]
+    got = K.linear_attention(q, k, v, B, N, heads, 32, relu_qk=relu)
+    for h in range(heads):
+        one = K.linear_attention(q[:, 32 * h:], k[:, 32 * h:], v[:, 32 * h:], B, N, 1, 32, relu_qk=relu)
+        assert torch.equal(got[:, 32 * h:32 * h + 32], one), h
+    sh = (B, N, heads, 32)
+    ref = _linear_attention_ref(q[:, :inner].reshape(sh), k[:, :inner].reshape(sh), v[:, :inner].reshape(sh), relu)
+    rel = ((got.float().view(sh) - ref).norm() / ref.norm()).item()
+    assert rel < 8e-3, rel
+
+
 @pytest.mark.parametrize("B,H,W,C,ks", [(2, 9, 13, 96, 5), (1, 64, 64, 384, 5), (2, 20, 40, 64, 3)])
 def test_dwconv_pw_vs_torch(dev, B, H, W, C, ks):
     """Fused depthwise conv + grouped 1x1 (groups of 32) vs torch: conv2d(groups=C) in fp32 rounded to
