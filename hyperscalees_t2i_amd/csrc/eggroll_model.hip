@@ -1335,6 +1335,35 @@ __device__ __forceinline__ la_bf16x8 xa_tr8_perm(const unsigned short* base, int
     return __builtin_bit_cast(la_bf16x8, f);
 }
 
+// k / v rows of caption u, head h -> LDS (row stride HD + 8), rows >= L zero.  Every load of the thread
+// is issued before the first store: the strided loop this replaces waited for each 16-B pair in turn (one
+// memory latency per trip, ~9 trips with one workgroup per CU and nothing to overlap them).
+template <int HD, int LM, int NT>
+__device__ __forceinline__ void xa_stage_kv(const unsigned short* __restrict__ k, const unsigned short* __restrict__ v,
+                                            int64_t ldkv, int u, int h, int L, int tid, unsigned short* sk,
+                                            unsigned short* sv) {
+    constexpr int RS = HD + 8, CH = HD / 8, NCH = LM * CH, IT = (NCH + NT - 1) / NT;
+    u16x8m kr[IT], vr[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int c = tid + it * NT, r = c / CH, cc = c - r * CH;
+        kr[it] = vr[it] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+        if (c < NCH && r < L) {
+            const int64_t off = ((int64_t)u * L + r) * ldkv + (int64_t)h * HD + cc * 8;
+            kr[it] = *reinterpret_cast<const u16x8m*>(k + off);
+            vr[it] = *reinterpret_cast<const u16x8m*>(v + off);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int c = tid + it * NT, r = c / CH, cc = c - r * CH;
+        if (NCH % NT == 0 || c < NCH) {
+            *reinterpret_cast<u16x8m*>(sk + r * RS + cc * 8) = kr[it];
+            *reinterpret_cast<u16x8m*>(sv + r * RS + cc * 8) = vr[it];
+        }
+    }
+}
+
 template <int HD, int NWAVE, int QF, int LM = XA_LMAX>
 __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short* __restrict__ q, int64_t ldq,
                                                     const unsigned short* __restrict__ k,
@@ -1356,19 +1385,8 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
     const bool u_bad = u_in < 0 || u_in >= U;  // out-of-range caption row: NaN output, no out-of-bounds read
     const int u = u_bad ? 0 : u_in;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
-    // stage k / v rows of caption u, head h: 14 chunks of 16 B per row; rows >= L are zeros
-    constexpr int CH = HD / 8;
-    for (int c = tid; c < LM * CH; c += NT) {
-        const int r = c / CH, cc = c - r * CH;
-        u16x8m kv = u16x8m{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
-        if (r < L) {
-            const int64_t off = ((int64_t)u * L + r) * ldkv + (int64_t)h * HD + cc * 8;
-            kv = *reinterpret_cast<const u16x8m*>(k + off);
-            vv = *reinterpret_cast<const u16x8m*>(v + off);
-        }
-        *reinterpret_cast<u16x8m*>(sk + r * RS + cc * 8) = kv;
-        *reinterpret_cast<u16x8m*>(sv + r * RS + cc * 8) = vv;
-    }
+    // stage k / v rows of caption u, head h: HD / 8 chunks of 16 B per row; rows >= L are zeros
+    xa_stage_kv<HD, LM, NT>(k, v, ldkv, u, h, L, tid, sk, sv);
     for (int r = tid; r < LM; r += NT)
         sb[r] = u_bad ? __builtin_nanf("") : r < L ? (bias ? b2f(bias[(int64_t)u * L + r]) : 0.0f) : -INFINITY;
     __syncthreads();
@@ -1529,18 +1547,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn_h2(const unsigned sho
     const bool u_bad = u_in < 0 || u_in >= U;  // out-of-range caption row: NaN output, no out-of-bounds read
     const int u = u_bad ? 0 : u_in;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
-    constexpr int CH = HD / 8;
-    for (int c = tid; c < LM * CH; c += NT) {
-        const int r = c / CH, cc = c - r * CH;
-        u16x8m kv = u16x8m{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
-        if (r < L) {
-            const int64_t off = ((int64_t)u * L + r) * ldkv + (int64_t)h * HD + cc * 8;
-            kv = *reinterpret_cast<const u16x8m*>(k + off);
-            vv = *reinterpret_cast<const u16x8m*>(v + off);
-        }
-        *reinterpret_cast<u16x8m*>(sk + r * RS + cc * 8) = kv;
-        *reinterpret_cast<u16x8m*>(sv + r * RS + cc * 8) = vv;
-    }
+    xa_stage_kv<HD, LM, NT>(k, v, ldkv, u, h, L, tid, sk, sv);
     for (int r = tid; r < LM; r += NT)
         sb[r] = u_bad ? __builtin_nanf("") : r < L ? (bias ? b2f(bias[(int64_t)u * L + r]) : 0.0f) : -INFINITY;
     __syncthreads();
