@@ -380,13 +380,19 @@ def main():
     # PMC traffic was collected on the Sana epoch's LoRA-GEMM launch mix (tools/lora_epoch_driver.py):
     # it belongs to that workload's line only
     pmc = load_pmc_traffic() if args.workload == "sana" and not args.small else None
+    # the roofline kernel's own launch shape (131072 x 2240 x 2240, r 2; tools/gemm_mfma_driver.py), preferred
+    pmc_shape = load_pmc("pmc_lora_gemm_rooflineshape.json") if args.workload == "sana" and not args.small else None
     roofline = {"kernel": f"{dom_name} (population LoRA GEMM + fused LoRA epilogue)", "bound": "mfma",
                 "achieved": achieved, "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / BF16_DENSE_PEAK_TFLOPS,
-                "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                "traffic_measured_on": ("one epoch's LoRA-GEMM launch mix x2 (tools/lora_epoch_driver.py: every Sana "
-                                        "LoRA'd linear's shape, no epilogue op); profiles/pmc_lora_gemm.json")
-                                       if pmc else None,
+                "traffic": (pmc_shape or pmc or {}).get("hbm_bytes_per_launch"),
+                "traffic_measured_on": (("the roofline kernel's launch shape, 131072 x 2240 x 2240 r 2 "
+                                         "(tools/gemm_mfma_driver.py; FETCH_SIZE x 2 + WRITE_SIZE per launch); "
+                                         "profiles/pmc_lora_gemm_rooflineshape.json") if pmc_shape else
+                                        ("one epoch's LoRA-GEMM launch mix x2 (tools/lora_epoch_driver.py: every Sana "
+                                         "LoRA'd linear's shape, no epilogue op); profiles/pmc_lora_gemm.json")
+                                        if pmc else None),
+                "traffic_launch_mix": (pmc or {}).get("hbm_bytes_per_launch"),
                 "mfma_busy": mfma_busy_summary() if args.workload == "sana" and not args.small else None,
                 "launches": dom["launches"], "avg_launch_us": dom["avg_us"],
                 "flops_per_launch": dom["flops"] / max(dom["launches"], 1),
