@@ -2354,8 +2354,17 @@ __device__ __forceinline__ void conv_rmsnorm_epilogue(f32x4 (&acc)[8][4], float*
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) sq += acc[i][j][e] * acc[i][j][e];
-        sq += __shfl_xor(sq, 16, 64);
-        sq += __shfl_xor(sq, 32, 64);
+        // xor-16 then xor-32 butterfly on v_permlane16_swap / v_permlane32_swap (VALU; the ds_bpermute
+        // shuffles were LDS round trips): each returns the lane's own value and its partner's, whose sum
+        // is the butterfly step — the same additions, the same bits
+        {
+            const auto r16 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, sq),
+                                                              __builtin_bit_cast(unsigned, sq), false, false);
+            sq = __builtin_bit_cast(float, (unsigned)r16[0]) + __builtin_bit_cast(float, (unsigned)r16[1]);
+            const auto r32 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, sq),
+                                                              __builtin_bit_cast(unsigned, sq), false, false);
+            sq = __builtin_bit_cast(float, (unsigned)r32[0]) + __builtin_bit_cast(float, (unsigned)r32[1]);
+        }
         ss[i] = sq;
     }
     if (cg == 0)

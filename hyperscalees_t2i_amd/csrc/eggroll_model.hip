@@ -333,6 +333,23 @@ __device__ __forceinline__ float seg_sum(float v) {
     return v;
 }
 
+// Reductions over the 4 lane groups of 16 (xor 16, then xor 32) on v_permlane16_swap / v_permlane32_swap
+// instead of two ds_bpermute shuffles (LDS round trips): each swap returns the lane's own value and its
+// partner's, combined exactly as `v op __shfl_xor(v, 16)` then `op __shfl_xor(v, 32)` (+ and max are
+// commutative, so the same bits).
+__device__ __forceinline__ float g4_sum(float v) {
+    auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    v = __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+    r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ float g4_max(float v) {
+    auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    v = fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+    r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+    return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
 // ------------------------------------------------------------------------------------
 // Fused row normalisation over the channel (last) dim of a [rows, C] bf16 tensor:
 //   y = norm(x)                      RMS (x / sqrt(mean x^2 + eps)) or LayerNorm (centred)
@@ -1455,8 +1472,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
         float sum[QF];
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
-            mx[x] = fmaxf(mx[x], __shfl_xor(mx[x], 16));
-            mx[x] = fmaxf(mx[x], __shfl_xor(mx[x], 32));
+            mx[x] = g4_max(mx[x]);
             sum[x] = 0.0f;
         }
 #pragma unroll
@@ -1474,8 +1490,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn(const unsigned short*
         }
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
-            sum[x] += __shfl_xor(sum[x], 16);
-            sum[x] += __shfl_xor(sum[x], 32);
+            sum[x] = g4_sum(sum[x]);
         }
         // O^T[dim][query] = sum_keys V^T[dim][key] P^T[key][query]
         la_f32x4 oc[QF][DF];
@@ -1624,8 +1639,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn_h2(const unsigned sho
             float alpha[QF];
 #pragma unroll
             for (int x = 0; x < QF; ++x) {
-                lm[x] = fmaxf(lm[x], __shfl_xor(lm[x], 16));
-                lm[x] = fmaxf(lm[x], __shfl_xor(lm[x], 32));
+                lm[x] = g4_max(lm[x]);
                 const float mn = fmaxf(mx[x], lm[x]);
                 alpha[x] = half == 0 ? 0.0f : __expf(mx[x] - mn);
                 mx[x] = mn;
@@ -1676,8 +1690,7 @@ __global__ __launch_bounds__(64 * NWAVE) void k_cross_attn_h2(const unsigned sho
         }
 #pragma unroll
         for (int x = 0; x < QF; ++x) {
-            sum[x] += __shfl_xor(sum[x], 16);
-            sum[x] += __shfl_xor(sum[x], 32);
+            sum[x] = g4_sum(sum[x]);
             const int qrow = qb * 16 * QF + 16 * x + r16;
             if (qrow < N) {
                 const float inv = 1.0f / sum[x];
@@ -2339,8 +2352,7 @@ __global__ __launch_bounds__(256, QF == 1 ? 3 : (QF == 2 ? 2 : 1)) void k_flash_
 #pragma unroll
             for (int f = 1; f < KF; ++f)
                 mb = fmaxf(fmaxf(mb, fmaxf(sf[x][f][0], sf[x][f][1])), fmaxf(sf[x][f][2], sf[x][f][3]));
-            mb = fmaxf(mb, __shfl_xor(mb, 16));
-            mb = fmaxf(mb, __shfl_xor(mb, 32));
+            mb = g4_max(mb);
             const float mn = fmaxf(m[x], mb * scale_log2);
             if (__builtin_amdgcn_ballot_w64(mn != m[x])) {   // a running max moved: rescale this query set
                 const float alpha = __builtin_amdgcn_exp2f(m[x] - mn);   // 0 on the first block (m = -inf)
@@ -2387,8 +2399,7 @@ __global__ __launch_bounds__(256, QF == 1 ? 3 : (QF == 2 ? 2 : 1)) void k_flash_
 #pragma unroll
     for (int x = 0; x < QF; ++x) {
         float sum = l[x];
-        sum += __shfl_xor(sum, 16);
-        sum += __shfl_xor(sum, 32);
+        sum = g4_sum(sum);
         const int qr = q0 + 16 * x + r16;
         if (qr < Nq) {
             const float inv = 1.0f / sum;

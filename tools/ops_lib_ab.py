@@ -45,6 +45,19 @@ def cases(dev, g):
         inner = hd * 32
         out[f"linear_attention dcae {Bd}x{N} h{hd}"] = (lambda flat=flat, inner=inner, Bd=Bd, N=N, hd=hd:
             K.linear_attention(flat, flat[:, inner:], flat[:, 2 * inner:], Bd, N, hd, 32, True))
+    # DC-AE ResBlock conv2 + RMSNorm + residual (halo kernel, NORM epilogue): 128 ch at 1024^2, 256 ch at 512^2
+    for Bc, Hc, Cc in ((8, 1024, 128), (8, 512, 256)):
+        xc = r(Bc, Hc, Hc, Cc, sc=0.5)
+        wpk = r(Cc, 9 * Cc, sc=(9 * Cc) ** -0.5)
+        nwc, nbc, resc = r(Cc, sc=0.5), r(Cc, sc=0.1), r(Bc, Hc, Hc, Cc)
+        out[f"conv3x3_rmsnorm {Bc}x{Hc}^2x{Cc}"] = (lambda xc=xc, wpk=wpk, nwc=nwc, nbc=nbc, resc=resc:
+            K.conv3x3_rmsnorm_nhwc(xc, wpk, None, 1, 1e-6, nwc, nbc, resc))
+    # flash attention (head dim 128): Z-Image's joint sequence (4 images x 4096+512 tokens x 30 heads) and a
+    # ragged one (a partial key block, Nq not a multiple of the query tile)
+    for Bf, Nf, Hf in ((4, 4608, 30), (2, 1000, 8)):
+        qf, kf, vf = (r(Bf, Nf, Hf, 128, sc=0.5) for _ in range(3))
+        out[f"flash_attention {Bf}x{Nf} h{Hf}"] = (lambda qf=qf, kf=kf, vf=vf:
+            K.flash_attention(qf, kf, vf, 128 ** -0.5))
     h0 = r(16 * 257, 1280, dt=torch.float32)
     h = h0.clone()
     y, w2, b2 = r(16 * 257, 1280), r(1280, sc=0.5), r(1280, sc=0.1)
