@@ -274,6 +274,21 @@ def mfma_busy_summary():
                     "against the peak clock (the vendor 2.5 PF figure's)"}
 
 
+def seeded_valu_summary():
+    """Counter-measured VALU issue of the engine-default seeded ES kernels (profiles/pmc_es_seeded_valu.json, written
+    by tools/es_valu_summary.py from tools/pmc_es_valu.sh): the factors are regenerated inside perturb / update
+    (Philox4x32-10 + Box-Muller), so these launches are priced against the VALU issue rate beside their HBM bytes."""
+    d = load_pmc("pmc_es_seeded_valu.json")
+    if not d:
+        return None
+    return {"method": d.get("method"), "source": "profiles/pmc_es_seeded_valu.json", "groups": d.get("groups"),
+            "note": "valu_active = SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the share of SIMD-cycles "
+                    "issuing VALU work (quarter-rate 32x32->64 multiplies and transcendentals at their cost); "
+                    "valu_issue_2 = SQ_INSTS_VALU x 2 cycles / the same: every op at the full wave64 rate; "
+                    "valu_active_at_2.4GHz = the VALU-active SIMD-cycles over duration x 2.4 GHz x 1024 SIMDs (the "
+                    "peak clock; the GRBM window of a 15-30 us launch includes dispatch overhead)"}
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup(args)
@@ -495,6 +510,7 @@ def main():
             "aux_kernels": aux,
             "aux_kernels_pop64_per_gpu": aux64,
             "aux_kernels_other_configs_per_gpu": aux_cfg,
+            "aux_kernels_seeded_valu": seeded_valu_summary() if not args.small else None,
             "model_kernels": model_kernels,
         }
         print(json.dumps(line), flush=True)

@@ -44,6 +44,7 @@ SIGNATURES = {
     "eggroll_lora_workspace_bytes": (i64, [i64, i64, i32, i64]),
     "eggroll_lora_project": (C.c_int, [vp, i64, vp, i64, i64, i32, i64, i64, i64, vp, vp]),
     "eggroll_lora_project_multi": (C.c_int, [vp, i64, vp, i64, vp, i32, i32, i64, i64, i64, vp, vp]),
+    "eggroll_lora_delta_f32": (C.c_int, [vp, i64, vp, i64, vp, i64, i32, f32, i64, i64, i64, i64, vp, i64, vp]),
     "eggroll_dwconv_nhwc": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, i32, i32, i32, vp, vp]),
     "eggroll_rownorm": (C.c_int, [vp, i64, i64, f32, i32, vp, vp, vp, vp, i64, i64, i32, vp, vp, vp]),
     "eggroll_gated_residual": (C.c_int, [vp, vp, vp, i64, i64, i64, i64, vp]),

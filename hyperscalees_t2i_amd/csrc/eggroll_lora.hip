@@ -11,6 +11,7 @@
 //                    XOR-swizzled LDS, 2-stage pipeline) with the epilogue
 //                    + bias[n] + scale * sum_q T[row,q] * B_k[n,q]
 //   k_lora_expand  : Y += scale * T B_k^T  (for hosts that run the base GEMM elsewhere)
+#include <algorithm>
 #include "common.h"
 
 namespace eggroll {
@@ -1755,6 +1756,50 @@ __global__ __launch_bounds__(256) void k_lora_expand(const float* __restrict__ T
     }
 }
 
+// fp32 population LoRA term of LoRALinear.forward_fp32 (the time / guidance embedders, AdaLN modulation and
+// proj_out — the few small linears whose bf16 rounding moved whole members):
+//   y[m, :] += scale * (x[m, :] A_k^T) B_k^T,   k = m / rows_per_member,
+// A_k = A + k * lda_member as [R][K], B_k = B + k * ldb_member as [N][R] (the PEFT lora_A / lora_B layouts of
+// es_backend.py:193-200; member stride 0 = one adapter for every row).  One wave per row, grid-stride: the
+// skinny product T = x A_k^T as per-lane fp32 partial sums over k = lane + 64 i, reduced by a fixed xor
+// butterfly (a row's bits do not depend on the member count or the grid), then the rank-R expansion
+// y[m, n] + (T B_k^T)[n] * scale in PEFT's order (result + lora_B(lora_A(x)) * scaling).
+template <int R>
+__global__ __launch_bounds__(256) void k_lora_delta_f32(const float* __restrict__ x, int64_t ldx,
+                                                        const float* __restrict__ A, int64_t lda_m,
+                                                        const float* __restrict__ B, int64_t ldb_m, float scale,
+                                                        int64_t rows_per_member, int64_t M, int N, int K,
+                                                        float* __restrict__ y, int64_t ldy) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t m = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); m < M; m += nwaves) {
+        const int64_t kl = m / rows_per_member;
+        const float* xr = x + m * ldx;
+        const float* Ak = A + kl * lda_m;
+        float t[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) t[q] = 0.0f;
+#pragma unroll 4
+        for (int k = lane; k < K; k += 64) {
+            const float xv = xr[k];
+#pragma unroll
+            for (int q = 0; q < R; ++q) t[q] = fmaf(xv, Ak[(int64_t)q * K + k], t[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < R; ++q)
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) t[q] += __shfl_xor(t[q], o, 64);
+        const float* Bk = B + kl * ldb_m;
+        float* yr = y + m * ldy;
+        for (int n = lane; n < N; n += 64) {
+            float d = 0.0f;
+#pragma unroll
+            for (int q = 0; q < R; ++q) d = fmaf(t[q], Bk[(int64_t)n * R + q], d);
+            yr[n] = yr[n] + d * scale;
+        }
+    }
+}
+
 template <int R, int NI>
 static void launch_project_ra(const void* X, int64_t ldx, const float* tp, int64_t ldt, int64_t offA, int64_t rpm,
                               int64_t M, int64_t K, float* T, hipStream_t st) {
@@ -3346,6 +3391,31 @@ int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta
     hipLaunchKernelGGL(k_lora_expand, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, as_stream(stream), T,
                        theta_pop, ld_theta, offB, r, scale, rows_per_member, M, N, (unsigned short*)Y, ldy);
     EGG_CHECK_LAUNCH("lora_expand");
+    return EGGROLL_OK;
+}
+
+int eggroll_lora_delta_f32(const float* x, int64_t ldx, const float* A, int64_t lda_member, const float* B,
+                           int64_t ldb_member, int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
+                           int64_t K, float* y, int64_t ldy, void* stream) {
+    EGG_CHECK_ARG(r >= 1 && r <= 8, "lora_delta_f32: r=%d must be in [1, 8]", r);
+    EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0 && N < (1ll << 31) && K < (1ll << 31) && rows_per_member > 0,
+                  "lora_delta_f32: bad sizes M=%lld N=%lld K=%lld rows_per_member=%lld", (long long)M, (long long)N,
+                  (long long)K, (long long)rows_per_member);
+    EGG_CHECK_ARG(ldx >= K && ldy >= N && lda_member >= 0 && ldb_member >= 0, "lora_delta_f32: bad strides");
+    if (M == 0) return EGGROLL_OK;
+    EGG_CHECK_ARG(x && A && B && y, "lora_delta_f32: NULL pointer");
+    const int64_t blocks = std::min<int64_t>((M + 3) / 4, 2048);
+    hipStream_t st = as_stream(stream);
+#define EGG_DELTA(RV)                                                                                            \
+    case RV:                                                                                                     \
+        hipLaunchKernelGGL(k_lora_delta_f32<RV>, dim3((unsigned)blocks), dim3(256), 0, st, x, ldx, A, lda_member, \
+                           B, ldb_member, scale, rows_per_member, M, (int)N, (int)K, y, ldy);                    \
+        break;
+    switch (r) {
+        EGG_DELTA(1) EGG_DELTA(2) EGG_DELTA(3) EGG_DELTA(4) EGG_DELTA(5) EGG_DELTA(6) EGG_DELTA(7) EGG_DELTA(8)
+    }
+#undef EGG_DELTA
+    EGG_CHECK_LAUNCH("lora_delta_f32");
     return EGGROLL_OK;
 }
 

@@ -504,6 +504,31 @@ def lora_expand(T: torch.Tensor, theta_pop: torch.Tensor, offB: int, r: int, sca
     return y
 
 
+def lora_delta_f32(x: torch.Tensor, A: torch.Tensor, lda_member: int, B: torch.Tensor, ldb_member: int, r: int,
+                   scale: float, rows_per_member: int, y: torch.Tensor) -> torch.Tensor:
+    """y += scale * (x A_k^T) B_k^T in fp32 (eggroll_lora_delta_f32), k = row // rows_per_member; A / B point
+    at member 0's lora_A [r][K] / lora_B [N][r] (a theta_pop column slice or the module's own weights) with
+    member strides lda_member / ldb_member (0: one adapter for all rows).  x [M, K], y [M, N] fp32, rows with
+    unit column stride; y is updated in place and returned."""
+    _dev(x, "lora_delta_f32(x)", torch.float32, contiguous=False)
+    _dev(y, "lora_delta_f32(y)", torch.float32, contiguous=False)
+    _dev(A, "lora_delta_f32(A)", torch.float32, contiguous=False)
+    _dev(B, "lora_delta_f32(B)", torch.float32, contiguous=False)
+    M, Kd = x.shape
+    if y.shape[0] != M or x.stride(1) != 1 or y.stride(1) != 1:
+        raise ValueError(f"lora_delta_f32: x {tuple(x.shape)} / y {tuple(y.shape)} must have M rows of unit stride")
+    N = y.shape[1]
+    if M:
+        n_members = (M - 1) // rows_per_member + 1
+        for t, name, ld, need in ((A, "A", lda_member, r * Kd), (B, "B", ldb_member, N * r)):
+            # the last member's adapter must lie inside the tensor the pointer came from
+            if (n_members - 1) * ld + need > t.untyped_storage().nbytes() // 4 - t.storage_offset():
+                raise ValueError(f"lora_delta_f32: {name} too small for {n_members} members")
+    _lib.call("eggroll_lora_delta_f32", x.data_ptr(), x.stride(0), A.data_ptr(), lda_member, B.data_ptr(), ldb_member,
+              r, float(scale), rows_per_member, M, N, Kd, y.data_ptr(), y.stride(0), _stream(y.device))
+    return y
+
+
 class OpTimer:
     """Opt-in live timing of the model-side libeggroll kernels (bench.py's per-kernel HBM table):
     HIP events on the launching stream around each call + its ALGORITHMIC bytes (every input read

@@ -352,14 +352,14 @@ class LoRALinear(nn.Module):
         return self._w32
 
     def forward_fp32(self, x: torch.Tensor) -> torch.Tensor:
-        """The PEFT LoRA linear in fp32 (torch GEMMs on fp32 copies of the frozen weight): y = x W^T + b
-        + s (x A_k^T) B_k^T with member k's factors from the population context (rows member-major) or this
-        module's own lora_A / lora_B.  For the small-M linears whose outputs set a whole member's
+        """The PEFT LoRA linear in fp32: y = x W^T + b (the library fp32 GEMM on an fp32 copy of the frozen
+        weight) + s (x A_k^T) B_k^T (eggroll_lora_delta_f32, in place) with member k's factors from the
+        population context (rows member-major) or this module's own lora_A / lora_B.  For the small-M linears whose outputs set a whole member's
         behaviour — the time / guidance embedding and AdaLN modulation, and proj_out (the transformer
         output the reference rounds to fp16 only): their bf16 rounding was a measured source of
         member-differential error at sigma = 1e-2 (tools/drift_probe.py)."""
         shp = x.shape
-        x2 = x.reshape(-1, shp[-1]).float()
+        x2 = x.reshape(-1, shp[-1]).float().contiguous()
         M = x2.shape[0]
         W32, b32 = self._weight32()
         y = torch.nn.functional.linear(x2, W32, b32)
@@ -369,17 +369,26 @@ class LoRALinear(nn.Module):
             if M % n:
                 raise RuntimeError(f"{M} rows do not split over {n} members")
             tp = ctx.theta_pop
-            A = tp[:, self.theta_off_A:self.theta_off_A + self.r * self.in_features].view(n, self.r, self.in_features)
-            B = tp[:, self.theta_off_B:self.theta_off_B + self.out_features * self.r].view(n, self.out_features, self.r)
-            t = torch.bmm(x2.view(n, M // n, -1), A.transpose(1, 2))
-            y = y + self.scale * torch.bmm(t, B.transpose(1, 2)).view(M, -1)
+            if FP32_DELTA_KERNEL:
+                K.lora_delta_f32(x2, tp[:, self.theta_off_A:], tp.stride(0), tp[:, self.theta_off_B:], tp.stride(0),
+                                 self.r, self.scale, M // n, y)
+            else:
+                A = tp[:, self.theta_off_A:self.theta_off_A + self.r * self.in_features].view(n, self.r, -1)
+                B = tp[:, self.theta_off_B:self.theta_off_B + self.out_features * self.r].view(n, self.out_features, -1)
+                t = torch.bmm(x2.view(n, M // n, -1), A.transpose(1, 2))
+                y = y + self.scale * torch.bmm(t, B.transpose(1, 2)).view(M, -1)
         elif self.r:
-            A, B = self.lora_A.weight.detach(), self.lora_B.weight.detach()
-            y = y + self.scale * ((x2 @ A.t()) @ B.t())
+            A, B = self.lora_A.weight.detach().float().contiguous(), self.lora_B.weight.detach().float().contiguous()
+            K.lora_delta_f32(x2, A, 0, B, 0, self.r, self.scale, max(M, 1), y)
         y = y.view(*shp[:-1], self.out_features)
         for hook in self._forward_hooks.values():   # forward hooks see this path like __call__ (activation capture)
             hook(self, (x,), y)
         return y
+
+
+# LoRALinear.forward_fp32's population LoRA term on eggroll_lora_delta_f32 (True) or two torch bmm's (False, the
+# round-4 form: A/B measurement only)
+FP32_DELTA_KERNEL = True
 
 
 # Linears that read the same input (Sana attn1 to_q / to_k / to_v, attn2 to_k / to_v) get their LoRA

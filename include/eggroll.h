@@ -249,6 +249,16 @@ int eggroll_lora_project_multi(const void* X, int64_t ldx, const float* theta_po
 int eggroll_lora_expand(const float* T, const float* theta_pop, int64_t ld_theta, int64_t offB,
                         int32_t r, float scale, int64_t rows_per_member, int64_t M, int64_t N,
                         void* Y, int64_t ldy, void* stream);
+/* The PEFT LoRA term in fp32 for the few small linears the host keeps in fp32 (time / guidance embedders,
+ * AdaLN modulation, proj_out; es_backend.py:193-200 evaluated for all members at once):
+ *   y[m, :] += scale * (x[m, :] A_k^T) B_k^T,   k = m / rows_per_member,
+ * A_k = A + k * lda_member as [r][K] (lora_A), B_k = B + k * ldb_member as [N][r] (lora_B); member strides 0
+ * apply one adapter to every row.  x [M][ldx] fp32, y [M][ldy] fp32 (the base x W^T + b, updated in place).
+ * One wave per row: x A_k^T by a fixed-order wave reduction (a row's result does not depend on the member
+ * count), then y + (T B_k^T) * scale.  1 <= r <= 8. */
+int eggroll_lora_delta_f32(const float* x, int64_t ldx, const float* A, int64_t lda_member, const float* B,
+                           int64_t ldb_member, int32_t r, float scale, int64_t rows_per_member, int64_t M,
+                           int64_t N, int64_t K, float* y, int64_t ldy, void* stream);
 
 /* Model-side fused op of the Sana / DC-AE host (not part of the reference ES interface):
  * channels-last depthwise ks x ks conv (stride 1, zero pad ks/2) of in [B,H,W,C] bf16 with

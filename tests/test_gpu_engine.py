@@ -263,8 +263,9 @@ def test_gemm_timer_keeps_the_product_path_bits(dev):
         GemmTimer.reset(False)
     assert torch.equal(plain, timed)
     n_lora = sum(1 for m in be.es_model.transformer.modules() if getattr(m, "r", 0))
-    # six LoRA'd linears run fp32 torch GEMMs by design (LoRALinear.forward_fp32: the time / guidance embedders'
-    # linear_1 / linear_2, time_embed.linear, proj_out — DESIGN §3.2); every other one is a recorded launch
+    # six LoRA'd linears run in fp32 by design (LoRALinear.forward_fp32: the library fp32 GEMM + eggroll_lora_delta_f32
+    # for the time / guidance embedders' linear_1 / linear_2, time_embed.linear, proj_out — DESIGN §3.2); every
+    # other one is a recorded bf16 GEMM launch
     assert summ["all"]["launches"] == n_lora - 6 and summ["all"]["tflops"] > 0
     assert any(k.endswith(",4>") or k.endswith(",5>") for k in summ)   # the fp32-stream epilogue variants
 

@@ -1292,6 +1292,53 @@ def test_lora_project_multi_rejects_bad_args(dev):
         K.lora_project_multi(x, tp, [2], 1, 64)
 
 
+@pytest.mark.parametrize("M,Kd,N,r,rpm", [(128, 256, 2240, 2, 16), (37, 2240, 32, 1, 5), (512, 2240, 13440, 2, 64),
+                                          (64, 100, 70, 4, 64), (9, 3072, 129, 8, 3), (4096, 2240, 32, 2, 512)])
+def test_lora_delta_f32_vs_fp64(dev, M, Kd, N, r, rpm):
+    """eggroll_lora_delta_f32 (the fp32 LoRA term of LoRALinear.forward_fp32) vs the PEFT formula in fp64,
+    member factors read from a theta_pop column slice (rows member-major, ragged last member); each row equals
+    the same row run alone with that member's adapter at member stride 0 (bitwise: a row's reduction order does
+    not depend on the member count)."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + Kd + r)
+    n = -(-M // rpm)
+    offA, offB = 3, 3 + r * Kd + 5                  # unaligned slices, as theta offsets can be
+    ld = offB + N * r + 7
+    tp = torch.randn((n, ld), generator=g).to(dev)
+    x = torch.randn((M, Kd), generator=g).to(dev)
+    base = torch.randn((M, N), generator=g).to(dev)
+    scale = 4.0 / r
+    y = K.lora_delta_f32(x, tp[:, offA:], ld, tp[:, offB:], ld, r, scale, rpm, base.clone())
+    xd, td = x.double(), tp.double()
+    want = base.double().clone()
+    for k in range(n):
+        rows = slice(k * rpm, min(M, (k + 1) * rpm))
+        A = td[k, offA:offA + r * Kd].view(r, Kd)
+        B = td[k, offB:offB + N * r].view(N, r)
+        want[rows] += scale * ((xd[rows] @ A.t()) @ B.t())
+    bound = 4e-6 * (xd.abs() @ td[:, offA:offA + r * Kd].abs().view(n, r, Kd).amax(0).t()).amax() \
+        * td[:, offB:offB + N * r].abs().amax() * scale * r + 2e-7 * want.abs()
+    assert ((y.double() - want).abs() <= bound).all(), float((y.double() - want).abs().max())
+    for k in (0, n - 1):                            # the same rows alone, one adapter, stride 0
+        rows = slice(k * rpm, min(M, (k + 1) * rpm))
+        A = tp[k, offA:offA + r * Kd].contiguous()
+        B = tp[k, offB:offB + N * r].contiguous()
+        alone = K.lora_delta_f32(x[rows].contiguous(), A, 0, B, 0, r, scale, 1, base[rows].clone())
+        assert torch.equal(alone, y[rows])
+
+
+def test_lora_delta_f32_rejects_bad_args(dev):
+    x = torch.zeros((8, 64), device=dev)
+    y = torch.zeros((8, 32), device=dev)
+    A = torch.zeros(9 * 64, device=dev)
+    B = torch.zeros(9 * 32, device=dev)
+    with pytest.raises(K._lib.EggrollError, match="r=9"):
+        K.lora_delta_f32(x, A, 0, B, 0, 9, 1.0, 8, y)
+    with pytest.raises(ValueError, match="too small"):
+        K.lora_delta_f32(x, torch.zeros(2 * 64, device=dev), 2 * 64, B, 2 * 32, 2, 1.0, 4, y)  # member 1's A: past the end
+    with pytest.raises(K._lib.EggrollError, match="dtype"):
+        K.lora_delta_f32(x.bfloat16(), A, 0, B, 0, 1, 1.0, 8, y)
+
+
 def _integration_blocks():
     import re
     from pathlib import Path
