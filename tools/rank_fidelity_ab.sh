@@ -5,7 +5,7 @@ set -o pipefail
 tag=${1:-rank_ab}
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for seeds in 5:17 17:29; do
+for seeds in ${RANK_AB_SEEDS:-5:17 17:29}; do
   for kern in 1 0; do
     echo "== seeds $seeds kernel $kern" >> gpurun_out/$tag.log
     EGG_RANK_SEEDS=$seeds timeout -k 10 300 python3 -u -c "
