@@ -354,10 +354,11 @@ class LoRALinear(nn.Module):
     def forward_fp32(self, x: torch.Tensor) -> torch.Tensor:
         """The PEFT LoRA linear in fp32: y = x W^T + b (the library fp32 GEMM on an fp32 copy of the frozen
         weight) + s (x A_k^T) B_k^T (eggroll_lora_delta_f32, in place) with member k's factors from the
-        population context (rows member-major) or this module's own lora_A / lora_B.  For the small-M linears whose outputs set a whole member's
-        behaviour — the time / guidance embedding and AdaLN modulation, and proj_out (the transformer
-        output the reference rounds to fp16 only): their bf16 rounding was a measured source of
-        member-differential error at sigma = 1e-2 (tools/drift_probe.py)."""
+        population context (rows member-major) or this module's own lora_A / lora_B.  For the small-M
+        linears whose outputs set a whole member's behaviour — the time / guidance embedding and AdaLN
+        modulation, and proj_out (the transformer output the reference rounds to fp16 only): their bf16
+        rounding was a measured source of member-differential error at sigma = 1e-2 (DESIGN §3.2,
+        tools/drift_probe.py)."""
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).float().contiguous()
         M = x2.shape[0]

@@ -1337,6 +1337,8 @@ def test_lora_delta_f32_rejects_bad_args(dev):
         K.lora_delta_f32(x, torch.zeros(2 * 64, device=dev), 2 * 64, B, 2 * 32, 2, 1.0, 4, y)  # member 1's A: past the end
     with pytest.raises(K._lib.EggrollError, match="dtype"):
         K.lora_delta_f32(x.bfloat16(), A, 0, B, 0, 1, 1.0, 8, y)
+    empty = torch.zeros((0, 32), device=dev)                                   # no rows: a no-op
+    assert K.lora_delta_f32(torch.zeros((0, 64), device=dev), A, 0, B, 0, 1, 1.0, 8, empty).shape == (0, 32)
 
 
 def _integration_blocks():
