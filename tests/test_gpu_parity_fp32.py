@@ -51,14 +51,15 @@ BOUNDS = {   # ~1.5x the round-4 measurement (fp32 residual streams in the Sana 
 }
 S1_SCORE_ERR = 0.006
 KEYS = ("lora_rel", "eps_rel", "image_rel", "reward_abs", "S_abs")
-# test_rank_fidelity_over_seeds (sigma 1e-2, 24 epochs' seeds x 8 members, 672 member pairs): max |dS| at
-# ~1.3x the measurement; pooled Kendall tau >= 0.964 = at most 12 discordant pairs; best / worst member may
-# differ in at most 1 of the 24 epochs.  Measured (round 5, profiles/r11c_rank_fidelity_ab.log): 12 pairs,
-# best 1 / worst 1 miss, max |dS| 0.0120 with forward_fp32's LoRA term on eggroll_lora_delta_f32; 8 pairs with
-# the round-4 torch bmm form (the same bar held on its first 12 seeds: 5 pairs).  A pair count moves by a few
-# with any fp32-rounding-level change upstream, hence 24 seeds, not 12.
+# test_rank_fidelity_over_seeds (sigma 1e-2, 48 epochs' seeds x 8 members, 1344 member pairs): max |dS| at
+# ~1.2x the measurement; pooled Kendall tau >= 0.964 (round 4's bar, then on 12 seeds) = at most 24 discordant
+# pairs; best / worst member may differ in at most 2 of the 48 epochs (round 4: 1 of 12).  Measured (round 5,
+# profiles/r11c_rank_fidelity_ab.log + r11e_rank_fidelity_ab.log, four 12-seed sets): 18 pairs (8 + 4 + 4 + 2,
+# tau 0.973), best 2 / worst 1 miss, max |dS| 0.0135 with forward_fp32's LoRA term on eggroll_lora_delta_f32;
+# 16 pairs (5 + 3 + 6 + 2), best 2 / worst 2, max |dS| 0.0152 with the round-4 torch bmm form.  A 12-seed
+# count moves by a few with any fp32-rounding-level change upstream, hence 48 seeds.
 # The same bars at full model size: tests/test_gpu_parity_fullsize.py
-RANK_BOUNDS = {"S_abs": 0.016, "pooled_tau": 0.964, "best_worst_misses": 1}
+RANK_BOUNDS = {"S_abs": 0.016, "pooled_tau": 0.964, "best_worst_misses": 2}
 
 
 def kendall_tau(a, b):
@@ -228,8 +229,8 @@ def test_rank_fidelity_over_seeds(stack, dev, golden):
     stages = ("all", "transformer", "transformer+dcae", "towers")
     st = {k: {"disc": 0, "best": 0, "worst": 0, "S_abs": 0.0} for k in stages}
     taus, pairs, spread = [], 0, []
-    # 24 epochs' seeds, 672 member pairs (one pair = 0.003 of pooled tau); EGG_RANK_SEEDS=lo:hi re-draws them (A/B)
-    seeds = tuple(range(*map(int, os.environ.get("EGG_RANK_SEEDS", "5:29").split(":"))))
+    # 48 epochs' seeds, 1344 member pairs (one pair = 0.0015 of pooled tau); EGG_RANK_SEEDS=lo:hi re-draws them (A/B)
+    seeds = tuple(range(*map(int, os.environ.get("EGG_RANK_SEEDS", "5:53").split(":"))))
     for seed in seeds:
         info = be.step_sampling_info(seed)
         flat, m = info["flat_ids"], info["m"]
