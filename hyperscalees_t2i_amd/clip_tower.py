@@ -30,7 +30,7 @@ ACT = {"gelu": lambda x: F.gelu(x), "quick_gelu": lambda x: x * torch.sigmoid(1.
 
 class CLIPVisionTower:
     def __init__(self, model, pad_head_dim: bool = False, use_kernel: bool = True, fp32_residual: bool = True,
-                 fused_residual_ln: bool = True):
+                 fused_residual_ln: bool = True, fused_gelu: bool = True):
         vm = model.vision_model
         self.pad_head_dim = pad_head_dim
         self.fp32_residual = fp32_residual
@@ -43,6 +43,8 @@ class CLIPVisionTower:
         self.hd = self.C // self.heads
         self.patch = cfg.patch_size
         self.act = ACT[cfg.hidden_act]
+        # exact GELU in the fc1 GEMM's epilogue where fc1 runs on the 8-phase kernel (False: torch F.gelu, A/B)
+        self.fused_gelu = fused_gelu and cfg.hidden_act == "gelu"
         emb = vm.embeddings
         self.patch_w = emb.patch_embedding.weight.detach().reshape(self.C, -1).contiguous()     # [C, 3 p p]
         self.cls = emb.class_embedding.detach()
@@ -74,6 +76,17 @@ class CLIPVisionTower:
             x2 = x.reshape(-1, x.shape[-1]).contiguous()
             return K.lora_linear_pop(x2, w, b, None, 0, 0, 0, 0.0, x2.shape[0], kernel=8).view(*x.shape[:-1], w.shape[0])
         return F.linear(x, w, b)
+
+    def _fc1_act(self, y, L, ours: bool):
+        """act(fc1(y)).  On the 8-phase kernel an exact GELU (CLIP-H/14, hidden_act "gelu") runs in the GEMM's
+        epilogue (eggroll_lora_linear_pop_epi, epi 8): the same fp32 expression and erff as torch's GELU of
+        the bf16 fc1 output, so the same bits, without the separate pass over the [n T, 4C] activation."""
+        if ours and self.fused_gelu and y.dtype == torch.bfloat16 and L["w1"].shape[1] % 64 == 0:
+            from . import kernels as K
+            y2 = y.reshape(-1, y.shape[-1]).contiguous()
+            return K.lora_linear_pop_epi(y2, L["w1"], L["b1"], None, 0, 0, 0, 0.0, y2.shape[0], "gelu_erf",
+                                         kernel=8).view(*y.shape[:-1], L["w1"].shape[0])
+        return self.act(self._lin(y, L["w1"], L["b1"], ours))
 
     @staticmethod
     def _ln(mod, x):
@@ -127,7 +140,7 @@ class CLIPVisionTower:
             if fused:        # h += out_proj(o); y = LN2(h)  (h: [n, T, C], or the [CLS] rows [n, 1, C] strided)
                 h2 = h.view(n * T, C) if not last_i else h[:, 0]
                 y = ln_k(L["ln2"], h2, F.linear(o.reshape(-1, C), L["wo"], L["bo"]))
-                m = F.linear(self.act(self._lin(y, L["w1"], L["b1"], big and not last_i)), L["w2"], L["b2"])
+                m = F.linear(self._fc1_act(y, L, big and not last_i), L["w2"], L["b2"])
                 if not last_i:   # h += mlp(y); the next layer's LN1 in the same pass
                     y_next = ln_k(self.layers[i + 1]["ln1"], h2, m)
                 else:

@@ -783,7 +783,9 @@ __device__ __forceinline__ void lora_epilogue(f32x4 (&acc)[WTM / 16][WTN / 16], 
 // The same expressions as eggroll_gated_residual_f32, so fused == unfused bit for bit.
 //   EPI_GELU  : out = bf16(gelu_tanh(y))                   (Infinity / VAR ffn: fc1 -> GELU(tanh))
 //   EPI_MUL   : out = bf16(res * y)                        (Z-Image SwiGLU: silu(w1 x) * w3 x)
-enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3, EPI_RES32 = 4, EPI_GATED32 = 5, EPI_GELU = 6, EPI_MUL = 7 };
+//   EPI_GELU_ERF : out = bf16(gelu(y))                     (PickScore CLIP-H/14 mlp: fc1 -> exact GELU)
+enum { EPI_NONE = 0, EPI_SILU = 1, EPI_RES = 2, EPI_GATED = 3, EPI_RES32 = 4, EPI_GATED32 = 5, EPI_GELU = 6, EPI_MUL = 7,
+       EPI_GELU_ERF = 8 };
 struct EpiArgs {
     const unsigned short* res;
     int64_t ldr;
@@ -800,6 +802,12 @@ __device__ __forceinline__ float epi_gelu(float x) {
     constexpr float kKappa = 0.044715f;
     const float u = x + kKappa * (x * x * x);
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-kBeta2L * u));
+}
+// GELU, approximate = "none": x * 0.5 * (1 + erf(x / sqrt 2)) in fp32, the expression (and the erff) torch's
+// GeluCUDAKernelImpl evaluates on a bf16 tensor, so fused == F.gelu(bf16 GEMM output) bit for bit
+// (test_lora_linear_pop_gelu_erf_bitexact)
+__device__ __forceinline__ float epi_gelu_erf(float x) {
+    return x * 0.5f * (1.0f + erff(x * (float)M_SQRT1_2));
 }
 
 // x * sigmoid(x) on two values: the multiplies / add as packed fp32 ops (v_pk_mul_f32 / v_pk_add_f32),
@@ -829,6 +837,9 @@ __device__ __forceinline__ u16x8 epi_apply(u16x8 v, int row, int col, const EpiA
     } else if constexpr (EPI == EPI_GELU) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(epi_gelu(bf16_to_f32(v[u])));
+    } else if constexpr (EPI == EPI_GELU_ERF) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = f32_to_bf16(epi_gelu_erf(bf16_to_f32(v[u])));
     } else if constexpr (EPI == EPI_RES || EPI == EPI_GATED || EPI == EPI_MUL) {
         const u16x8 r = *reinterpret_cast<const u16x8*>(ea.res + (int64_t)row * ea.ldr + col);
         if constexpr (EPI == EPI_MUL) {
@@ -887,6 +898,7 @@ template <int EPI>
 __device__ __forceinline__ unsigned short epi_apply1(unsigned short v, int row, int col, const EpiArgs& ea) {
     if constexpr (EPI == EPI_SILU) return f32_to_bf16(epi_silu(bf16_to_f32(v)));
     if constexpr (EPI == EPI_GELU) return f32_to_bf16(epi_gelu(bf16_to_f32(v)));
+    if constexpr (EPI == EPI_GELU_ERF) return f32_to_bf16(epi_gelu_erf(bf16_to_f32(v)));
     if constexpr (EPI == EPI_RES) return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) + bf16_to_f32(v));
     if constexpr (EPI == EPI_MUL) return f32_to_bf16(bf16_to_f32(ea.res[(int64_t)row * ea.ldr + col]) * bf16_to_f32(v));
     if constexpr (EPI == EPI_GATED)
@@ -918,7 +930,7 @@ __device__ __forceinline__ void store_tile_t(f32x4 (&acc)[8][4], char* smem, int
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private tile)
     constexpr bool E32 = EPI == EPI_RES32 || EPI == EPI_GATED32;
     const bool full = m0 + rbase + 128 <= M && n0 + cbase + 64 <= N && (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0;
-    const bool epi_vec = EPI == EPI_NONE || EPI == EPI_SILU || EPI == EPI_GELU ||
+    const bool epi_vec = EPI == EPI_NONE || EPI == EPI_SILU || EPI == EPI_GELU || EPI == EPI_GELU_ERF ||
                          ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
                           ((EPI != EPI_GATED && EPI != EPI_GATED32) ||
                            ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0)));
@@ -1550,7 +1562,7 @@ __device__ __forceinline__ void store_tile_wg(f32x4 (&acc)[8][5], char* smem, in
     __syncthreads();
     constexpr bool E32 = EPI == EPI_RES32 || EPI == EPI_GATED32;
     const bool vec = (ldy & 7) == 0 && (((uintptr_t)Y) & 15) == 0 &&
-                     (EPI == EPI_NONE || EPI == EPI_SILU || EPI == EPI_GELU ||
+                     (EPI == EPI_NONE || EPI == EPI_SILU || EPI == EPI_GELU || EPI == EPI_GELU_ERF ||
                       ((ea.ldr & 7) == 0 && (((uintptr_t)ea.res) & 15) == 0 &&
                        ((EPI != EPI_GATED && EPI != EPI_GATED32) ||
                         ((ea.gstride & 7) == 0 && (((uintptr_t)ea.gate) & 15) == 0))));
@@ -2128,6 +2140,7 @@ static int launch_gemm8_epi(const void* X, int64_t ldx, const void* W, int64_t l
     switch (epi) {
         case EPI_SILU: EGG_GEMM8E_R(EPI_SILU); break;
         case EPI_GELU: EGG_GEMM8E_R(EPI_GELU); break;
+        case EPI_GELU_ERF: EGG_GEMM8E_R(EPI_GELU_ERF); break;
         case EPI_MUL: EGG_GEMM8E_R(EPI_MUL); break;
         case EPI_RES: EGG_GEMM8E_R(EPI_RES); break;
         case EPI_GATED: EGG_GEMM8E_R(EPI_GATED); break;
@@ -2180,6 +2193,7 @@ static int launch_gemm8n(const void* X, int64_t ldx, const void* W, int64_t ldw,
         case EPI_NONE: EGG_GEMM8N_R(EPI_NONE); break;
         case EPI_SILU: EGG_GEMM8N_R(EPI_SILU); break;
         case EPI_GELU: EGG_GEMM8N_R(EPI_GELU); break;
+        case EPI_GELU_ERF: EGG_GEMM8N_R(EPI_GELU_ERF); break;
         case EPI_MUL: EGG_GEMM8N_R(EPI_MUL); break;
         case EPI_RES: EGG_GEMM8N_R(EPI_RES); break;
         case EPI_GATED: EGG_GEMM8N_R(EPI_GATED); break;
@@ -3532,13 +3546,14 @@ static int epi_args_ok(const void* X, int64_t ldx, const void* W, int64_t ldw, i
                        int64_t M, int64_t N, int64_t K, const void* Y, int64_t ldy, int32_t epi, const void* res,
                        int64_t ldr, const void* gate, int64_t gstride, int64_t rows_per_group, int32_t kernel) {
     EGG_CHECK_ARG(kernel == 0 || kernel == 8 || kernel == 10, "lora_linear_pop_epi: kernel must be 0, 8 or 10");
-    EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_MUL, "lora_linear_pop_epi: epi=%d unknown", epi);
+    EGG_CHECK_ARG(epi >= EPI_SILU && epi <= EPI_GELU_ERF, "lora_linear_pop_epi: epi=%d unknown", epi);
     EGG_CHECK_ARG(r >= 0 && r <= 2, "lora_linear_pop_epi: r=%d (epilogue ops need r <= 2)", r);
     EGG_CHECK_ARG(r == 0 || rows_per_member >= 256, "lora_linear_pop_epi: rows_per_member must be >= 256 with r > 0");
     EGG_CHECK_ARG(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "lora_linear_pop_epi: need K %% 64 == 0");
     EGG_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldx >= K && ldw >= K && ldy >= N, "lora_linear_pop_epi: bad strides");
     EGG_CHECK_ARG(M < (1ll << 31) && N < (1ll << 31) && rows_per_member < (1ll << 31), "lora_linear_pop_epi: M/N too large");
-    EGG_CHECK_ARG(epi == EPI_SILU || epi == EPI_GELU || (res && ldr >= N), "lora_linear_pop_epi: res NULL or ldr < N");
+    EGG_CHECK_ARG(epi == EPI_SILU || epi == EPI_GELU || epi == EPI_GELU_ERF || (res && ldr >= N),
+                  "lora_linear_pop_epi: res NULL or ldr < N");
     EGG_CHECK_ARG((epi != EPI_GATED && epi != EPI_GATED32) || (gate && gstride >= N && rows_per_group > 0),
                   "lora_linear_pop_epi: bad gate");
     if (M == 0) return EGGROLL_OK;

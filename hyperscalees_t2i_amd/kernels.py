@@ -340,7 +340,7 @@ def lora_linear_pop(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tenso
     return out
 
 
-EPI = {None: 0, "silu": 1, "res": 2, "gated": 3, "res32": 4, "gated32": 5, "gelu": 6, "mul": 7}
+EPI = {None: 0, "silu": 1, "res": 2, "gated": 3, "res32": 4, "gated32": 5, "gelu": 6, "mul": 7, "gelu_erf": 8}
 
 
 def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], theta_pop: Optional[torch.Tensor],
@@ -349,7 +349,7 @@ def lora_linear_pop_epi(x: torch.Tensor, W: torch.Tensor, bias: Optional[torch.T
                         rows_per_group: int = 1, out: Optional[torch.Tensor] = None,
                         T_ws: Optional[torch.Tensor] = None, kernel: int = 0) -> torch.Tensor:
     """lora_linear_pop with an epilogue op on the bf16 output y (eggroll_lora_linear_pop_epi_sel):
-    "silu": silu(y); "gelu": gelu(y, approximate="tanh"); "mul": res * y; "res": res + y; "gated": res + gate[row // rows_per_group] * y.  With res given and
+    "silu": silu(y); "gelu": gelu(y, approximate="tanh"); "gelu_erf": gelu(y) (exact, torch's bits); "mul": res * y; "res": res + y; "gated": res + gate[row // rows_per_group] * y.  With res given and
     out None the result is written into res (in place, as the residual adds it replaces).
     "res32" / "gated32": res is the fp32 residual stream, updated in place (res + y /
     fma(gate, y, res), gate fp32); out (optional) receives its bf16 shadow; returns res.

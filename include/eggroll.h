@@ -165,6 +165,7 @@ int eggroll_update_seeded(uint64_t seed, const float* theta, const float* fitnes
  *   epi 5: res = fma(gate[row/rpg, :], y, res)     (res fp32, gate fp32; eggroll_gated_residual_f32)
  *   epi 6: Y = bf16(gelu_tanh(y))                  Infinity ffn fc1 -> GELU(tanh) (x * sigmoid(2k), <= 1 ulp)
  *   epi 7: Y = bf16(res * y)                       Z-Image SwiGLU silu(w1 x) * w3 x (res may alias Y)
+ *   epi 8: Y = bf16(gelu(y))                       PickScore CLIP-H/14 mlp fc1 -> exact (erf) GELU (= torch bits)
  * res [M, ldr] bf16 may alias Y; gate rows gstride apart.  epi 4 / 5: res is an fp32 stream updated in
  * place and Y (may be NULL) receives bf16(res).  Requires r <= 2 (and rows_per_member >= 256 when
  * r > 0) and K % 64 == 0: always an MFMA-addend 8-phase kernel.  epi 0 = linear_pop.               */

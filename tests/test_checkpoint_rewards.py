@@ -148,6 +148,20 @@ def test_clip_vision_tower_matches_transformers(dev, which):
     assert rel < 2e-2 and cos > 0.9995
 
 
+@pytest.mark.gpu
+def test_clip_h14_tower_fused_gelu_bitexact(dev):
+    """CLIP-H/14 at the epoch's batch (64 images: the 8-phase fc1 path): exact GELU in fc1's GEMM epilogue
+    gives the same image embeddings, bit for bit, as fc1 followed by torch's F.gelu."""
+    from hyperscalees_t2i_amd.clip_tower import CLIPVisionTower
+    from hyperscalees_t2i_amd.rewards import CLIP_H14, build_clip
+    model = build_clip(CLIP_H14, dev, seed=7)
+    g = torch.Generator(device=dev).manual_seed(3)
+    px = torch.randn((64, 3, 224, 224), generator=g, device=dev)
+    fused, plain = CLIPVisionTower(model, fused_gelu=True), CLIPVisionTower(model, fused_gelu=False)
+    assert fused.fused_gelu and not plain.fused_gelu
+    assert torch.equal(fused(px), plain(px))
+
+
 def test_var_checkpoint_roundtrip(tmp_path):
     """VarBackend save_lora / load_lora (shared adapter helpers) on CPU at a tiny VAR: the adapter holds
     every theta entry in parameter order — the mat_qkv LoRA entries the reference's F.linear bypasses

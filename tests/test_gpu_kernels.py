@@ -1005,6 +1005,27 @@ def test_full_size_sana_layout_properties(dev, pop):
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-8)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("r,M,N,Kd,rpm,kernel", [(0, 128 * 257, 5120, 1280, 128 * 257, 8), (0, 777, 200, 128, 777, 8),
+                                                 (0, 8192, 2304, 512, 8192, 10), (2, 2 * 8192, 2304, 512, 8192, 8),
+                                                 (2, 2 * 8192 + 100, 2240, 2240, 8192, 10)])
+def test_lora_linear_pop_gelu_erf_bitexact(dev, r, M, N, Kd, rpm, kernel):
+    """Epilogue 8 (exact GELU, the PickScore CLIP-H/14 fc1) == torch's F.gelu of the same kernel's bf16
+    output, bit for bit: the CLIP-H shape (128 images x 257 tokens, 1280 -> 5120), ragged M / N, both
+    8-phase tiles, with and without the LoRA term."""
+    g = torch.Generator(device=dev).manual_seed(M + N + r)
+    x = torch.randn((M, Kd), generator=g, device=dev).to(torch.bfloat16)
+    W = (torch.randn((N, Kd), generator=g, device=dev) * (2.0 / Kd ** 0.5)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=dev).to(torch.bfloat16)
+    tp = torch.randn((-(-M // rpm), Kd * r + N * r + 8), generator=g, device=dev) * 0.05 if r else None
+    y = K.lora_gemm(x, W, bias, K.lora_project(x, tp, 0, r, rpm), tp, Kd * r, r, 2.0, rpm, kernel=kernel) if r \
+        else K.lora_linear_pop(x, W, bias, None, 0, 0, 0, 0.0, M, kernel=kernel)
+    ref = torch.nn.functional.gelu(y)
+    out = K.lora_linear_pop_epi(x, W, bias, tp, 0, Kd * r, r, 2.0, rpm, "gelu_erf", kernel=kernel)
+    assert float(y.float().abs().max()) > 3.0          # the erf's tails are exercised
+    assert torch.equal(out, ref), int((out != ref).sum())
+
+
 @pytest.mark.parametrize("epi,r,M,N,Kd,rpm", [("silu", 0, 16384, 2304, 512, 16384), ("res", 2, 4 * 4096, 2240, 2240, 4096),
                                              ("gated", 2, 4 * 4096, 2240, 2240, 4096), ("gated", 1, 3 * 1000 + 200, 384, 256, 1000),
                                              ("res", 0, 777, 200, 128, 777), ("gelu", 2, 2 * 8192, 2304, 512, 8192),
