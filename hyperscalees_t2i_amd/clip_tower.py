@@ -30,7 +30,7 @@ ACT = {"gelu": lambda x: F.gelu(x), "quick_gelu": lambda x: x * torch.sigmoid(1.
 
 class CLIPVisionTower:
     def __init__(self, model, pad_head_dim: bool = False, use_kernel: bool = True, fp32_residual: bool = True,
-                 fused_residual_ln: bool = True, fused_gelu: bool = True):
+                 fused_residual_ln: bool = True, fused_gelu: bool = False):
         vm = model.vision_model
         self.pad_head_dim = pad_head_dim
         self.fp32_residual = fp32_residual
@@ -43,7 +43,10 @@ class CLIPVisionTower:
         self.hd = self.C // self.heads
         self.patch = cfg.patch_size
         self.act = ACT[cfg.hidden_act]
-        # exact GELU in the fc1 GEMM's epilogue where fc1 runs on the 8-phase kernel (False: torch F.gelu, A/B)
+        # exact GELU in the fc1 GEMM's epilogue where fc1 runs on the 8-phase kernel.  Off by default: measured
+        # 1.7x SLOWER than fc1 + torch's F.gelu (842 vs 361 + 137 us per CLIP-H fc1 at the epoch's batch,
+        # profiles/r12c_gelu_erf_epilogue_ab.txt) — ocml's erff is ~40 VALU ops per element and the 8-phase
+        # kernel's epilogue runs at one block per CU, exposed, where torch's pass runs at full occupancy
         self.fused_gelu = fused_gelu and cfg.hidden_act == "gelu"
         emb = vm.embeddings
         self.patch_w = emb.patch_embedding.weight.detach().reshape(self.C, -1).contiguous()     # [C, 3 p p]
@@ -78,9 +81,9 @@ class CLIPVisionTower:
         return F.linear(x, w, b)
 
     def _fc1_act(self, y, L, ours: bool):
-        """act(fc1(y)).  On the 8-phase kernel an exact GELU (CLIP-H/14, hidden_act "gelu") runs in the GEMM's
+        """act(fc1(y)).  With fused_gelu, an exact GELU (CLIP-H/14, hidden_act "gelu") runs in the 8-phase GEMM's
         epilogue (eggroll_lora_linear_pop_epi, epi 8): the same fp32 expression and erff as torch's GELU of
-        the bf16 fc1 output, so the same bits, without the separate pass over the [n T, 4C] activation."""
+        the bf16 fc1 output, so the same bits (measured slower, see __init__)."""
         if ours and self.fused_gelu and y.dtype == torch.bfloat16 and L["w1"].shape[1] % 64 == 0:
             from . import kernels as K
             y2 = y.reshape(-1, y.shape[-1]).contiguous()
