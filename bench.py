@@ -70,7 +70,8 @@ def parse():
     p.add_argument("--latent", type=int, default=32, help="32 -> 1024 px")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--small", action="store_true", help="tiny architecture (smoke only; not a valid metric)")
-    p.add_argument("--aux-out", type=str, default="", help="write per-phase / per-kernel details here")
+    p.add_argument("--aux-out", type=str, default="",
+                   help="write the full record (per-phase / per-kernel tables) here; default gpurun_out/bench_aux.json")
     p.add_argument("--workload", choices=("sana", "var_d16", "zimage", "infinity"), default="sana",
                    help="var_d16: BASELINE configs[0] (VAR-d16, LoRA r 4, 4 classes x 4 batches) on the GPU path; "
                         "zimage: configs[3] (Z-Image-Turbo, egg rank 4, one GPU's 16 of pop 128, 384 px, 7 steps); "
@@ -289,6 +290,76 @@ def seeded_valu_summary():
                     "peak clock; the GRBM window of a 15-30 us launch includes dispatch overhead)"}
 
 
+LINE_MAX_BYTES = 4096   # the driver reads the tail of stdout: the headline line stays small
+DEFAULT_AUX = ROOT / "gpurun_out" / "bench_aux.json"
+
+
+def algo_bytes(shape):
+    """bf16 X [M,K] + W [K,N] read once + Y [M,N] written once: the GEMM's algorithmic HBM bytes."""
+    try:
+        M, K, N = (int(v) for v in str(shape).split("x"))
+    except (TypeError, ValueError):
+        return None
+    return 2.0 * (M * K + K * N + M * N)
+
+
+def _r(x, nd=4):
+    return None if x is None else (round(float(x), nd) if isinstance(x, (int, float)) else x)
+
+
+def compact_line(full: dict, aux_path: str) -> dict:
+    """The one stdout line: headline keys, the roofline kernel's own figures and the CPU baseline's
+    value / cores / kind / one-line sample.  Everything else (per-kernel tables, in-product mix,
+    achievable peaks, per-variant MFMA-busy) lives in the aux JSON named in `details`."""
+    roof = full.get("roofline") or {}
+    mb = roof.get("mfma_busy") or {}
+    dom = str(roof.get("kernel", "")).split(" ")[0]
+    busy = None
+    for k, v in (mb.get("kernels") or {}).items():
+        if k.replace(" ", "") == dom.replace(" ", ""):
+            busy = v.get("mfma_busy_frac")
+    mix = roof.get("in_product_mix") or {}
+    croof = {"kernel": dom, "bound": roof.get("bound"), "achieved": _r(roof.get("achieved"), 2),
+             "peak": roof.get("peak"), "unit": roof.get("unit"), "frac": _r(roof.get("frac")),
+             "traffic": _r(roof.get("traffic"), 0), "algorithmic_bytes": _r(roof.get("algorithmic_bytes"), 0),
+             "avg_launch_us": _r(roof.get("avg_launch_us"), 2), "launches": roof.get("launches"),
+             "flops_per_launch": _r(roof.get("flops_per_launch"), 0), "mfma_busy": _r(busy),
+             "in_product_mix_frac": _r(mix.get("frac"))}
+    cpu = full.get("cpu_baseline")
+    ccpu = None
+    if cpu:
+        sample = " ".join(str(cpu.get("sample", "")).split())
+        ccpu = {"value": _r(cpu.get("value"), 6), "unit": cpu.get("unit"), "cores": cpu.get("cores"),
+                "kind": cpu.get("kind"), "sample": sample[:700]}
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config")
+    out = {k: full.get(k) for k in keep}
+    out["roofline"] = croof
+    out["cpu_baseline"] = ccpu
+    for k in ("theta_replicas_identical", "theta_final_sha16"):
+        if k in full:
+            out[k] = full[k]
+    out["details"] = aux_path
+    return out
+
+
+def emit(full: dict, gemm: dict, args) -> None:
+    """Write the full record to --aux-out (default gpurun_out/bench_aux.json), then print the compact
+    headline line LAST on stdout so a tail reader always sees it whole."""
+    aux = Path(args.aux_out) if args.aux_out else DEFAULT_AUX
+    try:
+        aux.parent.mkdir(parents=True, exist_ok=True)
+        aux.write_text(json.dumps({"line": full, "gemm": gemm}, indent=1, default=str))
+        aux_s = os.path.relpath(aux, ROOT) if aux.is_absolute() else str(aux)
+    except OSError as e:
+        log(f"aux write failed: {e}")
+        aux_s = None
+    line = json.dumps(compact_line(full, aux_s), separators=(",", ":"))
+    assert len(line.encode()) <= LINE_MAX_BYTES, len(line)
+    sys.stderr.flush()
+    print(line, flush=True)
+
+
 def main():
     args = parse()
     rank, world, local = dist_setup(args)
@@ -409,6 +480,7 @@ def main():
                                         if pmc else None),
                 "traffic_launch_mix": (pmc or {}).get("hbm_bytes_per_launch"),
                 "mfma_busy": mfma_busy_summary() if args.workload == "sana" and not args.small else None,
+                "algorithmic_bytes": algo_bytes(dom.get("shape")),
                 "launches": dom["launches"], "avg_launch_us": dom["avg_us"],
                 "flops_per_launch": dom["flops"] / max(dom["launches"], 1),
                 "window": {"epochs": n_roof, "ms_per_step": roof_ms_per_step,
@@ -445,9 +517,6 @@ def main():
             "roofline": roofline, "cpu_baseline": None, "phases_ms": phases, "aux_kernels": aux,
             "model_kernels": model_kernels,
         }
-        print(json.dumps(line), flush=True)
-        if args.aux_out:
-            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
     elif rank == 0 and args.workload == "infinity":
         c = backend.cfg
         line = {
@@ -466,9 +535,6 @@ def main():
             "roofline": roofline, "cpu_baseline": None, "phases_ms": phases, "aux_kernels": aux,
             "model_kernels": model_kernels,
         }
-        print(json.dumps(line), flush=True)
-        if args.aux_out:
-            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
     elif rank == 0 and args.workload == "var_d16":
         c = backend.cfg
         line = {
@@ -486,9 +552,6 @@ def main():
             "roofline": roofline, "cpu_baseline": None, "phases_ms": phases, "aux_kernels": aux,
             "model_kernels": model_kernels,
         }
-        print(json.dumps(line), flush=True)
-        if args.aux_out:
-            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
     elif rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "member-evals/s", "n_gpus": world, "steps": args.steps,
@@ -513,9 +576,8 @@ def main():
             "aux_kernels_seeded_valu": seeded_valu_summary() if not args.small else None,
             "model_kernels": model_kernels,
         }
-        print(json.dumps(line), flush=True)
-        if args.aux_out:
-            Path(args.aux_out).write_text(json.dumps({"line": line, "gemm": gemm}, indent=1))
+    if rank == 0:
+        emit(line, gemm, args)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

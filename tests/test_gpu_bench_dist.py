@@ -36,6 +36,8 @@ def test_bench_two_ranks_same_device(tmp_path):
     assert rc == 0, err_tail
     lines = [ln for ln in out.read_text().splitlines() if ln.startswith('{"metric"')]
     assert len(lines) == 1, (out.read_text()[-2000:], err_tail)     # rank 0 prints exactly one line
+    assert out.read_text().rstrip().splitlines()[-1] == lines[0]     # ... and it is the last stdout line
+    assert len(lines[0].encode()) <= 8192, len(lines[0])              # the driver parses the tail of stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["pop_total"] == 8 and line["config"]["pop_per_gpu"] == 4
     assert line["theta_replicas_identical"] is True
