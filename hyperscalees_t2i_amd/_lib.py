@@ -86,6 +86,8 @@ SIGNATURES = {
                                             vp, i64, i32, vp, i64, vp, i64, i64, i32, vp]),
     "eggroll_cross_attention": (C.c_int, [vp, i64, vp, vp, i64, vp, vp, i64, i64, i64, i64, i64, i64, f32, vp, i64,
                                          vp]),
+    "eggroll_cross_attention_sel": (C.c_int, [vp, i64, vp, vp, i64, vp, vp, i64, i64, i64, i64, i64, i64, f32, vp,
+                                             i64, i32, vp]),
     "eggroll_clip_preprocess": (C.c_int, [vp, i64, i64, i64, i64, i64, i64, i64, i32, vp, vp, i32, i32, i64, i64,
                                           i64, vp, vp, vp, vp, vp]),
 }

@@ -2613,10 +2613,14 @@ extern "C" int eggroll_group_norm_nhwc(const void* x, int64_t B, int64_t HW, int
     return EGGROLL_OK;
 }
 
-extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
-                                       const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
-                                       int64_t heads, int64_t head_dim, int64_t L, int64_t U, float scale, void* o,
-                                       int64_t ldo, void* stream) {
+// variant: 0 = automatic (the 32-query two-half online-softmax k_cross_attn_h2), 1 = the 16-query two-pass
+// k_cross_attn (one max / exp pass over all keys), 2 = k_cross_attn_h2 explicitly.  Both are exact softmax up
+// to fp32 rounding; the selector lets the full-size rank test score the same epochs through each form.
+extern "C" int eggroll_cross_attention_sel(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                                           const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
+                                           int64_t heads, int64_t head_dim, int64_t L, int64_t U, float scale, void* o,
+                                           int64_t ldo, int32_t variant, void* stream) {
+    EGG_CHECK_ARG(variant >= 0 && variant <= 2, "cross_attention: variant must be 0 (auto), 1 (two-pass) or 2 (online)");
     EGG_CHECK_ARG(head_dim == 64 || head_dim == 80 || head_dim == 112 || head_dim == 128, "cross_attention: head_dim "
                   "%lld unsupported (64, 80, 112, 128)", (long long)head_dim);
     // head dim 128 (Infinity's text cross-attention) stages at most 256 keys: k + v at 320 would not fit 160 KiB
@@ -2635,16 +2639,10 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
     // 8 waves x 16-query blocks (164 VGPRs, 2 waves per SIMD): measured 0.80 ms at the Sana attn2 shape
     // (B 128, N 1024, 20 heads, L 300) vs 0.94 for 4 waves x 32 queries and 1.27 for 4 x 16 (SDPA on
     // the gathered k / v with the mask: 1.53 ms)
-#ifndef EGG_XA_H2
-#define EGG_XA_H2 1   // 32-query blocks with the two-half online softmax (k_cross_attn_h2); 0 = k_cross_attn
-#endif
-#if EGG_XA_H2
-#define EGG_XA_KERNEL(HD_, LM_) (k_cross_attn_h2<HD_, 8, LM_>)
-#else
-#define EGG_XA_KERNEL(HD_, LM_) (k_cross_attn<HD_, 8, 1, LM_>)
-#endif
+    // default: 32-query blocks with the two-half online softmax (k_cross_attn_h2)
 #define EGG_XA(HD_, LM_)                                                                                         \
-    hipLaunchKernelGGL(EGG_XA_KERNEL(HD_, LM_), dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream),     \
+    hipLaunchKernelGGL(variant == 1 ? (k_cross_attn<HD_, 8, 1, LM_>) : (k_cross_attn_h2<HD_, 8, LM_>),           \
+                       dim3((unsigned)(B * heads)), dim3(512), 0, as_stream(stream),                              \
                        (const unsigned short*)q, ldq, (const unsigned short*)k, (const unsigned short*)v, ldkv,    \
                        (const unsigned short*)bias, enc_index, (int)heads, (int)N, (int)L, (int)U, scale, (unsigned short*)o, \
                        ldo)
@@ -2653,7 +2651,14 @@ extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k
     else if (head_dim == 80) EGG_XA(80, XA_LMAX);
     else EGG_XA(64, XA_LMAX);
 #undef EGG_XA
-#undef EGG_XA_KERNEL
     EGG_CHECK_LAUNCH("cross_attention");
     return EGGROLL_OK;
+}
+
+extern "C" int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                                       const void* bias, const int32_t* enc_index, int64_t B, int64_t N,
+                                       int64_t heads, int64_t head_dim, int64_t L, int64_t U, float scale, void* o,
+                                       int64_t ldo, void* stream) {
+    return eggroll_cross_attention_sel(q, ldq, k, v, ldkv, bias, enc_index, B, N, heads, head_dim, L, U, scale, o, ldo,
+                                       0, stream);
 }

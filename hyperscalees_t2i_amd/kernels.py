@@ -1066,6 +1066,11 @@ def bias_act_(y: torch.Tensor, bias: torch.Tensor, act: Optional[str]) -> torch.
     return y
 
 
+# eggroll_cross_attention_sel's kernel form: 0 automatic (online two-half softmax), 1 two-pass, 2 online.
+# The product runs 0; tests/test_gpu_rank_fidelity_fullsize.py scores the same epochs through 1 and 2.
+XATTN_VARIANT = 0
+
+
 def cross_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, N: int, heads: int, head_dim: int,
                     L: int, scale: float, bias: Optional[torch.Tensor] = None, enc_index: Optional[torch.Tensor] = None,
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -1100,8 +1105,9 @@ def cross_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, B: int, N
     elif U < B:
         raise ValueError(f"cross_attention: {U} caption rows for B={B} images without enc_index")
     e0 = OpTimer.begin()
-    _lib.call("eggroll_cross_attention", q.data_ptr(), q.stride(0), k.data_ptr(), v.data_ptr(), k.stride(0), _p(bias),
-              _p(ei), B, N, heads, head_dim, L, U, float(scale), out.data_ptr(), out.stride(0), _stream(q.device))
+    _lib.call("eggroll_cross_attention_sel", q.data_ptr(), q.stride(0), k.data_ptr(), v.data_ptr(), k.stride(0),
+              _p(bias), _p(ei), B, N, heads, head_dim, L, U, float(scale), out.data_ptr(), out.stride(0),
+              int(XATTN_VARIANT), _stream(q.device))
     OpTimer.end(e0, "cross_attention", 2.0 * (2 * B * N * heads * head_dim + 2 * k.shape[0] * heads * head_dim),
                 f"B{B} N{N} L{L}")
     return out

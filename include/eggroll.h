@@ -451,6 +451,12 @@ int eggroll_clip_preprocess(const void* img, int64_t n, int64_t H, int64_t W, in
 int eggroll_cross_attention(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv, const void* bias,
                             const int32_t* enc_index, int64_t B, int64_t N, int64_t heads, int64_t head_dim,
                             int64_t L, int64_t U, float scale, void* o, int64_t ldo, void* stream);
+/* The same with the kernel form chosen (variant 0: automatic = 2; 1: 16-query blocks, two-pass softmax over all
+ * keys; 2: 32-query blocks, online softmax over two key halves) — numerics / timing A/B.                */
+int eggroll_cross_attention_sel(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                                const void* bias, const int32_t* enc_index, int64_t B, int64_t N, int64_t heads,
+                                int64_t head_dim, int64_t L, int64_t U, float scale, void* o, int64_t ldo,
+                                int32_t variant, void* stream);
 
 /* GroupNorm over NHWC bf16 activations (+ SiLU when act = 1):
  *   y[b,p,c] = act((x[b,p,c] - mean[b,g]) * rstd[b,g] * w[c] + bias[c]),  g = c / (C / G)

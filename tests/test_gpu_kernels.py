@@ -1213,10 +1213,13 @@ def test_lora_gemm_epi_with_given_T_bitexact(dev, epi):
                                            # Infinity text cross-attention: head dim 128, k / v interleaved in
                                            # one [U*L, 2C] row (mat_kv), -inf masks, rows -> text rows
                                            (8, 36, 4, 77, 4, 128), (6, 145, 2, 256, 3, 128), (5, 1, 3, 20, 2, 128)])
-def test_cross_attention_vs_sdpa(dev, B, N, H, L, U, hd):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_cross_attention_vs_sdpa(dev, monkeypatch, B, N, H, L, U, hd, variant):
     """eggroll_cross_attention (MFMA, caption rows through enc_index, additive mask) vs fp32 SDPA on the
-    gathered k / v; ragged N, L not a multiple of 16/32, fully-valid and heavily-masked captions."""
+    gathered k / v; ragged N, L not a multiple of 16/32, fully-valid and heavily-masked captions.  Both
+    kernel forms: 0 = the product's online two-half softmax, 1 = the two-pass form."""
     import torch.nn.functional as F
+    monkeypatch.setattr(K, "XATTN_VARIANT", variant)
     g = torch.Generator(device=dev).manual_seed(B * 131 + L)
     q = torch.randn((B * N, H * hd), generator=g, device=dev).to(torch.bfloat16)
     if hd == 128:

@@ -12,9 +12,8 @@ casts, models/SanaSprint.py:122-160), one member at a time as unifed_es.py:159-2
   D = 1,515,456).  The injected eps is checked bit-exactly (sha256 of the reference's eps bytes), then
   every LoRA'd linear output, the transformer output, the image, the per-image reward and S are
   compared member by member.
-* test_fullsize_rank_fidelity: pop 8, the product's own counter-based noise (the same eps on both
-  sides), several epochs' seeds: S drift, pooled Kendall tau of the promptnorm fitness order, best /
-  worst member.
+* The fitness-rank fidelity at this size (12 epochs' seeds, pop 8, both cross-attention forms) is
+  tests/test_gpu_rank_fidelity_fullsize.py.
 
 Bounds ~1.5x the measurement ("full size")."""
 import hashlib
@@ -25,11 +24,9 @@ import numpy as np
 import pytest
 import torch
 
-from hyperscalees_t2i_amd import kernels as K
 from hyperscalees_t2i_amd.es import EggRollNoiser
 from hyperscalees_t2i_amd.es_step import aggregate_member_rewards
 from hyperscalees_t2i_amd.lora import LoRALinear
-from oracle import eggroll_oracle as O
 from oracle import member_eval_fp32 as R
 
 pytestmark = pytest.mark.gpu
@@ -40,15 +37,6 @@ BOUNDS = {"lora_rel": 6.5e-3,     # every LoRA'd linear output, ||y - y32|| / ||
           "image_rel": 0.055,     # decoded image (3.7 %: the bf16 1024-px DC-AE stages)
           "reward_abs": 5e-3,     # per-image combined reward (0.0032)
           "S_abs": 3e-3}          # S[k, j] (0.0018; member spread of S 0.029)
-# pooled over SEEDS x 28 member pairs: measured tau 1.0 (round 5, 4 seeds, profiles/r08c_fullsize_parity.txt)
-# and 0.982 after the cross-attention's online softmax: one discordant pair of 112, a worst-member swap
-# whose fp32 scores are 1.45x the epoch's score error apart (profiles/r09t_fullsize_rank_fidelity.log);
-# max |dS| 0.0017-0.0020 against a member spread of 0.013.  A bf16 build cannot order two members whose
-# fp32 fitness scores differ by less than its own score error, so every discordant pair and every best /
-# worst miss must be such a near-tie: its fp32 score gap at most NEAR_TIE x the epoch's largest
-# |score - score32| (the member-level error of the same epoch).
-RANK_BOUNDS = {"S_abs": 3e-3, "pooled_tau": 0.95, "near_tie": 2.0}
-SEEDS = (5, 6, 7, 8)
 DECODE_CHUNK = 4
 
 
@@ -172,62 +160,3 @@ def test_fullsize_member_eval_reference_noise(full, dev, golden, fp32_math, monk
     print("[fp32-parity-full] reference noise pop 2", json.dumps(report))
     for k, b in BOUNDS.items():
         assert worst[k] <= b, (k, worst[k], b, report)
-
-
-def test_fullsize_rank_fidelity(full, dev, fp32_math):
-    """Fitness order of 8 members over several epochs' seeds, product path (fused epilogues, shared
-    projections, the counter-based noise of kernel (1)) vs the fp32 restatement on the same eps."""
-    be, rewards, rewards32, theta = full
-    params, shapes = be.collect_lora_params()
-    sigma, pop, gs = 1e-2, 8, be.cfg.guidance_scale
-    noiser = EggRollNoiser(shapes, sigma=sigma, lr_scale=0.1, rank=1, use_antithetic=True)
-    disc = best = worst = pairs = 0
-    S_abs, taus, spread, tie_ratio = 0.0, [], [], 0.0
-    for seed in SEEDS:
-        fac = noiser.sample_factors(pop, dev, seed=seed)
-        eps = noiser.eps_from_factors(fac, pop)
-        tp = noiser.perturb(theta, fac, pop, 0, pop)
-        info = be.step_sampling_info(seed)
-        flat, m = info["flat_ids"], info["m"]
-        B = len(flat)
-        pe, am = be._gather(flat)
-        imgs = be.generate_population(flat, seed, gs, tp)
-        j_of = torch.tensor([info["pid_to_j"][p] for p in flat], device=dev)
-        feats = rewards.prompt_features(info["unique_texts"])
-        S = aggregate_member_rewards(rewards.score(imgs, j_of.repeat(pop), feats), flat, info["pid_to_j"], pop, m)[0]
-        del imgs
-        lat = be.es_model._latents(B, seed, be.cfg.height_latent, be.cfg.width_latent)
-        feats32 = rewards32.prompt_features(info["unique_texts"])
-        rows = []
-        for k in range(pop):
-            with torch.no_grad():
-                img32 = R.generate_fp32(be.es_model, theta + sigma * eps[k], pe, am, lat, gs,
-                                        decode_chunk=DECODE_CHUNK)[1]
-                rows.append(aggregate_member_rewards(rewards32.score(img32, j_of, feats32), flat, info["pid_to_j"],
-                                                     1, m)[0][0])
-            del img32
-        S32 = torch.stack(rows)
-        sc = K.fitness(S, True)["scores"].cpu().numpy()
-        sc32, _, _ = O.ref_promptnorm(S32.cpu().numpy())
-        t = kendall_tau(sc, sc32)
-        taus.append(round(float(t), 4))
-        o, o32 = np.argsort(sc, kind="stable"), np.argsort(sc32, kind="stable")
-        disc += round((1 - t) / 2 * (pop * (pop - 1) // 2))
-        best += int(o[-1] == o32[-1])
-        worst += int(o[0] == o32[0])
-        err = float(np.abs(sc - sc32).max())
-        gaps = [abs(sc32[i] - sc32[j]) for i in range(pop) for j in range(i + 1, pop)
-                if np.sign(sc[i] - sc[j]) * np.sign(sc32[i] - sc32[j]) < 0]
-        gaps += [sc32[o32[-1]] - sc32[o[-1]], sc32[o[0]] - sc32[o32[0]]]   # best / worst misses (0 if none)
-        tie_ratio = max(tie_ratio, float(max(gaps)) / max(err, 1e-12))
-        pairs += pop * (pop - 1) // 2
-        S_abs = max(S_abs, float((S - S32).abs().max()))
-        spread.append(float(S32.std(0).mean()))
-    report = {"sigma": sigma, "seeds": list(SEEDS), "kendall_tau": taus, "pooled_tau": round(1 - 2 * disc / pairs, 4),
-              "discordant_pairs": disc, "pairs": pairs, "best_same": best, "worst_same": worst,
-              "S_abs_max": round(S_abs, 6), "S_member_spread_mean": round(float(np.mean(spread)), 6),
-              "misorder_gap_over_score_err": round(tie_ratio, 4)}
-    print("[fp32-parity-full] rank fidelity", json.dumps(report))
-    assert S_abs <= RANK_BOUNDS["S_abs"], report
-    assert report["pooled_tau"] >= RANK_BOUNDS["pooled_tau"], report
-    assert tie_ratio <= RANK_BOUNDS["near_tie"], report   # every misorder / best-worst miss is a near-tie
