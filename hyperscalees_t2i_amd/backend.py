@@ -12,7 +12,7 @@ from __future__ import annotations
 import json
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
 
@@ -91,8 +91,9 @@ class SanaConfig:
     vae_chunk: int = 8
     # members per population pass (ESEngine): 8 keeps every GEMM operand of the 1024-px forward under the
     # 32-bit buffer range (the FFN's 16-image x 1024-token x 5632 hidden map is 184 MB per member: 11
-    # members reach 2 GiB) and fixes the batch a member is evaluated in, so theta' does not depend on how
-    # many ranks share the population (configs[2]: 8 ranks x 8 == one process x 64)
+    # members reach 2 GiB) and fixes the batch a member is evaluated in: passes sit on global member
+    # indices (ESEngine.member_passes), so theta' does not depend on how many ranks share the population
+    # when every shard boundary is a multiple of it (configs[2]: 8 ranks x 8 == one process x 64)
     members_per_pass: int = 8
     synthetic_prompts: int = 4        # used when encoded_prompt_path is empty
     lora_b_std: float = 0.02          # nonzero B so the LoRA path is live
@@ -235,22 +236,30 @@ class SanaBackend(ESBackend):
 # ---------------------------------------------------------------------------------------
 
 
-def _save_adapter(model: torch.nn.Module, save_dir: Path, cfg_dict: Dict[str, Any]) -> None:
+def _adapter_keys(model: torch.nn.Module, rename: Optional[Callable[[str], str]] = None) -> Dict[str, torch.Tensor]:
+    """PEFT save_pretrained key names of the model's trainable (LoRA) parameters: base_model.model.<name>,
+    <name> the wrapped module's own parameter name (`rename` maps a build name to it where the build's
+    module tree differs from the reference's, e.g. the FLUX VAE decoder)."""
+    rn = rename or (lambda n: n)
+    return {f"base_model.model.{rn(n)}": p for n, p in model.named_parameters() if p.requires_grad}
+
+
+def _save_adapter(model: torch.nn.Module, save_dir: Path, cfg_dict: Dict[str, Any],
+                  rename: Optional[Callable[[str], str]] = None) -> None:
     from safetensors.torch import save_file
     save_dir = Path(save_dir)
     save_dir.mkdir(parents=True, exist_ok=True)
-    tensors = {f"base_model.model.{n}": p.detach().float().cpu().contiguous()
-               for n, p in model.named_parameters() if p.requires_grad}
+    tensors = {k: p.detach().float().cpu().contiguous() for k, p in _adapter_keys(model, rename).items()}
     save_file(tensors, str(save_dir / "adapter_model.safetensors"))
     (save_dir / "adapter_config.json").write_text(json.dumps(cfg_dict, indent=2))
 
 
-def _load_adapter(model: torch.nn.Module, save_dir: Path) -> None:
+def _load_adapter(model: torch.nn.Module, save_dir: Path, rename: Optional[Callable[[str], str]] = None) -> None:
     """Copy save_dir/adapter_model.safetensors back into the model's LoRA parameters.  Every trainable
     parameter must be present with its shape, and no extra key may exist (ValueError otherwise)."""
     from safetensors.torch import load_file
     tensors = load_file(str(Path(save_dir) / "adapter_model.safetensors"))
-    want = {f"base_model.model.{n}": p for n, p in model.named_parameters() if p.requires_grad}
+    want = _adapter_keys(model, rename)
     if set(tensors) != set(want):
         raise ValueError(f"adapter keys differ: missing {sorted(set(want) - set(tensors))[:3]}, "
                          f"unexpected {sorted(set(tensors) - set(want))[:3]}")
@@ -512,14 +521,18 @@ class ZImageBackend(ESBackend):
         _save_adapter(self.es_model.transformer, Path(save_dir) / "transformer",
                       self._adapter_cfg(c.lora_r, c.lora_alpha, c.lora_dropout, c.lora_target_modules))
         if c.use_vae_decoder_lora:
+            # PEFT wraps pipe.vae.decoder (es_backend.py:598-608): keys carry diffusers' Decoder names
+            # (base_model.model.mid_block.attentions.0.to_q.lora_A.weight), not flux_vae.py's (mid.1...)
+            from .checkpoints import flux_decoder_name
             _save_adapter(self.es_model.vae, Path(save_dir) / "vae_decoder",
                           self._adapter_cfg(c.vae_lora_r, c.vae_lora_alpha, c.vae_lora_dropout,
-                                            c.vae_lora_target_modules))
+                                            c.vae_lora_target_modules), rename=flux_decoder_name)
 
     def load_lora(self, save_dir: Path) -> None:
         _load_adapter(self.es_model.transformer, Path(save_dir) / "transformer")
         if self.cfg.use_vae_decoder_lora:
-            _load_adapter(self.es_model.vae, Path(save_dir) / "vae_decoder")
+            from .checkpoints import flux_decoder_name
+            _load_adapter(self.es_model.vae, Path(save_dir) / "vae_decoder", rename=flux_decoder_name)
 
     def _total_prompts(self) -> int:
         pe = self.base_prompt_embeds

@@ -357,21 +357,22 @@ def zimage_rules(model: nn.Module) -> List[Rule]:
     return [_same(n) for n in _frozen_params(model)]
 
 
+def flux_decoder_name(n: str) -> str:
+    """A flux_vae.py parameter name -> the diffusers `Decoder` module's own name for it (relative to
+    vae.decoder): mid.0 / mid.1 / mid.2 -> mid_block.resnets.0 / mid_block.attentions.0 /
+    mid_block.resnets.1, up_blocks.i.upsample.* -> up_blocks.i.upsamplers.0.conv.*, the rest as is."""
+    head, _, rest = n.partition(".")
+    if head == "mid":
+        i, _, leaf = rest.partition(".")
+        return {"0": "mid_block.resnets.0.", "2": "mid_block.resnets.1.", "1": "mid_block.attentions.0."}[i] + leaf
+    if head == "up_blocks" and ".upsample." in n:
+        i = rest.split(".")[0]
+        return f"up_blocks.{i}.upsamplers.0.conv.{n.rsplit('.', 1)[1]}"
+    return n
+
+
 def flux_vae_rules(vae: nn.Module) -> List[Rule]:
-    rules: List[Rule] = []
-    for n in _frozen_params(vae):
-        head, _, rest = n.partition(".")
-        if head == "mid":
-            i, _, leaf = rest.partition(".")
-            dn = {"0": "decoder.mid_block.resnets.0.", "2": "decoder.mid_block.resnets.1.",
-                  "1": "decoder.mid_block.attentions.0."}[i] + leaf
-        elif head == "up_blocks" and ".upsample." in n:
-            i = rest.split(".")[0]
-            dn = f"decoder.up_blocks.{i}.upsamplers.0.conv.{n.rsplit('.', 1)[1]}"
-        else:
-            dn = f"decoder.{n}"
-        rules.append(_same(n, dn))
-    return rules
+    return [_same(n, "decoder." + flux_decoder_name(n)) for n in _frozen_params(vae)]
 
 
 def zimage_arch_from_config(cfg: dict):

@@ -288,11 +288,19 @@ class UpBlock(nn.Module):
         self.w4p = (K.pack_conv3x3_weight(self.w4, 1)
                     if 64 <= cin <= 2048 and cin & (cin - 1) == 0 and self.w4.shape[0] % 64 == 0 else None)
 
+    def fused_ok(self) -> bool:
+        """eggroll_conv2x2_subpixel_nhwc's shape rule (Cin a power of two in [64, 2048] — already required
+        for w4p —, 4*Cout a multiple of 256 and <= 8192, 4*Cout / Cin in {1, 2, 4}); other widths take the
+        two-launch conv + subpixel_shortcut form."""
+        n4, cin = self.w4.shape[0], self.w4.shape[1]
+        return (self.w4p is not None and FUSED_SUBPIXEL and n4 % 256 == 0 and n4 <= 8192 and n4 % cin == 0
+                and n4 // cin in (1, 2, 4))
+
     def forward(self, x):  # NHWC
         if self.w4 is None:
             self.refresh_phase_weights()
         x = x.contiguous()
-        if self.w4p is not None and FUSED_SUBPIXEL and self.w4.shape[0] % 256 == 0:
+        if self.fused_ok():
             return K.conv2x2_subpixel(x, self.w4p, x, bias=self.conv.bias)   # one launch, the same bits
         # bias-free phase conv; the conv bias is added in fp32 by the interleave kernel
         if self.w4p is not None:
@@ -307,7 +315,7 @@ class UpBlock(nn.Module):
         if self.w4 is None:
             self.refresh_phase_weights()
         B, H, W, _ = x32.shape
-        if self.w4p is not None and FUSED_SUBPIXEL and self.w4.shape[0] % 256 == 0:
+        if self.fused_ok():
             s16 = torch.empty((B, 2 * H, 2 * W, self.w4.shape[0] // 4), dtype=torch.bfloat16, device=x32.device)
             return K.conv2x2_subpixel(x16, self.w4p, x32, bias=self.conv.bias, shadow=s16), s16
         if self.w4p is not None:

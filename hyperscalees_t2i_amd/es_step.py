@@ -160,6 +160,24 @@ class ESEngine:
         self.timings: Dict[str, float] = {}
         self.last_images: Optional[torch.Tensor] = None
 
+    def member_passes(self) -> List[Tuple[int, int]]:
+        """This rank's members in passes of the backend's pass size, as local [c0, c1) ranges.  Pass
+        boundaries sit on GLOBAL member indices (multiples of members_per_pass from member 0 of the
+        population), so a member is evaluated in the same batch whichever rank holds it whenever the
+        shard boundaries are themselves multiples of the pass size (pop 64 over 8 ranks at 8 per pass);
+        a shard that starts mid-pass evaluates the part of that global pass it holds."""
+        nl = self.hi - self.lo
+        per = self.backend.members_per_pass() if hasattr(self.backend, "members_per_pass") else None
+        if not per:
+            return [(0, nl)] if nl else []
+        out, c0 = [], 0
+        while c0 < nl:
+            g0 = self.lo + c0
+            c1 = min(nl, (g0 // per + 1) * per - self.lo)
+            out.append((c0, c1))
+            c0 = c1
+        return out
+
     @torch.no_grad()
     def evaluate_local(self, theta: torch.Tensor, seed: int, guidance_scale: float, *, keep_images: bool = False,
                        mark=lambda name: None):
@@ -177,13 +195,9 @@ class ESEngine:
         mark("perturb")
         if nl == 0:
             return torch.empty((0, m), device=self.device), torch.empty((0, 5), device=self.device), factors, info
-        # members in passes of the backend's pass size, boundaries fixed from this rank's first member
-        per = self.backend.members_per_pass() if hasattr(self.backend, "members_per_pass") else None
-        per = nl if not per else min(per, nl)
         S_parts, raw_parts, logs = [], [], []
         feats = None
-        for c0 in range(0, nl, per):
-            c1 = min(nl, c0 + per)
+        for c0, c1 in self.member_passes():
             imgs = self.backend.generate_population(flat_ids, seed, guidance_scale, tp[c0:c1])      # (2) inside
             mark("generate")
             if feats is None:

@@ -370,7 +370,7 @@ class LoRALinear(nn.Module):
             if M % n:
                 raise RuntimeError(f"{M} rows do not split over {n} members")
             tp = ctx.theta_pop
-            if FP32_DELTA_KERNEL:
+            if FP32_DELTA_KERNEL and self.r <= LORA_DELTA_F32_MAX_R:
                 K.lora_delta_f32(x2, tp[:, self.theta_off_A:], tp.stride(0), tp[:, self.theta_off_B:], tp.stride(0),
                                  self.r, self.scale, M // n, y)
             else:
@@ -380,7 +380,10 @@ class LoRALinear(nn.Module):
                 y = y + self.scale * torch.bmm(t, B.transpose(1, 2)).view(M, -1)
         elif self.r:
             A, B = self.lora_A.weight.detach().float().contiguous(), self.lora_B.weight.detach().float().contiguous()
-            K.lora_delta_f32(x2, A, 0, B, 0, self.r, self.scale, max(M, 1), y)
+            if self.r <= LORA_DELTA_F32_MAX_R:
+                K.lora_delta_f32(x2, A, 0, B, 0, self.r, self.scale, max(M, 1), y)
+            else:   # ranks above the kernel's register budget: the plain fp32 product
+                y = y + self.scale * ((x2 @ A.t()) @ B.t())
         y = y.view(*shp[:-1], self.out_features)
         for hook in self._forward_hooks.values():   # forward hooks see this path like __call__ (activation capture)
             hook(self, (x,), y)
@@ -390,6 +393,9 @@ class LoRALinear(nn.Module):
 # LoRALinear.forward_fp32's population LoRA term on eggroll_lora_delta_f32 (True) or two torch bmm's (False, the
 # round-4 form: A/B measurement only)
 FP32_DELTA_KERNEL = True
+# eggroll_lora_delta_f32 holds the r projections per row in registers: 1 <= r <= 8 (include/eggroll.h).  LoRA
+# ranks above it (--sana_lora_r 16 etc.; the bf16 population GEMM takes r up to 16) use the two bmm's.
+LORA_DELTA_F32_MAX_R = 8
 
 
 # Linears that read the same input (Sana attn1 to_q / to_k / to_v, attn2 to_k / to_v) get their LoRA

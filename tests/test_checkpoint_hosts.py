@@ -149,6 +149,43 @@ def test_zimage_vae_decoder_lora_theta_layout():
     assert [m.theta_off_B for m in mods] == [d_tr + i * 4 * Cv + 2 * Cv for i in range(4)]
 
 
+def test_zimage_vae_decoder_adapter_keys_are_peft_decoder_names(tmp_path):
+    """save_lora's vae_decoder/ adapter carries the keys PEFT's save_pretrained writes for a LoRA'd
+    pipe.vae.decoder (es_backend.py:598-619): base_model.model.mid_block.attentions.0.<target>.lora_A|B.weight
+    — diffusers' Decoder names, not flux_vae.py's mid.1 — and load_lora reads exactly that key set back."""
+    from safetensors.torch import load_file
+    from hyperscalees_t2i_amd.backend import ZImageBackend, ZImageConfig
+    cfg = dict(synthetic_weights=True, arch=ZTINY, vae_widths=ZVAE_W, synthetic_prompts=2, synthetic_prompt_lens=(4, 9),
+               use_vae_decoder_lora=True)
+    be = ZImageBackend("cpu", ZImageConfig(**cfg))
+    be.init_and_attach_lora()
+    be.save_lora(tmp_path)
+    keys = set(load_file(str(tmp_path / "vae_decoder" / "adapter_model.safetensors")))
+    want = {f"base_model.model.mid_block.attentions.0.{t}.lora_{ab}.weight"
+            for t in ("to_q", "to_k", "to_v", "to_out.0") for ab in ("A", "B")}
+    assert keys == want
+    tr_keys = set(load_file(str(tmp_path / "transformer" / "adapter_model.safetensors")))
+    assert all(k.startswith("base_model.model.") and ".lora_" in k for k in tr_keys)
+    be2 = ZImageBackend("cpu", ZImageConfig(**cfg))
+    be2.init_and_attach_lora()
+    for m in lora_modules_of(be2.es_model.vae):
+        torch.nn.init.zeros_(m.lora_A.weight)
+    be2.load_lora(tmp_path)
+    for a, b in zip(lora_modules_of(be.es_model.vae), lora_modules_of(be2.es_model.vae)):
+        assert torch.equal(a.lora_A.weight, b.lora_A.weight) and torch.equal(a.lora_B.weight, b.lora_B.weight)
+    import safetensors.torch as st                               # a flux_vae.py-named file is refused
+    t = load_file(str(tmp_path / "vae_decoder" / "adapter_model.safetensors"))
+    st.save_file({k.replace("mid_block.attentions.0", "mid.1"): v for k, v in t.items()},
+                 str(tmp_path / "vae_decoder" / "adapter_model.safetensors"))
+    with pytest.raises(ValueError, match="adapter keys differ"):
+        be2.load_lora(tmp_path)
+
+
+def lora_modules_of(m):
+    from hyperscalees_t2i_amd.lora import lora_modules
+    return lora_modules(m)
+
+
 # ---------------------------------------------------------------------------------------------- Infinity
 from hyperscalees_t2i_amd.infinity import InfinityArch, InfinityTransformer, infinity_vae  # noqa: E402
 

@@ -131,6 +131,35 @@ def test_member_shard_partition():
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
 
 
+def test_member_passes_on_global_boundaries():
+    """ESEngine.member_passes: passes of members_per_pass sit on global member indices.  Every global
+    pass is the union of the ranks' passes that overlap it, and with shard boundaries on multiples of
+    the pass size (pop 64 / 8 ranks, pop 24 / 3 ranks) each rank's passes ARE the global passes."""
+    from types import SimpleNamespace
+    from hyperscalees_t2i_amd.es_step import ESEngine
+
+    def passes(pop, rank, world, per):
+        e = ESEngine.__new__(ESEngine)
+        e.lo, e.hi = member_shard(pop, rank, world)
+        e.backend = SimpleNamespace(members_per_pass=lambda: per)
+        return [(e.lo + a, e.lo + b) for a, b in e.member_passes()]
+
+    for pop in (1, 7, 8, 24, 64, 65):
+        for per in (1, 3, 8):
+            single = passes(pop, 0, 1, per)
+            assert single == [(a, min(pop, a + per)) for a in range(0, pop, per)]
+            for world in (2, 3, 8):
+                got = [p for r in range(world) for p in passes(pop, r, world, per)]
+                assert got[0][0] == 0 and got[-1][1] == pop and all(a[1] == b[0] for a, b in zip(got, got[1:]))
+                assert all(a // per == (b - 1) // per for a, b in got)       # no pass straddles a global one
+                if all(member_shard(pop, r, world)[0] % per == 0 for r in range(world)):
+                    assert got == single
+    assert passes(24, 1, 2, 8) == [(12, 16), (16, 24)]                      # shard starting mid-pass
+    e = ESEngine.__new__(ESEngine)
+    e.lo, e.hi, e.backend = 3, 9, SimpleNamespace()                          # no pass size: one pass
+    assert e.member_passes() == [(0, 6)]
+
+
 def _verify_worker(rank, world, port, diverge, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -621,10 +621,13 @@ def test_dcae_head_matches_unfused(dev, B, H, W):
 
 
 def test_subpixel_upblock_matches_reference(dev):
-    """Sub-pixel phase conv + fused interleave/shortcut == nearest-x2 upsample + 3x3 conv + shortcut."""
+    """Sub-pixel phase conv + fused interleave/shortcut == nearest-x2 upsample + 3x3 conv + shortcut.
+    Widths on both sides of the fused kernel's shape rule (UpBlock.fused_ok): (64, 64), (128, 64) fused; (64, 128)
+    (4*Cout / Cin = 8) and (64, 96) (4*Cout % 256 != 0) on the two-launch form instead of an error."""
     from hyperscalees_t2i_amd.dcae import UpBlock
     torch.manual_seed(0)
-    for cin, cout, H, W in ((64, 32, 6, 5), (32, 32, 8, 8), (64, 64, 4, 7)):
+    for cin, cout, H, W in ((64, 32, 6, 5), (32, 32, 8, 8), (64, 64, 4, 7), (128, 64, 4, 6), (64, 128, 5, 4),
+                            (64, 96, 3, 4)):
         with torch.device(dev):
             up = UpBlock(cin, cout)
         with torch.no_grad():
@@ -632,6 +635,7 @@ def test_subpixel_upblock_matches_reference(dev):
             up.conv.bias.copy_(torch.randn_like(up.conv.bias, dtype=torch.float32) * 0.1)
         up.refresh_phase_weights()
         x = torch.randn(2, H, W, cin, device=dev).to(torch.bfloat16)
+        assert up.fused_ok() == ((cin, cout) in ((64, 64), (128, 64)))
         got = up(x).float()
         ref = up.forward_reference(x).float()
         rel = ((got - ref).norm() / ref.norm()).item()
@@ -1363,6 +1367,37 @@ def test_lora_delta_f32_rejects_bad_args(dev):
         K.lora_delta_f32(x.bfloat16(), A, 0, B, 0, 1, 1.0, 8, y)
     empty = torch.zeros((0, 32), device=dev)                                   # no rows: a no-op
     assert K.lora_delta_f32(torch.zeros((0, 64), device=dev), A, 0, B, 0, 1, 1.0, 8, empty).shape == (0, 32)
+
+
+@pytest.mark.parametrize("r", [2, 8, 16])
+def test_forward_fp32_any_lora_rank(dev, r):
+    """LoRALinear.forward_fp32 at LoRA ranks the bf16 population GEMM accepts (r 16 is above
+    eggroll_lora_delta_f32's register budget and takes the bmm form): the population path (rows
+    member-major, theta_pop) and the single-member path both equal the PEFT formula in fp64."""
+    from hyperscalees_t2i_amd.lora import LoRALinear, PopulationContext
+    g = torch.Generator(device="cpu").manual_seed(r)
+    Kd, N, n, rpm = 256, 96, 3, 5
+    lin = LoRALinear(Kd, N, bias=True, r=r, alpha=2.0 * r).to(dev)
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn((N, Kd), generator=g).to(dev, torch.bfloat16) * 0.05)
+        lin.bias.copy_(torch.randn(N, generator=g).to(dev, torch.bfloat16))
+    lin.reset_lora(g, b_std=0.1)
+    lin.theta_off_A, lin.theta_off_B = 0, r * Kd
+    tp = torch.randn((n, r * Kd + N * r), generator=g).to(dev) * 0.1
+    x = torch.randn((n * rpm, Kd), generator=g).to(dev)
+    W, b = lin.weight.double(), lin.bias.double()
+    lin.ctx = PopulationContext(theta_pop=tp, n_members=n)
+    y = lin.forward_fp32(x).double()
+    for k in range(n):
+        rows = slice(k * rpm, (k + 1) * rpm)
+        A, B = tp[k, :r * Kd].double().view(r, Kd), tp[k, r * Kd:].double().view(N, r)
+        want = x[rows].double() @ W.t() + b + lin.scale * ((x[rows].double() @ A.t()) @ B.t())
+        assert float((y[rows] - want).abs().max()) < 1e-4 * float(want.abs().max()), (r, k)
+    lin.ctx = None
+    y1 = lin.forward_fp32(x).double()
+    A, B = lin.lora_A.weight.double(), lin.lora_B.weight.double()
+    want = x.double() @ W.t() + b + lin.scale * ((x.double() @ A.t()) @ B.t())
+    assert float((y1 - want).abs().max()) < 1e-4 * float(want.abs().max()), r
 
 
 def _integration_blocks():
