@@ -478,10 +478,16 @@ template <int R, bool V4, bool GEN>
 __global__ __launch_bounds__(256) void k_perturb(const float* __restrict__ theta, FacSrc src,
                                                  const eggroll_mat_t* __restrict__ mats,
                                                  const eggroll_tile_t* __restrict__ tiles, int r, float sqrt_r,
-                                                 int32_t pop, int32_t antithetic, int64_t member_lo, int n_members,
-                                                 float sigma, float* __restrict__ out, int64_t ld_out) {
+                                                 int32_t pop, int32_t antithetic, int64_t member_lo, int n_all,
+                                                 int mpb, float sigma, float* __restrict__ out_all, int64_t ld_out) {
     const eggroll_tile_t tl = tiles[blockIdx.x];
     const eggroll_mat_t mt = mats[tl.mat];
+    // grid.y splits the members into groups of mpb (perturb_launch): a member's row is computed the same
+    // way whichever group holds it
+    const int g0 = (int)blockIdx.y * mpb;
+    const int n_members = n_all - g0 < mpb ? n_all - g0 : mpb;
+    member_lo += g0;
+    float* __restrict__ out = out_all + (int64_t)g0 * ld_out;
     dispatch_tile<R, V4>(
         mt, r,
         [&](auto KD, auto NUv) {
@@ -954,6 +960,13 @@ int eggroll_philox_words(uint64_t seed, int64_t j, int64_t n_quads, uint32_t* ou
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+#ifndef EGG_PTB_SPLIT  // perturb: target workgroup count for the member split over grid.y (0: no split; A/B knob)
+#define EGG_PTB_SPLIT 4096
+#endif
+#ifndef EGG_PTB_MIN_GROUP
+#define EGG_PTB_MIN_GROUP 16
+#endif
+
 static int launch_rank(int32_t rank) { return (rank == 1 || rank == 2 || rank == 4) ? rank : 0; }
 
 static int perturb_launch(const float* theta, FacSrc src, bool gen, const eggroll_mat_t* mats,
@@ -970,8 +983,23 @@ static int perturb_launch(const float* theta, FacSrc src, bool gen, const eggrol
     auto* k = launch_rank(rank) == 1 ? EGG_PTB_K(1) : launch_rank(rank) == 2 ? EGG_PTB_K(2)
             : launch_rank(rank) == 4 ? EGG_PTB_K(4) : EGG_PTB_K(0);
 #undef EGG_PTB_K
-    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles), dim3(256), 0, as_stream(stream), theta, src, mats, tiles,
-                       rank, sqrt_r, pop, antithetic, member_lo, (int)(member_hi - member_lo), sigma, out, ld_out);
+    // A launch of n_tiles workgroups that walk every member is one wave round at the product sizes (Sana:
+    // ~1500 tiles x 4 waves), each thread a serial chain of per-member factor loads / Philox + stores.
+    // With many members (>= 2 x EGG_PTB_MIN_GROUP) the members are split over grid.y until ~EGG_PTB_SPLIT
+    // workgroups exist (theta re-read once per group, from L2): Sana, all 64 members in one call 95.8 ->
+    // 85.7 us.  Splitting 8 members (one GPU's share of pop 64) measured 14.3 -> 24.1 us (per-workgroup
+    // setup and the regenerated factors' VALU, not memory, bound it), so groups keep >= 16 members.
+    // Same bits either way: each member row is computed the same way (profiles/r13b_es_perturb_split_ab.log).
+    const int n = (int)(member_hi - member_lo);
+    int ny = 1;
+    if (EGG_PTB_SPLIT > 0 && n_tiles < EGG_PTB_SPLIT && n >= 2 * EGG_PTB_MIN_GROUP) {
+        const int64_t want = (EGG_PTB_SPLIT + n_tiles - 1) / n_tiles, cap = n / EGG_PTB_MIN_GROUP;
+        ny = (int)(want < cap ? want : cap);
+    }
+    const int mpb = (n + ny - 1) / ny;
+    ny = (n + mpb - 1) / mpb;
+    hipLaunchKernelGGL(k, dim3((unsigned)n_tiles, (unsigned)ny), dim3(256), 0, as_stream(stream), theta, src, mats,
+                       tiles, rank, sqrt_r, pop, antithetic, member_lo, n, mpb, sigma, out, ld_out);
     EGG_CHECK_LAUNCH("perturb");
     return EGGROLL_OK;
 }

@@ -1381,7 +1381,7 @@ def test_forward_fp32_any_lora_rank(dev, r):
     with torch.no_grad():
         lin.weight.copy_(torch.randn((N, Kd), generator=g).to(dev, torch.bfloat16) * 0.05)
         lin.bias.copy_(torch.randn(N, generator=g).to(dev, torch.bfloat16))
-    lin.reset_lora(g, b_std=0.1)
+    lin.reset_lora(torch.Generator(device=dev).manual_seed(r), b_std=0.1)
     lin.theta_off_A, lin.theta_off_B = 0, r * Kd
     tp = torch.randn((n, r * Kd + N * r), generator=g).to(dev) * 0.1
     x = torch.randn((n * rpm, Kd), generator=g).to(dev)

@@ -43,6 +43,7 @@ def main(pa, pb, rounds=7):
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     out = {}
     for name, shapes, rank, pop, nloc in (("sana_r1_pop64", sana_lora_shapes(), 1, 64, 8),
+                                          ("sana_r1_pop8", sana_lora_shapes(), 1, 8, 8),
                                           ("zimage_r4_pop128", zimage_turbo_lora_shapes(), 4, 128, 16)):
         lay = K.ThetaLayout(shapes, rank)
         nb = K.n_base_samples(pop, True)
@@ -69,8 +70,23 @@ def main(pa, pb, rounds=7):
                                           tiles.data_ptr(), lay.n_tiles, lay.D, rank, 1e-3, 0.0, 40.0,
                                           ws[i].buf.data_ptr(), upd[i].data_ptr(), st) == 0
 
+        tps = [torch.empty((nloc, K._pad4(lay.D)), device=dev) for _ in libs]
+        tpp = [torch.empty((pop, K._pad4(lay.D)), device=dev) for _ in libs]
+
+        def perturb_seeded(i):   # this GPU's members of the node-level population (default engine path)
+            assert libs[i].eggroll_perturb_seeded(7, theta.data_ptr(), mats.data_ptr(), tiles.data_ptr(), lay.n_tiles,
+                                                  lay.D, rank, pop, 1, 0, nloc, 1e-2, tps[i].data_ptr(),
+                                                  tps[i].stride(0), st) == 0
+
+        def perturb_seeded_all(i):   # one process over the whole population (N = 1 at pop = pop)
+            assert libs[i].eggroll_perturb_seeded(7, theta.data_ptr(), mats.data_ptr(), tiles.data_ptr(), lay.n_tiles,
+                                                  lay.D, rank, pop, 1, 0, pop, 1e-2, tpp[i].data_ptr(),
+                                                  tpp[i].stride(0), st) == 0
+
         res = {}
-        for kname, fn, buf in (("noise", noise, fac), ("perturb", perturb, tp), ("update_caps", update, upd)):
+        for kname, fn, buf in (("noise", noise, fac), ("perturb", perturb, tp), ("update_caps", update, upd),
+                               ("perturb_seeded", perturb_seeded, tps),
+                               ("perturb_seeded_allpop", perturb_seeded_all, tpp)):
             fn(0)
             fn(1)
             torch.cuda.synchronize()
@@ -84,7 +100,7 @@ def main(pa, pb, rounds=7):
             print(json.dumps({name: {kname: res[kname]}}), flush=True)
             assert same, (name, kname)
         out[name] = res
-        del fac, tp, upd
+        del fac, tp, upd, tps, tpp
     print(json.dumps(out))
 
 
