@@ -749,6 +749,9 @@ constexpr int LA_T = 256;                     // tokens per chunk
 #ifndef EGG_LA_HEAD_PAIRS
 #define EGG_LA_HEAD_PAIRS 1
 #endif
+#ifndef EGG_LA_FOLD  // k_la_kv_fold for few chunks per head (A/B knob; 0 = k_la_kv + k_la_reduce)
+#define EGG_LA_FOLD 1
+#endif
 
 // Pass 1 per (image*head, chunk of LA_T tokens) on MFMA: k (ReLU'd) and v staged into LDS token-major
 // as bf16 (all 8 loads per thread in flight), then kv^T-free: C[i][j] = sum_n v[n][i] relu(k[n][j]) as
@@ -873,6 +876,134 @@ __global__ __launch_bounds__(256) void k_la_kv(const unsigned short* __restrict_
         float* dst = part + ((int64_t)b * heads + h0 + hh) * nchunk * LA_PART + (int64_t)c * LA_PART;
         const float(*r4)[LA_PART] = red + hh * 4;
         for (int e = tid; e < LA_PART; e += 256) dst[e] = ((r4[0][e] + r4[1][e]) + r4[2][e]) + r4[3][e];
+    }
+}
+
+// Round 6: the kv pass with the chunk reduction folded in, for few chunks per head
+// (N <= LA_FOLD_MAX * LA_T) on grids large enough to fill the chip with one block per head (group): the block
+// walks its head's chunks in order, computes each chunk's partial exactly as k_la_kv does (same MFMAs, same
+// ((w0 + w1) + w2) + w3 wave sum), and adds it into a per-thread running sum that starts at 0 as
+// k_la_reduce's does — the same additions in the same order, so kvsum is bitwise k_la_kv + k_la_reduce's,
+// without the partials' round trip through HBM or the reduce launch.  The next chunk's k / v loads are
+// issued as soon as this chunk is in LDS, so they land under its MFMAs and reduction.
+constexpr int LA_FOLD_MAX = 4;
+template <int HP>
+__global__ __launch_bounds__(256) void k_la_kv_fold(const unsigned short* __restrict__ k, const unsigned short* __restrict__ v,
+                                                    int64_t ld, int64_t hstride, int heads, int N, int nchunk, int relu,
+                                                    float* __restrict__ kvsum) {
+    __shared__ __attribute__((aligned(16))) unsigned short lds_kv[HP * 2 * LA_T * LA_RS];
+    float(*red)[LA_PART] = reinterpret_cast<float(*)[LA_PART]>(lds_kv);
+    static_assert(HP * 4 * LA_PART * 4 <= HP * 2 * LA_T * LA_RS * 2, "reduction buffer fits in the staging LDS");
+    constexpr int EPT = (LA_PART + 255) / 256;  // kvsum elements per thread per head
+    const int bhp = xcd_remap(blockIdx.x, gridDim.x);
+    const int hg = heads / HP, b = bhp / hg, h0 = (bhp - b * hg) * HP;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+    constexpr int U = 4 * HP;
+    u16x8m kr[U], vr[U];
+    auto load = [&](int c) {
+        const int n0 = c * LA_T, cnt = (N - n0) < LA_T ? (N - n0) : LA_T;
+#pragma unroll
+        for (int it = 0; it < U; ++it) {
+            const int u = tid + it * 256, t = u / U, q8 = u % U;
+            kr[it] = vr[it] = u16x8m{0, 0, 0, 0, 0, 0, 0, 0};
+            if (t < cnt) {
+                const int64_t off = ((int64_t)b * N + n0 + t) * ld + (int64_t)h0 * hstride + (q8 >> 2) * hstride + (q8 & 3) * 8;
+                kr[it] = *reinterpret_cast<const u16x8m*>(k + off);
+                vr[it] = *reinterpret_cast<const u16x8m*>(v + off);
+            }
+        }
+    };
+    la_bf16x8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(r16 == 0 ? 1.0f : 0.0f);
+    float sum[HP][EPT];
+#pragma unroll
+    for (int hh = 0; hh < HP; ++hh)
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) sum[hh][q] = 0.f;
+    load(0);
+#pragma unroll 1
+    for (int c = 0; c < nchunk; ++c) {
+        if (c > 0) __syncthreads();  // every thread is done reading the previous chunk's reduction table
+#pragma unroll
+        for (int it = 0; it < U; ++it) {
+            const int u = tid + it * 256, t = u / U, q8 = u % U;
+            unsigned short* sk = lds_kv + (q8 >> 2) * (2 * LA_T * LA_RS);
+            unsigned short* sv = sk + LA_T * LA_RS;
+            if (relu) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) kr[it][i] = (kr[it][i] & 0x8000) ? (unsigned short)0 : kr[it][i];
+            }
+            *reinterpret_cast<u16x8m*>(sk + t * LA_RS + (q8 & 3) * 8) = kr[it];
+            *reinterpret_cast<u16x8m*>(sv + t * LA_RS + (q8 & 3) * 8) = vr[it];
+        }
+        if (c + 1 < nchunk) load(c + 1);  // in flight under this chunk's MFMAs
+        __syncthreads();
+        la_f32x4 acc[HP][2][2], ks[HP][2];
+#pragma unroll
+        for (int hh = 0; hh < HP; ++hh)
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                ks[hh][x] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int y = 0; y < 2; ++y) acc[hh][x][y] = la_f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+        for (int hh = 0; hh < HP; ++hh) {
+            const unsigned short* sk = lds_kv + hh * (2 * LA_T * LA_RS);
+            const unsigned short* sv = sk + LA_T * LA_RS;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int t0 = w * 64 + s * 32;
+                la_bf16x8 av[2], bk[2];
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    av[x] = la_tr8(sv + t0 * LA_RS + 16 * x, lane);
+                    bk[x] = la_tr8(sk + t0 * LA_RS + 16 * x, lane);
+                }
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[hh][x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[x], bk[y], acc[hh][x][y], 0, 0, 0);
+                    ks[hh][x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bk[x], ks[hh][x], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int hh = 0; hh < HP; ++hh) {
+            float* rw = red[hh * 4 + w];
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) rw[(16 * x + 4 * g + e) * LA_D + 16 * y + r16] = acc[hh][x][y][e];
+            if (g == 0) {
+#pragma unroll
+                for (int y = 0; y < 2; ++y) rw[LA_D * LA_D + 16 * y + r16] = ks[hh][y][0];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int hh = 0; hh < HP; ++hh) {
+            const float(*r4)[LA_PART] = red + hh * 4;
+#pragma unroll
+            for (int q = 0; q < EPT; ++q) {
+                const int e = tid + 256 * q;
+                if (e < LA_PART) sum[hh][q] += ((r4[0][e] + r4[1][e]) + r4[2][e]) + r4[3][e];
+            }
+        }
+    }
+#pragma unroll
+    for (int hh = 0; hh < HP; ++hh) {
+        float* dst = kvsum + ((int64_t)b * heads + h0 + hh) * LA_PART;
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+            const int e = tid + 256 * q;
+            if (e < LA_PART) dst[e] = sum[hh][q];
+        }
     }
 }
 
@@ -2130,23 +2261,37 @@ extern "C" int eggroll_linear_attention(const void* q, const void* k, const void
     // 1-4 % (profiles/r10d_linear_attention_head_pairs_ab.log).  The reference-layout interleaved q | k | v
     // (hstride 96) stays per head.
     const int hp = hstride == LA_D && heads % 2 == 0 && blocks >= 8192 && EGG_LA_HEAD_PAIRS ? 2 : 1;
-    if (hp == 2)
-        hipLaunchKernelGGL(k_la_kv<2>, dim3((unsigned)(blocks / 2)), dim3(256), 0, st, (const unsigned short*)k,
-                           (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
-                           (float*)workspace);
-    else
-        hipLaunchKernelGGL(k_la_kv<1>, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)k,
-                           (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
-                           (float*)workspace);
-    EGG_CHECK_LAUNCH("linear_attention_kv");
     float* kvsum = (float*)workspace + blocks * LA_PART;
-    if (nchunk >= LA_RED_WIDE)
-        hipLaunchKernelGGL(k_la_reduce_e, dim3((unsigned)(B * heads * LA_RED_WAVES)), dim3(64), 0, st,
-                           (const float*)workspace, (int)nchunk, kvsum);
-    else
-        hipLaunchKernelGGL(k_la_reduce, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const float*)workspace,
-                           (int)nchunk, kvsum);
-    EGG_CHECK_LAUNCH("linear_attention_reduce");
+    // few chunks per head on a grid that one block per head (group) still fills (Sana attn1: 128 x 35 head
+    // pairs x 4 chunks): the reduction folded into the kv pass (k_la_kv_fold, the same bits)
+    const bool fold = EGG_LA_FOLD && nchunk <= LA_FOLD_MAX && B * heads / hp >= 2048;
+    if (fold) {
+        if (hp == 2)
+            hipLaunchKernelGGL(k_la_kv_fold<2>, dim3((unsigned)(B * heads / 2)), dim3(256), 0, st,
+                               (const unsigned short*)k, (const unsigned short*)v, ld, hstride, (int)heads, (int)N,
+                               (int)nchunk, relu_qk, kvsum);
+        else
+            hipLaunchKernelGGL(k_la_kv_fold<1>, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const unsigned short*)k,
+                               (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk, kvsum);
+        EGG_CHECK_LAUNCH("linear_attention_kv_fold");
+    } else {
+        if (hp == 2)
+            hipLaunchKernelGGL(k_la_kv<2>, dim3((unsigned)(blocks / 2)), dim3(256), 0, st, (const unsigned short*)k,
+                               (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
+                               (float*)workspace);
+        else
+            hipLaunchKernelGGL(k_la_kv<1>, dim3((unsigned)blocks), dim3(256), 0, st, (const unsigned short*)k,
+                               (const unsigned short*)v, ld, hstride, (int)heads, (int)N, (int)nchunk, relu_qk,
+                               (float*)workspace);
+        EGG_CHECK_LAUNCH("linear_attention_kv");
+        if (nchunk >= LA_RED_WIDE)
+            hipLaunchKernelGGL(k_la_reduce_e, dim3((unsigned)(B * heads * LA_RED_WAVES)), dim3(64), 0, st,
+                               (const float*)workspace, (int)nchunk, kvsum);
+        else
+            hipLaunchKernelGGL(k_la_reduce, dim3((unsigned)(B * heads)), dim3(256), 0, st, (const float*)workspace,
+                               (int)nchunk, kvsum);
+        EGG_CHECK_LAUNCH("linear_attention_reduce");
+    }
     const bool big = N >= 8192;  // 16 tiles per wave at the DC-AE's 128^2 maps
     const int64_t tpb = 4 * 16 * (big ? 16 : 8);
     const int64_t oblk = (N + tpb - 1) / tpb;

@@ -90,6 +90,29 @@ def main():
         return
     del x, y
 
+    # DC-AE up-block phase convs with the fused sub-pixel epilogue (eggroll_conv2x2_subpixel_nhwc): the four
+    # product shapes (B 8; (H, Cin) -> Cout), bf16 stream
+    for H, Cin, Cout in ((512, 256, 128), (256, 512, 256), (128, 512, 512), (64, 1024, 512)):
+        xs = torch.randn(8, H, H, Cin, device=dev, dtype=torch.bfloat16)
+        w3 = (torch.randn(Cout, Cin, 3, 3, device=dev) / (9 * Cin) ** 0.5)
+        from hyperscalees_t2i_amd.dcae import subpixel_phase_weights
+        w4 = subpixel_phase_weights(w3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w4p = K.pack_conv3x3_weight(w4, 1)
+        bias = torch.randn(Cout, device=dev).bfloat16()
+        ys = torch.empty(8, 2 * H, 2 * H, Cout, device=dev, dtype=torch.bfloat16)
+        nblk = -(-(8 * (H + 1) * (H + 1)) // 256) * (4 * Cout // 256)
+
+        def up():
+            rc = lib.eggroll_conv2x2_subpixel_nhwc(
+                ctypes.c_void_p(xs.data_ptr()), ctypes.c_void_p(w4p.data_ptr()), ctypes.c_void_p(bias.data_ptr()),
+                ctypes.c_void_p(xs.data_ptr()), ctypes.c_int32(0), ctypes.c_int64(8), ctypes.c_int64(H),
+                ctypes.c_int64(H), ctypes.c_int64(Cin), ctypes.c_int64(Cout), ctypes.c_void_p(ys.data_ptr()), None, st)
+            assert rc == 0
+        report(f"conv2x2_subpixel 8x{H}x{H}x{Cin}->{Cout}", nblk, up)
+        del xs, ys
+    if len(sys.argv) > 1 and sys.argv[1] == "up":
+        return
+
     # DC-AE ResBlock convs (8 images): 128 ch at 1024^2 (512x128 tile), 256 at 512^2, 512 at 256^2
     for C, hw in ((128, 1024), (256, 512), (512, 256)):
         xc = torch.randn(8, hw, hw, C, device=dev, dtype=torch.bfloat16)
