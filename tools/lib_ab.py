@@ -34,7 +34,7 @@ def build_a(rev):
     print(out)
 
 
-def main(pa, pb):
+def main(pa, pb, kern=8):
     import torch
     libs = [ctypes.CDLL(str(Path(p).resolve())) for p in (pa, pb)]
     dev = torch.device("cuda:0")
@@ -55,7 +55,7 @@ def main(pa, pb):
             rc = libs[i].eggroll_lora_gemm_sel(vp(x.data_ptr()), i64(K), vp(W.data_ptr()), i64(K),
                                                vp(b.data_ptr() if b is not None else 0), vp(T.data_ptr()),
                                                vp(tp.data_ptr()), i64(tp.stride(0)), i64(r * K), i32(r), f32(4.0),
-                                               i64(rpm), i64(M), i64(N), i64(K), vp(ys[i].data_ptr()), i64(N), i32(8),
+                                               i64(rpm), i64(M), i64(N), i64(K), vp(ys[i].data_ptr()), i64(N), i32(kern),
                                                st)
             assert rc == 0, rc
         return run, ys
@@ -99,4 +99,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "build-a":
         build_a(sys.argv[2] if len(sys.argv) > 2 else "HEAD")
     else:
-        main(sys.argv[1], sys.argv[2])
+        main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 8)
