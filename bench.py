@@ -371,8 +371,10 @@ def main():
     backend, engine, noiser, theta, pop = build(args, world, rank, device)
     log(f"rank {rank}: built (pop {pop}, D {noiser.num_params})")
     guidance = backend.cfg.guidance_scale
+    S_log = []   # (epoch seed, gathered S [pop, m]) per epoch: the aux record's per-epoch S digests
     for w in range(args.warmup):
-        theta, _ = engine.step(theta, seed=w, guidance_scale=guidance)
+        theta, st_w = engine.step(theta, seed=w, guidance_scale=guidance)
+        S_log.append((w, st_w.get("_S")))
         torch.cuda.synchronize()
         log(f"rank {rank}: warmup epoch {w} done")
     torch.cuda.synchronize()
@@ -382,6 +384,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         theta, stats = engine.step(theta, seed=args.warmup + s, guidance_scale=guidance)
+        S_log.append((args.warmup + s, stats.get("_S")))   # host copy the step already made
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -396,7 +399,8 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for s in range(n_roof):
-        theta, _ = engine.step(theta, seed=args.warmup + args.steps + s, guidance_scale=guidance)
+        theta, st_r = engine.step(theta, seed=args.warmup + args.steps + s, guidance_scale=guidance)
+        S_log.append((args.warmup + args.steps + s, st_r.get("_S")))
     torch.cuda.synchronize()
     roof_ms_per_step = 1e3 * (time.perf_counter() - t1) / n_roof
     GemmTimer.active = False
@@ -413,13 +417,16 @@ def main():
     # one extra instrumented epoch for the per-phase breakdown (not part of the timed region)
     from hyperscalees_t2i_amd.kernels import OpTimer
     OpTimer.reset(True)
-    theta, _ = engine.step(theta, seed=10_000, guidance_scale=guidance, timing=True)
+    theta, st_t = engine.step(theta, seed=10_000, guidance_scale=guidance, timing=True)
+    S_log.append((10_000, st_t.get("_S")))
     OpTimer.active = False
     # final theta (after every epoch this run made): equal across ranks and to a single-process run of
     # the same total population (tests/test_gpu_bench_dist.py compares them)
     import hashlib
     theta_sha16 = hashlib.sha256(theta.detach().cpu().numpy().tobytes()).hexdigest()[:16]
     phases = dict(engine.timings)
+    S_epochs = [{"seed": sd, "sha16": hashlib.sha256(S.numpy().tobytes()).hexdigest()[:16], "S": S.tolist()}
+                for sd, S in S_log if S is not None]
     model_kernels = OpTimer.summary(HBM_PEAK_GBPS)
     from hyperscalees_t2i_amd.measure import aux_kernel_rooflines
     aux = aux_kernel_rooflines(noiser.layout, pop, engine.lo, engine.hi, device, theta=theta)
@@ -569,6 +576,7 @@ def main():
             "cpu_baseline": cpu,
             "theta_replicas_identical": replicas_identical,
             "theta_final_sha16": theta_sha16,
+            "S_epochs": S_epochs,
             "phases_ms": phases,
             "aux_kernels": aux,
             "aux_kernels_pop64_per_gpu": aux64,

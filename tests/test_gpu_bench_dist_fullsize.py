@@ -1,0 +1,63 @@
+"""BASELINE configs[2] end to end at the FULL architecture (Sana-Sprint 1.6B at 1024 px, DC-AE, CLIP-H/14 +
+CLIP-B/32), on one GPU: `torch.distributed.run --nproc-per-node 8 bench.py --gpus 8 --pop-per-gpu 8` with
+EGGROLL_DIST_BACKEND=gloo EGGROLL_SAME_DEVICE=1 (8 ranks sharing cuda:0 — RCCL refuses two ranks on one
+device) against ONE process evaluating all 64 members (`bench.py --pop-per-gpu 64`).  Every rank's theta'
+must be identical (verify_theta_replicas) and equal, bit for bit, to the single process's after the same
+epochs: the member shard + S all-gather of the node-level metric reproduces the whole-population epoch
+(unifed_es.py:159-215 evaluates members independently; utills.py:115-136 updates from the full S).
+
+Opt-in (EGGROLL_FULLSIZE_DIST=1): eight full-size model replicas on one card take ~3-5 minutes and ~150 GB of
+HBM; the tiny-architecture version of the same check runs in the default suite
+(tests/test_gpu_bench_dist.py::test_bench_eight_ranks_configs2_partition), and the full-size per-member row
+invariance it rests on is tests/test_gpu_member_slices_fullsize.py."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("EGGROLL_FULLSIZE_DIST") != "1",
+                                 reason="opt-in: EGGROLL_FULLSIZE_DIST=1 (8 full-size replicas on one GPU)")]
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(tmp_path, tag, nproc, extra):
+    env = dict(os.environ, EGGROLL_DIST_BACKEND="gloo", EGGROLL_SAME_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               OMP_NUM_THREADS="2", EGGROLL_MIOPEN_FIND="0")
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+               "--gpus", str(nproc)]
+    else:
+        cmd = [sys.executable, str(ROOT / "bench.py")]
+    cmd += ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--aux-out", str(tmp_path / f"{tag}_aux.json")] + extra
+    out, err = tmp_path / f"{tag}.out", tmp_path / f"{tag}.err"
+    with open(out, "w") as fo, open(err, "w") as fe:
+        rc = subprocess.run(cmd, env=env, stdout=fo, stderr=fe, timeout=1500, cwd=str(ROOT)).returncode
+    assert rc == 0, err.read_text()[-3000:]
+    lines = [ln for ln in out.read_text().splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, (out.read_text()[-2000:], err.read_text()[-2000:])
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(1800)
+def test_bench_eight_ranks_configs2_fullsize(tmp_path):
+    eight = _run(tmp_path, "ws8", 8, ["--pop-per-gpu", "8"])
+    one = _run(tmp_path, "ws1", 1, ["--pop-per-gpu", "64"])
+    assert eight["config"]["workload"] == one["config"]["workload"] == "sana_sprint_1.6b_onestep_1024px_es_epoch"
+    assert eight["n_gpus"] == 8 and eight["config"]["pop_total"] == 64 and eight["config"]["pop_per_gpu"] == 8
+    assert one["n_gpus"] == 1 and one["config"]["pop_total"] == 64
+    assert eight["theta_replicas_identical"] is True
+    assert eight["theta_final_sha16"] == one["theta_final_sha16"], (eight["theta_final_sha16"], one["theta_final_sha16"])
+    print(f"[configs2-fullsize] theta' {eight['theta_final_sha16']}: 8 gloo ranks x 8 members == one process x 64 "
+          f"(1.6B / 1024 px); {eight['value']:.2f} vs {one['value']:.2f} member-evals/s on one shared GPU")
