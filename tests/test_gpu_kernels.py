@@ -620,6 +620,35 @@ def test_dcae_head_matches_unfused(dev, B, H, W):
     assert rel < 1e-2, rel
 
 
+@pytest.mark.parametrize("cin,cout,H,W", [(32, 1024, 32, 32), (16, 256, 16, 48)])
+def test_conv3x3_small_cin_on_libeggroll(dev, cin, cout, H, W):
+    """dcae.Conv3x3 below 64 input channels (the DC-AE conv_in: 32 latent channels -> 1024) runs libeggroll's
+    halo conv on channel-padded operands, not MIOpen: vs the fp32 torch conv of the same bf16 operands, and
+    the MIOpen path (LIB_SMALL_CIN False) within the same bf16 tolerance."""
+    from hyperscalees_t2i_amd import dcae
+    g = torch.Generator(device=dev).manual_seed(cin + H)
+    with torch.device(dev):
+        c = dcae.Conv3x3(cin, cout)
+    with torch.no_grad():
+        c.weight.copy_((torch.randn(c.weight.shape, generator=g, device=dev) / (9 * cin) ** 0.5).to(torch.bfloat16))
+        c.bias.copy_(torch.randn(cout, generator=g, device=dev).to(torch.bfloat16))
+    x = torch.randn((2, H, W, cin), generator=g, device=dev).to(torch.bfloat16)
+    assert c.lib_small_cin(x)
+    got = c(x).float()
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), c.weight.float(), c.bias.float(),
+                                     padding=1).permute(0, 2, 3, 1)
+    assert got.shape == ref.shape
+    assert float((got - ref).norm() / ref.norm()) < 4e-3
+    assert torch.equal(c(x), c(x))                           # run to run
+    lib = c(x)
+    try:
+        dcae.LIB_SMALL_CIN = False
+        miopen = c(x).float()
+    finally:
+        dcae.LIB_SMALL_CIN = True
+    assert float((lib.float() - miopen).norm() / miopen.norm()) < 8e-3
+
+
 def test_subpixel_upblock_matches_reference(dev):
     """Sub-pixel phase conv + fused interleave/shortcut == nearest-x2 upsample + 3x3 conv + shortcut.
     Widths on both sides of the fused kernel's shape rule (UpBlock.fused_ok): (64, 64), (128, 64) fused; (64, 128)
