@@ -152,5 +152,53 @@ def main(n_hammers=3):
     out.write_text(json.dumps({"ref_lib_calls": ref["lib"], "diffs": diffs}, indent=1, default=str))
 
 
+def self_check(tag, reps):
+    """One of N identical processes started together: each compares its own repeated evals with its first
+    (no hammers: the other instances are the load, as 8 gloo ranks sharing one GPU are)."""
+    import bench
+    from hyperscalees_t2i_amd.es_step import aggregate_member_rewards
+    dev = torch.device("cuda:0")
+    torch.backends.cudnn.benchmark = False
+    args = SimpleNamespace(workload="sana", small=False, pop_per_gpu=8, latent=32)
+    be, engine, noiser, theta, pop = bench.build(args, 1, 0, dev)
+    rewards = engine.rewards
+    seed, gs = 1, be.cfg.guidance_scale
+    fac = noiser.epoch_noise(pop, seed=seed)
+    tp = noiser.perturb(theta, fac, pop, 0, pop, out=engine.theta_pop[:pop])
+    info = be.step_sampling_info(seed)
+    flat, m = info["flat_ids"], info["m"]
+    j_of = torch.tensor([info["pid_to_j"][p] for p in flat], device=dev).repeat(pop)
+    feats = rewards.prompt_features(info["unique_texts"])
+    B = len(flat)
+
+    def one(rec):
+        rec.log.clear()
+        rec.on = True
+        with torch.no_grad():
+            imgs = be.generate_population(flat, seed, gs, tp)
+            rw = rewards.score(imgs, j_of, feats)
+        torch.cuda.synchronize()
+        rec.on = False
+        S = aggregate_member_rewards(rw, flat, info["pid_to_j"], pop, m)[0]
+        return {"S_rows": [digest(S[k]) for k in range(pop)], "lib": list(rec.log),
+                "img": [digest(imgs[k * B:(k + 1) * B]) for k in range(pop)]}
+    out = []
+    with Recorder() as rec:
+        ref = one(rec)
+        for rep in range(reps):
+            r = one(rec)
+            d = {"rep": rep, "rows_differ": [k for k in range(pop) if r["S_rows"][k] != ref["S_rows"][k]],
+                 "img_differ": [k for k in range(pop) if r["img"][k] != ref["img"][k]],
+                 "lib_differ": [(i,) + tuple(ref["lib"][i][:3]) for i in range(min(len(r["lib"]), len(ref["lib"])))
+                                if r["lib"][i][3] != ref["lib"][i][3]][:12]}
+            out.append(d)
+            print(tag, json.dumps(d), flush=True)
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / f"selfcheck_{tag}.json").write_text(json.dumps({"ref_S_rows": ref["S_rows"], "reps": out}))
+
+
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 3)
+    if len(sys.argv) > 1 and sys.argv[1] == "self":
+        self_check(sys.argv[2], int(sys.argv[3]))
+    else:
+        main(int(sys.argv[1]) if len(sys.argv) > 1 else 3)

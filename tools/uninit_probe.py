@@ -1,11 +1,10 @@
-"""Does any kernel read memory it did not write?  Every torch.empty / empty_like / new_empty made from
-Python (kernel outputs and workspaces in kernels.py, model buffers) is filled with a poison value; the
-member-eval is run under two poisons and each module's output (execution order) is compared.  A
-module whose output depends on the poison reads uninitialised memory.
-
-    python tools/uninit_probe.py [--small] [--pop 8]
-"""
-import argparse
+"""Does any op of the full-size member-eval read memory it did not write?  The caching allocator is emptied and
+one huge block is allocated, filled with a byte pattern and freed again, so every allocation of the next
+member-eval is carved from pattern-filled memory; the eval's outputs (transformer output, images, S) are
+compared with a reference eval across patterns 0x00 / 0xFF (NaN in fp32 and bf16) / 0x7F (huge).  An op that
+reads unwritten bytes shows up as a pattern-dependent result.
+usage: python tools/uninit_probe.py [GiB]"""
+import hashlib
 import json
 import sys
 from pathlib import Path
@@ -13,87 +12,70 @@ from types import SimpleNamespace
 
 import torch
 
-sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-
-_orig = {"empty": torch.empty, "empty_like": torch.empty_like}
-_orig_new_empty = torch.Tensor.new_empty
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
 
 
-def _fill(t, val):
-    if t.is_floating_point():
-        t.fill_(val)
-    elif t.dtype in (torch.int32, torch.int64, torch.int16):
-        t.fill_(-7 if val != val else 12345)   # noqa: PLR0124 (nan test)
-    elif t.dtype == torch.uint8:
-        t.fill_(0xA5 if val != val else 0x3C)  # noqa: PLR0124
-    return t
+def digest(t):
+    return hashlib.sha256(t.detach().contiguous().view(torch.uint8).cpu().numpy().tobytes()).hexdigest()[:12]
 
 
-def poison(val):
-    torch.empty = lambda *a, **k: _fill(_orig["empty"](*a, **k), val)
-    torch.empty_like = lambda *a, **k: _fill(_orig["empty_like"](*a, **k), val)
-    torch.Tensor.new_empty = lambda self, *a, **k: _fill(_orig_new_empty(self, *a, **k), val)
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--small", action="store_true")
-    ap.add_argument("--pop", type=int, default=8)
-    a = ap.parse_args()
+def main(gib=150):
     import bench
-    torch.backends.cudnn.benchmark = False
+    from hyperscalees_t2i_amd.es_step import aggregate_member_rewards
+    from hyperscalees_t2i_amd.lora import LoRALinear
     dev = torch.device("cuda:0")
-    be, eng, nz, theta, _ = bench.build(SimpleNamespace(workload="sana", small=a.small, pop_per_gpu=a.pop, latent=32),
-                                        1, 0, dev)
-    gs, seed = be.cfg.guidance_scale, 1
+    torch.backends.cudnn.benchmark = False
+    args = SimpleNamespace(workload="sana", small=False, pop_per_gpu=8, latent=32)
+    be, engine, noiser, theta, pop = bench.build(args, 1, 0, dev)
+    rewards = engine.rewards
+    seed, gs = 0, be.cfg.guidance_scale
     info = be.step_sampling_info(seed)
-    mods = [(n, m) for n, m in be.es_model.transformer.named_modules() if n]
-    mods += [("vae." + n if n else "vae", m) for n, m in be.es_model.vae.named_modules()]
-    order = []
+    flat, m = info["flat_ids"], info["m"]
+    j_of = torch.tensor([info["pid_to_j"][p] for p in flat], device=dev).repeat(pop)
+    caps = {}
+    hooks = []
+    for name, mod in be.es_model.transformer.named_modules():
+        if isinstance(mod, LoRALinear) and name.startswith(("transformer_blocks.0.", "transformer_blocks.19.")):
+            hooks.append(mod.register_forward_hook(lambda _m, _i, o, n=name: caps.setdefault(n, []).append(digest(o))))
+    be.es_model.transformer.register_forward_hook(lambda _m, _i, o: caps.setdefault("transformer", []).append(digest(o)))
 
-    def run(val):
+    def one():
+        caps.clear()
+        with torch.no_grad():
+            fac = noiser.epoch_noise(pop, seed=seed)
+            tp = noiser.perturb(theta, fac, pop, 0, pop, out=engine.theta_pop[:pop])
+            feats = rewards.prompt_features(info["unique_texts"])
+            imgs = be.generate_population(flat, seed, gs, tp)
+            rw = rewards.score(imgs, j_of, feats)
+            S = aggregate_member_rewards(rw, flat, info["pid_to_j"], pop, m)[0]
+        torch.cuda.synchronize()
+        return {"caps": {k: list(v) for k, v in caps.items()}, "img": digest(imgs), "S": digest(S),
+                "S_rows": [digest(S[k]) for k in range(pop)], "img_per_member": [digest(imgs[k * len(flat):(k + 1) * len(flat)]) for k in range(pop)],
+                "feats": {k: digest(v) for k, v in feats.items()}}
+
+    ref = one()
+    res = []
+    for pat in (0x00, 0xFF, 0x7F, 0x00, 0xFF):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        poison(val)
-        outs = {}
-        def hook(_m, _i, o, n):
-            if n not in outs:
-                order.append(n)
-            outs.setdefault(n, []).append(o.detach().clone() if torch.is_tensor(o) else None)
-        hooks = [m.register_forward_hook(lambda _m, _i, o, n=n: hook(_m, _i, o, n)) for n, m in mods]
-        try:
-            fac = nz.sample_factors(a.pop, dev, seed=seed)
-            tp = nz.perturb(theta, fac, a.pop, 0, a.pop)
-            imgs = be.generate_population(info["flat_ids"], seed, gs, tp)
-            j = torch.tensor([info["pid_to_j"][p] for p in info["flat_ids"]], device=dev).repeat(a.pop)
-            comb = eng.rewards.score(imgs, j, eng.rewards.prompt_features(info["unique_texts"]))["combined"]
-            torch.cuda.synchronize()
-        finally:
-            for h in hooks:
-                h.remove()
-            torch.empty, torch.empty_like = _orig["empty"], _orig["empty_like"]
-            torch.Tensor.new_empty = _orig_new_empty
-        return outs, tp.clone(), imgs.clone(), comb.clone()
-
-    A = run(0.0)
-    order_a = list(dict.fromkeys(order))
-    B = run(float("nan"))
-    C = run(1e4)
-    res = {"tp_equal": [bool(torch.equal(A[1], X[1])) for X in (B, C)],
-           "images_equal": [bool(torch.equal(A[2], X[2])) for X in (B, C)],
-           "rewards_equal": [bool(torch.equal(A[3], X[3])) for X in (B, C)],
-           "images_nan": bool(torch.isnan(B[2]).any()), "first": []}
-    for n in order_a:
-        for X, tag in ((B, "nan"), (C, "1e4")):
-            for ci, (x, y) in enumerate(zip(A[0].get(n, []), X[0].get(n, []))):
-                if x is not None and y is not None and not torch.equal(x, y):
-                    res["first"].append({"module": n, "call": ci, "poison": tag, "nan": bool(torch.isnan(y).any()),
-                                         "max_abs": float((x.float() - y.float()).abs().nan_to_num(1e30).max())})
-                    break
-        if len(res["first"]) >= 8:
-            break
-    print(json.dumps(res))
+        free = torch.cuda.mem_get_info(dev)[0]
+        n = min(int(gib) << 30, free - (8 << 30))
+        big = torch.empty(n, dtype=torch.uint8, device=dev)
+        big.fill_(pat)
+        del big       # stays in the caching allocator: the next allocations are split from it
+        r = one()
+        d = {"pattern": hex(pat), "filled_GiB": round(n / 2 ** 30, 1), "S_equal": r["S"] == ref["S"],
+             "img_equal": r["img"] == ref["img"], "feats_equal": r["feats"] == ref["feats"],
+             "rows_differ": [k for k in range(pop) if r["S_rows"][k] != ref["S_rows"][k]],
+             "img_members_differ": [k for k in range(pop) if r["img_per_member"][k] != ref["img_per_member"][k]],
+             "caps_differ": sorted(k for k in ref["caps"] if r["caps"].get(k) != ref["caps"][k])[:20]}
+        res.append(d)
+        print(json.dumps(d), flush=True)
+    out = ROOT / "gpurun_out" / "uninit_probe.json"
+    out.parent.mkdir(exist_ok=True)
+    out.write_text(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main()
+    main(float(sys.argv[1]) if len(sys.argv) > 1 else 150)
