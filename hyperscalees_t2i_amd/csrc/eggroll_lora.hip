@@ -2476,6 +2476,9 @@ struct SubpixArgs {
     int H, W, Cin, Cout;
 };
 
+#ifndef EGG_SPX_REGS  // VGPRs of shortcut words in flight per batch in the sub-pixel epilogue (A/B knob)
+#define EGG_SPX_REGS 64
+#endif
 // KP: the wave's phase (wave-uniform, dispatched by the caller) — a compile-time shortcut channel index
 template <int SP, int REP, int KP>
 __device__ __forceinline__ void store_tile_subpix(f32x4 (&acc)[8][4], char* smem, int wave, int lane, int rbase,
@@ -2483,7 +2486,9 @@ __device__ __forceinline__ void store_tile_subpix(f32x4 (&acc)[8][4], char* smem
     constexpr int ROWB = 128, SLOTS = 8;
     constexpr int XW = 32 / REP;                     // shortcut channels spanned by 8 outputs
     constexpr int WD = SP == 2 ? XW : XW / 2;        // their dwords (raw, converted at use)
-    constexpr int RBAT = WD >= 16 ? 64 / WD : 8;     // rows whose shortcut loads are in flight together (<= 64 VGPRs)
+    // rows whose shortcut loads are in flight together (<= EGG_SPX_REGS VGPRs of raw shortcut words)
+    constexpr int RBAT_ = EGG_SPX_REGS / WD > 16 ? 16 : (EGG_SPX_REGS / WD > 0 ? EGG_SPX_REGS / WD : 1);
+    constexpr int RBAT = 16 % RBAT_ == 0 ? RBAT_ : 8;
     char* ctile = smem + wave * (128 * ROWB);
     {
         const int r_l = lane & 15, c_l = (lane >> 4) * 4;
@@ -2520,14 +2525,14 @@ __device__ __forceinline__ void store_tile_subpix(f32x4 (&acc)[8][4], char* smem
 #pragma unroll
     for (int it0 = 0; it0 < 16; it0 += RBAT) {
         uint32_t raw[RBAT][WD];
-        int64_t opix[RBAT];
+        int32_t opix[RBAT];   // B * 4 * H * W * Cout < 2^31 (host check): pixel and element offsets fit 32 bits
         bool ok[RBAT];
 #pragma unroll
         for (int u = 0; u < RBAT; ++u) {
             const int h = hp - pi, w = wp - pj;
             ok[u] = p < Mp && h >= 0 && h < H && w >= 0 && w < W;
             const int64_t lp = ok[u] ? ((int64_t)bb * H + h) * W + w : 0;
-            opix[u] = ((int64_t)bb * 2 * H + 2 * h + pi) * (2 * W) + 2 * w + pj;
+            opix[u] = (bb * 2 * H + 2 * h + pi) * (2 * W) + 2 * w + pj;
             // window of channels (4c + k) / REP, c = c0 .. c0+7: XW channels from 4 c0 / REP
             const uint32_t* src = reinterpret_cast<const uint32_t*>(
                 reinterpret_cast<const char*>(sp.src) + (lp * sp.Cin + 4 * c0 / REP) * (SP == 2 ? 4 : 2));
@@ -2558,7 +2563,7 @@ __device__ __forceinline__ void store_tile_subpix(f32x4 (&acc)[8][4], char* smem
                                           : bf16_to_f32((unsigned short)(raw[u][ch >> 1] >> (16 * (ch & 1))));
                 f[q] = bf16_to_f32(v[q]) + bv[q] + xsv;
             }
-            const int64_t oo = opix[u] * sp.Cout + c0;
+            const int32_t oo = opix[u] * sp.Cout + c0;
             if constexpr (SP == 2) {
                 float* o32 = reinterpret_cast<float*>(sp.out) + oo;
                 *reinterpret_cast<f32x4*>(o32) = f32x4{f[0], f[1], f[2], f[3]};

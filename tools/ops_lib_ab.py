@@ -58,6 +58,23 @@ def cases(dev, g):
         qf, kf, vf = (r(Bf, Nf, Hf, 128, sc=0.5) for _ in range(3))
         out[f"flash_attention {Bf}x{Nf} h{Hf}"] = (lambda qf=qf, kf=kf, vf=vf:
             K.flash_attention(qf, kf, vf, 128 ** -0.5))
+    # DC-AE up-blocks: 2x2 phase conv + sub-pixel interleave + bias + shortcut in one launch (the four product
+    # shapes, 8 images; the 512->1024 one also on the fp32 stream with its bf16 shadow)
+    from hyperscalees_t2i_amd.dcae import subpixel_phase_weights
+    for Hs, Cin, Cout, f32 in ((512, 256, 128, False), (256, 512, 256, False), (128, 512, 512, False),
+                               (64, 1024, 512, False), (64, 1024, 512, True)):
+        xs = r(8, Hs, Hs, Cin, sc=0.5)
+        w4 = subpixel_phase_weights(torch.randn(Cout, Cin, 3, 3, device=dev, generator=g) / (9 * Cin) ** 0.5)
+        w4p = K.pack_conv3x3_weight(w4.to(torch.bfloat16).contiguous(memory_format=torch.channels_last), 1)
+        bs = r(Cout, sc=0.1)
+        if f32:
+            src = r(8, Hs, Hs, Cin, dt=torch.float32)
+            sh = torch.empty(8, 2 * Hs, 2 * Hs, Cout, device=dev, dtype=torch.bfloat16)
+            out[f"conv2x2_subpixel f32 8x{Hs}^2 {Cin}->{Cout}"] = (lambda xs=xs, w4p=w4p, src=src, bs=bs, sh=sh:
+                torch.cat([K.conv2x2_subpixel(xs, w4p, src, bias=bs, shadow=sh).flatten(), sh.float().flatten()]))
+        else:
+            out[f"conv2x2_subpixel 8x{Hs}^2 {Cin}->{Cout}"] = (lambda xs=xs, w4p=w4p, bs=bs:
+                K.conv2x2_subpixel(xs, w4p, xs, bias=bs))
     h0 = r(16 * 257, 1280, dt=torch.float32)
     h = h0.clone()
     y, w2, b2 = r(16 * 257, 1280), r(1280, sc=0.5), r(1280, sc=0.1)
