@@ -37,7 +37,12 @@ __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcp
 constexpr int DW_CS = 32;  // channels per plane per block (64 B per pixel: adjacent blocks share lines)
 constexpr int DW_TW = 32;  // output columns per block
 constexpr int DW_TH = 8;   // output rows per block
-constexpr int DW_ORDER_AUTO = 0;  // block order of kernel 0 (eggroll_dwconv_nhwc_sel: 1 = order 0, 2 = order 1)
+constexpr int DW_ORDER_AUTO = 0;
+#ifndef EGG_DW5_DOT2  // 5x5 taps on v_dot2_f32_bf16 (1) or bf16 -> fp32 conversions + fp32 FMAs (0, the default):
+// the dot2 form issues 100 instead of ~150 VALU per output row but measured SLOWER — 385 -> 412 us at
+// 8 x 128^2 x 1536, 203 -> 222 at 8 x 64^2 x 3072 (profiles/r14b_dw5_dot2_ab.log; numerics within 1 bf16 ulp)
+#define EGG_DW5_DOT2 0
+#endif  // block order of kernel 0 (eggroll_dwconv_nhwc_sel: 1 = order 0, 2 = order 1)
 
 typedef __attribute__((ext_vector_type(4))) unsigned short u16x4m;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2m;
@@ -176,15 +181,24 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
     float res[DW_TH][4];  // value-plane results, gated by the second plane (GLU)
 #pragma unroll 1
     for (int pl = 0; pl < PLANES; ++pl) {
-        float w[KS * KS][4], bs[4];
+        // DOT2 (5x5, EGG_DW5_DOT2): weights kept as bf16 pairs (w, 0) / (0, w) for v_dot2_f32_bf16 against the
+        // raw bf16 channel pairs of a tap — no per-tap bf16 -> fp32 conversions (the 5x5 form's VALU bound)
+        constexpr bool DOT2 = KS == 5 && EGG_DW5_DOT2;
+        float w[DOT2 ? 1 : KS * KS][4], bs[4];
+        uint32_t wd[DOT2 ? KS * KS : 1][4];
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(wt + pl * Cout), (short)0, (int)(KS * KS * cin2), 0x00020000);
 #pragma unroll
         for (int t = 0; t < KS * KS; ++t) {
             const u16x4m wv = __builtin_bit_cast(u16x4m, __builtin_amdgcn_raw_buffer_load_b64(rw, (uint32_t)cq * 2,
                                                                                             t * (int)cin2, 0));
+            if constexpr (DOT2) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) w[t][i] = b2f(wv[i]);
+                for (int i = 0; i < 4; ++i) wd[t][i] = (i & 1) ? ((uint32_t)wv[i] << 16) : (uint32_t)wv[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[t][i] = b2f(wv[i]);
+            }
         }
         if (bias) {
             const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(bias + pl * Cout), (short)0,
@@ -267,10 +281,24 @@ __global__ __launch_bounds__(256) void k_dwconv_nhwc(const unsigned short* __res
                 for (int dy = 0; dy < KS; ++dy)
 #pragma unroll
                     for (int dx = 0; dx < KS; ++dx) {
-                        float tap[4];
-                        rd(pl, oy + dy, xs + dx, tap);
+                        if constexpr (DOT2) {
+                            typedef __attribute__((ext_vector_type(2))) __bf16 dw_bf2;
+                            const u32x2m v = *reinterpret_cast<const u32x2m*>(
+                                lds + ((pl * TR + oy + dy) * TC + xs + dx) * PIXB + q * 8);
+                            // (the dwords through a plain array: hipcc miscompiles __builtin_bit_cast of an
+                            // ext-vector subscript v[i >> 1] into element 0 for every i)
+                            const uint32_t xw[2] = {v.x, v.y};
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) acc[i] += tap[i] * w[dy * KS + dx][i];
+                            for (int i = 0; i < 4; ++i)
+                                acc[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(dw_bf2, xw[i >> 1]),
+                                                                         __builtin_bit_cast(dw_bf2, wd[dy * KS + dx][i]),
+                                                                         acc[i], false);
+                        } else {
+                            float tap[4];
+                            rd(pl, oy + dy, xs + dx, tap);
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) acc[i] += tap[i] * w[dy * KS + dx][i];
+                        }
                     }
                 emit(oy, acc);
             }

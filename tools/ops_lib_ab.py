@@ -75,6 +75,12 @@ def cases(dev, g):
         else:
             out[f"conv2x2_subpixel 8x{Hs}^2 {Cin}->{Cout}"] = (lambda xs=xs, w4p=w4p, bs=bs:
                 K.conv2x2_subpixel(xs, w4p, xs, bias=bs))
+    # DC-AE multi-scale branch: 5x5 depthwise + grouped 1x1 (the three product shapes)
+    for Hd, Cd in ((128, 1536), (64, 3072), (32, 3072)):
+        xd = r(8, Hd, Hd, Cd, sc=0.5)
+        wd = r(25, Cd, sc=0.2)
+        pwd = r(Cd // 32, 32, 32, sc=1 / 6)
+        out[f"~dwconv_pw5 8x{Hd}^2x{Cd}"] = lambda xd=xd, wd=wd, pwd=pwd: K.dwconv_pw_nhwc(xd, wd, pwd, 5)
     h0 = r(16 * 257, 1280, dt=torch.float32)
     h = h0.clone()
     y, w2, b2 = r(16 * 257, 1280), r(1280, sc=0.5), r(1280, sc=0.1)
@@ -107,8 +113,11 @@ def main(paths, rounds=7, only=None):
                 us[i].append(timed(fn))
         res[name] = {"bitwise_equal_to_A": same, **{Path(p).name: round(statistics.median(u), 1)
                                                      for p, u in zip(paths, us)}}
+        if name.startswith("~"):   # a numerics-changing A/B: report the largest relative difference instead
+            res[name]["max_rel_diff_to_A"] = [float((o.float() - outs[0].float()).abs().max() /
+                                                    outs[0].float().abs().max().clamp_min(1e-30)) for o in outs[1:]]
         print(json.dumps({name: res[name]}), flush=True)
-        assert all(same), name
+        assert all(same) or name.startswith("~"), name
     print(json.dumps(res))
 
 
