@@ -28,7 +28,7 @@ def cases(dev, g):
     xb = r(131072, 2240)
     wb = r(2240, sc=0.5)
     out["rms bf16 131072x2240 +w"] = lambda: K.rownorm(xb, 1e-6, w=wb)
-    for C, rows in ((512, 8 * 256 * 256), (1024, 8 * 128 * 128)):
+    for C, rows in ((512, 8 * 256 * 256), (512, 8 * 128 * 128), (1024, 8 * 128 * 128)):
         xc, wc, bc = r(rows, C), r(C, sc=0.5), r(C, sc=0.1)
         res0 = r(rows, C, dt=torch.float32)
         res = res0.clone()
@@ -37,6 +37,11 @@ def cases(dev, g):
             res.copy_(res0)
             return K.rownorm(xc, 1e-5, w=wc, b=bc, res=res)
         out[f"dcae rms+res32 {rows}x{C}"] = f
+        o32, sh = torch.empty_like(res0), torch.empty(rows, C, device=dev, dtype=torch.bfloat16)
+
+        def f2(xc=xc, wc=wc, bc=bc, res0=res0, o32=o32, sh=sh):   # the product form, out of place (no copy timed)
+            return K.rownorm(xc, 1e-5, w=wc, b=bc, res=res0, out=o32, shadow=sh)
+        out[f"dcae rms+res32+shadow {rows}x{C}"] = f2
     # linear attention: Sana attn1 (separate q / k / v [B*N, 2240], 70 heads) and DC-AE planar [Q|K|V]
     qs, ks, vs = r(128 * 1024, 2240), r(128 * 1024, 2240), r(128 * 1024, 2240)
     out["linear_attention sana 128x1024 h70"] = lambda: K.linear_attention(qs, ks, vs, 128, 1024, 70, 32, False)
